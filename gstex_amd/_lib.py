@@ -1,0 +1,142 @@
+"""ctypes binding of libgstex_hip.so (the C-ABI declared in include/gstex_hip.h).
+
+The shared library is built in-tree (``make -C gstex_amd/csrc`` or ``__graft_entry__.build()``).
+There is no fallback: if the library is missing every op raises, so a GPU run can never silently
+fall back to a CPU path.  ``torch`` must be imported before the library is loaded so that the HIP
+runtime torch ships (soname libamdhip64.so.7) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_void_p, c_char_p
+
+import torch  # noqa: F401  (load torch's HIP runtime first)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
+
+REC_FLOATS = 32
+PARTIAL_FLOATS = 24
+SETTING_AA_BLUR = 1 << 9
+SETTING_DIST_REG = 1 << 10
+SETTING_EDIT = 1 << 13
+SETTING_EVAL_NORMAL = 1 << 15
+
+
+class GstexCamera(ctypes.Structure):
+    _fields_ = [
+        ("viewmat", c_void_p),
+        ("c2w", c_void_p),
+        ("fx", c_float),
+        ("fy", c_float),
+        ("cx", c_float),
+        ("cy", c_float),
+        ("H", c_int32),
+        ("W", c_int32),
+        ("block", c_int32),
+    ]
+
+
+_P = c_void_p
+_CAM = POINTER(GstexCamera)
+
+# name -> (restype, argtypes); must mirror include/gstex_hip.h
+SIGNATURES = {
+    "gstex_last_error": (c_char_p, []),
+    "gstex_abi_version": (c_int32, []),
+    "gstex_project_points": (c_int32, [c_int32, _P, _CAM, _P, _P, _P]),
+    "gstex_project_points_bwd": (c_int32, [c_int32, _P, _CAM, _P, _P, _P, _P]),
+    "gstex_aabb_2d": (c_int32, [c_int32, _P, _P, c_float, _P, _CAM, _P, _P, _P]),
+    "gstex_aabb_2d_bwd": (c_int32, [c_int32, _P, _P, c_float, _P, _CAM, _P, _P, _P, _P, _P]),
+    "gstex_num_tiles_hit": (c_int32, [c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P]),
+    "gstex_scan_workspace_size": (c_size_t, [c_int32]),
+    "gstex_scan_offsets": (c_int32, [c_int32, _P, _P, _P, c_size_t, _P]),
+    "gstex_bin_workspace_size": (c_size_t, [c_int32, c_int64, c_int32]),
+    "gstex_bin_sort": (
+        c_int32,
+        [c_int32, c_int64, _P, _P, _P, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, c_size_t, _P],
+    ),
+    "gstex_raster_setup": (
+        c_int32,
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
+    ),
+    "gstex_raster_fwd": (
+        c_int32,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "gstex_raster_bwd": (
+        c_int32,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "gstex_raster_setup_bwd": (
+        c_int32,
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "gstex_sh_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
+    "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
+    "gstex_texture_sample": (c_int32, [c_int64, c_int32, _P, _P, c_int64, _P, _P, _P]),
+    "gstex_texture_sample_bwd": (c_int32, [c_int64, c_int32, _P, c_int64, _P, _P, _P, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class GstexError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and return the C-ABI library; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise GstexError(
+                    f"{path} is missing: build it with `make -C gstex_amd/csrc` "
+                    "(or `python -c 'import __graft_entry__ as g; g.build()'`). "
+                    "gstex_amd has no CPU fallback."
+                )
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    msg = load().gstex_last_error()
+    return msg.decode() if msg else ""
+
+
+def call(name: str, *args) -> None:
+    """Call a status-returning entry point; raise GstexError with the library's message."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise GstexError(f"{name} failed (status {rc}): {last_error()}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None / empty)."""
+    if t is None:
+        return None
+    if t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def make_camera(viewmat, c2w, fx, fy, cx, cy, H, W, block) -> GstexCamera:
+    """viewmat: device fp32 (3,4) contiguous; c2w: device fp32 (4,4) contiguous or None."""
+    return GstexCamera(
+        ptr(viewmat), ptr(c2w) if c2w is not None else None,
+        float(fx), float(fy), float(cx), float(cy), int(H), int(W), int(block),
+    )

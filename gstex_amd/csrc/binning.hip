@@ -1,0 +1,347 @@
+// binning.hip — tile binning and per-tile depth sort (the sort that happens inside the reference's
+// texture_gaussians, args at nerfstudio/models/gstex.py:1136-1139,1158).
+//
+// Output order is the gsplat-0.1 lineage order: per tile, splats ascending by (depth float bits,
+// splat id) — what a stable radix sort of (tile << 32 | depth_bits) over gid-major emitted pairs
+// produces.  The MI355X design does not run a 64-bit global radix sort; instead:
+//   1. count:  per splat, one returning atomic per covered tile gives the pair its rank in the
+//              tile bucket (order inside a bucket is arbitrary at this point);
+//   2. scan:   exclusive scan of the per-tile counts -> tile ranges;
+//   3. place:  each pair writes its 64-bit key (depth_bits << 32 | id) to start[tile] + rank;
+//   4. sort:   one workgroup per tile sorts its bucket in LDS (bitonic, power-of-two padded);
+//              buckets larger than the LDS capacity are chunk-sorted in LDS and merged in global
+//              memory with merge-path by the same workgroup.
+// Keys are unique (id is part of the key), so any correct sort yields the same, bit-exact order.
+#include "gstex_common.h"
+#include "gstex_error.h"
+
+using namespace gstex;
+
+namespace {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanThreads * kScanItems;
+constexpr int kSortThreads = 256;
+constexpr int kSortCap = 4096;  // keys per LDS sort (32 KiB)
+
+// Inclusive wave64 scan.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// Exclusive scan of one 256-thread block's per-thread totals; returns the block total in *total.
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = wave_incl_scan(v);
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    int wave_off = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        int s = s_wave[w];
+        if (w < wave) wave_off += s;
+        sum += s;
+    }
+    __syncthreads();
+    *total = sum;
+    return wave_off + incl - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_partials_kernel(int n, const int32_t* __restrict__ in,
+                                                                     int32_t* __restrict__ block_sums) {
+    __shared__ int s_wave[kScanThreads / 64];
+    int base = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) v += (base + k < n) ? in[base + k] : 0;
+    int total;
+    block_excl_scan(v, s_wave, &total);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+}
+
+// Single block: exclusive scan of the block sums in place.
+__global__ __launch_bounds__(kScanThreads) void scan_block_sums_kernel(int nb, int32_t* __restrict__ sums) {
+    __shared__ int s_wave[kScanThreads / 64];
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += kScanThreads) {
+        int i = b0 + threadIdx.x;
+        int v = (i < nb) ? sums[i] : 0;
+        int total;
+        int ex = block_excl_scan(v, s_wave, &total);
+        if (i < nb) sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_final_kernel(int n, const int32_t* __restrict__ in,
+                                                                  const int32_t* __restrict__ block_offs,
+                                                                  int32_t* __restrict__ out) {
+    __shared__ int s_wave[kScanThreads / 64];
+    int base = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    int vals[kScanItems];
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        vals[k] = (base + k < n) ? in[base + k] : 0;
+        v += vals[k];
+    }
+    int total;
+    int ex = block_excl_scan(v, s_wave, &total) + block_offs[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        if (base + k < n) out[base + k] = ex;
+        ex += vals[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = ex;
+}
+
+int run_scan(int n, const int32_t* in, int32_t* out, int32_t* block_sums, hipStream_t st) {
+    int nb = div_up(n, kScanTile);
+    if (nb == 0) {
+        (void)hipMemsetAsync(out, 0, sizeof(int32_t), st);
+        return launch_status("scan(empty)");
+    }
+    scan_partials_kernel<<<nb, kScanThreads, 0, st>>>(n, in, block_sums);
+    scan_block_sums_kernel<<<1, kScanThreads, 0, st>>>(nb, block_sums);
+    scan_final_kernel<<<nb, kScanThreads, 0, st>>>(n, in, block_sums, out);
+    return launch_status("scan");
+}
+
+size_t scan_ws_bytes(int n) { return (size_t)(div_up(n, kScanTile) + 1) * sizeof(int32_t); }
+
+// 1. count + rank
+__global__ __launch_bounds__(256) void count_kernel(int n, const float* __restrict__ centers,
+                                                    const float* __restrict__ extents,
+                                                    const int32_t* __restrict__ offsets, int tiles_x,
+                                                    int tiles_y, int block, int32_t* __restrict__ tile_count,
+                                                    int32_t* __restrict__ rank) {
+    int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
+                       tiles_y, block);
+    int e = offsets[g];
+    for (int ty = r.y0; ty < r.y1; ++ty)
+        for (int tx = r.x0; tx < r.x1; ++tx) rank[e++] = atomicAdd(&tile_count[ty * tiles_x + tx], 1);
+}
+
+// 3. place keys
+__global__ __launch_bounds__(256) void place_kernel(int n, const float* __restrict__ centers,
+                                                    const float* __restrict__ extents,
+                                                    const float* __restrict__ depths,
+                                                    const int32_t* __restrict__ offsets, int tiles_x,
+                                                    int tiles_y, int block,
+                                                    const int32_t* __restrict__ tile_start,
+                                                    const int32_t* __restrict__ rank,
+                                                    unsigned long long* __restrict__ keys) {
+    int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
+                       tiles_y, block);
+    const unsigned long long key =
+        ((unsigned long long)__float_as_uint(depths[g]) << 32) | (unsigned long long)(unsigned)g;
+    int e = offsets[g];
+    for (int ty = r.y0; ty < r.y1; ++ty)
+        for (int tx = r.x0; tx < r.x1; ++tx) {
+            int t = ty * tiles_x + tx;
+            keys[tile_start[t] + rank[e++]] = key;
+        }
+}
+
+__device__ __forceinline__ void bitonic_lds(unsigned long long* s, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < (P >> 1); p += kSortThreads) {
+                int i = 2 * p - (p & (j - 1));
+                int ixj = i + j;
+                unsigned long long a = s[i], b = s[ixj];
+                bool up = ((i & k) == 0);
+                if ((a > b) == up) {
+                    s[i] = b;
+                    s[ixj] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ void write_sorted(int t, int tiles_x, int block, int pos, unsigned long long key,
+                                             const float* centers, const float* extents,
+                                             const int32_t* offsets, int tiles_y, int32_t* sorted_ids,
+                                             int32_t* sorted_slots) {
+    int g = (int)(unsigned)(key & 0xffffffffull);
+    sorted_ids[pos] = g;
+    Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
+                       tiles_y, block);
+    int tx = t % tiles_x, ty = t / tiles_x;
+    sorted_slots[pos] = offsets[g] + (ty - r.y0) * (r.x1 - r.x0) + (tx - r.x0);
+}
+
+// 4. one workgroup per tile
+__global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
+    int n_tiles, int tiles_x, int tiles_y, int block, const int32_t* __restrict__ tile_start,
+    unsigned long long* __restrict__ keys, unsigned long long* __restrict__ scratch,
+    const float* __restrict__ centers, const float* __restrict__ extents,
+    const int32_t* __restrict__ offsets, int32_t* __restrict__ tile_ranges, int32_t* __restrict__ sorted_ids,
+    int32_t* __restrict__ sorted_slots) {
+    __shared__ unsigned long long s_keys[kSortCap];
+    const int t = blockIdx.x;
+    const int start = tile_start[t], end = tile_start[t + 1];
+    const int K = end - start;
+    if (threadIdx.x == 0) {
+        tile_ranges[2 * t] = start;
+        tile_ranges[2 * t + 1] = end;
+    }
+    if (K == 0) return;
+    unsigned long long* src = keys + start;
+    if (K <= kSortCap) {
+        int P = 1;
+        while (P < K) P <<= 1;
+        for (int i = threadIdx.x; i < P; i += kSortThreads) s_keys[i] = (i < K) ? src[i] : ~0ull;
+        __syncthreads();
+        bitonic_lds(s_keys, P);
+        for (int i = threadIdx.x; i < K; i += kSortThreads)
+            write_sorted(t, tiles_x, block, start + i, s_keys[i], centers, extents, offsets, tiles_y, sorted_ids,
+                         sorted_slots);
+        return;
+    }
+    // Large bucket: sort kSortCap-sized chunks in LDS, then merge-path passes in global memory.
+    for (int c0 = 0; c0 < K; c0 += kSortCap) {
+        int len = min(kSortCap, K - c0);
+        int P = 1;
+        while (P < len) P <<= 1;
+        for (int i = threadIdx.x; i < P; i += kSortThreads) s_keys[i] = (i < len) ? src[c0 + i] : ~0ull;
+        __syncthreads();
+        bitonic_lds(s_keys, P);
+        for (int i = threadIdx.x; i < len; i += kSortThreads) src[c0 + i] = s_keys[i];
+        __syncthreads();
+    }
+    unsigned long long* a_buf = src;
+    unsigned long long* b_buf = scratch + start;
+    for (int L = kSortCap; L < K; L <<= 1) {
+        for (int pb = 0; pb < K; pb += 2 * L) {
+            const int a0 = pb, a1 = min(pb + L, K), b1 = min(pb + 2 * L, K);
+            const int la = a1 - a0, lb = b1 - a1, total = la + lb;
+            const unsigned long long* A = a_buf + a0;
+            const unsigned long long* B = a_buf + a1;
+            unsigned long long* O = b_buf + a0;
+            const int per = (total + kSortThreads - 1) / kSortThreads;
+            int diag = min((int)threadIdx.x * per, total);
+            int dend = min(diag + per, total);
+            int lo = max(0, diag - lb), hi = min(diag, la);
+            while (lo < hi) {
+                int mid = (lo + hi) >> 1;
+                if (A[mid] < B[diag - 1 - mid]) lo = mid + 1;
+                else hi = mid;
+            }
+            int i = lo, j = diag - lo;
+            for (int o = diag; o < dend; ++o) {
+                bool take_a = (j >= lb) || (i < la && A[i] < B[j]);
+                O[o] = take_a ? A[i++] : B[j++];
+            }
+        }
+        __syncthreads();
+        unsigned long long* tmp = a_buf;
+        a_buf = b_buf;
+        b_buf = tmp;
+    }
+    for (int i = threadIdx.x; i < K; i += kSortThreads)
+        write_sorted(t, tiles_x, block, start + i, a_buf[i], centers, extents, offsets, tiles_y, sorted_ids,
+                     sorted_slots);
+}
+
+struct BinWorkspace {
+    int32_t* tile_count;   // n_tiles + 1 (scan output reused as tile_start)
+    int32_t* tile_start;   // n_tiles + 1
+    int32_t* scan_ws;      // scan block sums
+    int32_t* rank;         // n_isect
+    unsigned long long* keys;     // n_isect
+    unsigned long long* scratch;  // n_isect
+};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t bin_layout(int n_tiles, int64_t n_isect, char* base, BinWorkspace* ws) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* p = base ? base + off : nullptr;
+        off += align256(bytes);
+        return p;
+    };
+    char* p0 = take((size_t)(n_tiles + 1) * 4);
+    char* p1 = take((size_t)(n_tiles + 1) * 4);
+    char* p2 = take(scan_ws_bytes(n_tiles + 1));
+    char* p3 = take((size_t)n_isect * 4);
+    char* p4 = take((size_t)n_isect * 8);
+    char* p5 = take((size_t)n_isect * 8);
+    if (ws) {
+        ws->tile_count = (int32_t*)p0;
+        ws->tile_start = (int32_t*)p1;
+        ws->scan_ws = (int32_t*)p2;
+        ws->rank = (int32_t*)p3;
+        ws->keys = (unsigned long long*)p4;
+        ws->scratch = (unsigned long long*)p5;
+    }
+    return off;
+}
+
+}  // namespace
+
+extern "C" size_t gstex_scan_workspace_size(int32_t n) { return scan_ws_bytes(n < 0 ? 0 : n); }
+
+extern "C" int gstex_scan_offsets(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && offsets, "gstex_scan_offsets: invalid arguments");
+    GSTEX_REQUIRE(n == 0 || num_tiles_hit, "gstex_scan_offsets: null input");
+    GSTEX_REQUIRE(workspace_bytes >= scan_ws_bytes(n) && workspace, "gstex_scan_offsets: workspace too small");
+    return run_scan(n, num_tiles_hit, offsets, (int32_t*)workspace, as_stream(stream));
+}
+
+extern "C" size_t gstex_bin_workspace_size(int32_t n, int64_t n_isect, int32_t n_tiles) {
+    (void)n;
+    return bin_layout(n_tiles, n_isect, nullptr, nullptr);
+}
+
+extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float* extents,
+                              const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                              int32_t H, int32_t W, int32_t block, int32_t* tile_ranges, int32_t* sorted_ids,
+                              int32_t* sorted_slots, void* workspace, size_t workspace_bytes, void* stream) {
+    (void)num_tiles_hit;
+    GSTEX_REQUIRE(n >= 0 && n_isect >= 0 && n_isect < (1ll << 31) && H > 0 && W > 0 && block > 0,
+                  "gstex_bin_sort: invalid sizes (n=%d, n_isect=%lld, H=%d, W=%d, block=%d)", n,
+                  (long long)n_isect, H, W, block);
+    GSTEX_REQUIRE(block == kTile, "gstex_bin_sort: block_width must be %d (got %d)", kTile, block);
+    const int tiles_x = (W + block - 1) / block, tiles_y = (H + block - 1) / block;
+    const int n_tiles = tiles_x * tiles_y;
+    GSTEX_REQUIRE(tile_ranges, "gstex_bin_sort: null tile_ranges");
+    size_t need = bin_layout(n_tiles, n_isect, nullptr, nullptr);
+    GSTEX_REQUIRE(workspace && workspace_bytes >= need, "gstex_bin_sort: workspace too small (%zu < %zu)",
+                  workspace_bytes, need);
+    hipStream_t st = as_stream(stream);
+    if (n_isect == 0) {
+        (void)hipMemsetAsync(tile_ranges, 0, (size_t)n_tiles * 2 * sizeof(int32_t), st);
+        return launch_status("gstex_bin_sort(empty)");
+    }
+    GSTEX_REQUIRE(centers && extents && depths && offsets && sorted_ids && sorted_slots,
+                  "gstex_bin_sort: null pointer");
+    BinWorkspace ws;
+    bin_layout(n_tiles, n_isect, (char*)workspace, &ws);
+    (void)hipMemsetAsync(ws.tile_count, 0, (size_t)(n_tiles + 1) * sizeof(int32_t), st);
+    count_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, offsets, tiles_x, tiles_y, block,
+                                                  ws.tile_count, ws.rank);
+    int rc = run_scan(n_tiles, ws.tile_count, ws.tile_start, ws.scan_ws, st);
+    if (rc) return rc;
+    place_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, depths, offsets, tiles_x, tiles_y, block,
+                                                  ws.tile_start, ws.rank, ws.keys);
+    tile_sort_kernel<<<n_tiles, kSortThreads, 0, st>>>(n_tiles, tiles_x, tiles_y, block, ws.tile_start, ws.keys,
+                                                       ws.scratch, centers, extents, offsets, tile_ranges,
+                                                       sorted_ids, sorted_slots);
+    return launch_status("gstex_bin_sort");
+}

@@ -1,0 +1,331 @@
+// gstex_common.h — device math shared by every gfx950 kernel of libgstex_hip.so.
+//
+// The fp32 operation ORDER in this file is part of the numerical contract: oracle/raster.py
+// restates each function below op-for-op (the library is compiled with -ffp-contract=off, so no
+// fused multiply-adds are formed), which is what makes the threshold decisions of the composite
+// (alpha >= 1/255, T < 1e-4, z >= near) agree between the GPU and the CPU oracle.
+//
+// Semantics follow the call-site contracts of the reference (nerfstudio/models/gstex.py) and the
+// 2DGS formulation its argument list implies.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gstex_hip.h"
+
+namespace gstex {
+
+constexpr int kTile = 16;               // BLOCK_WIDTH, gstex.py:1075
+constexpr int kTilePixels = kTile * kTile;
+constexpr float kCutoff2 = 9.0f;        // 3-sigma AABB cutoff (2DGS compute_aabb)
+constexpr float kMinExtent = 2.1213180f;// cutoff * FilterSize (3 * 0.707106)
+constexpr float kNear = 0.2f;           // 2DGS near_n
+constexpr float kFarRatio = 100.0f / 99.8f;  // far_n / (far_n - near_n), rounded to fp32 once
+constexpr float kAlphaMax = 0.99f;
+constexpr float kAlphaMin = 1.0f / 255.0f;
+constexpr float kTMin = 1e-4f;
+constexpr float kFilterInvSq = 2.0f;    // 2DGS FilterInvSquare
+constexpr float kProjClip = 0.01f;      // project_points near clip (gsplat-0.1 clip_thresh)
+
+// Kernel argument form of gstex_camera (device pointers + scalars).
+struct CamArgs {
+    const float* viewmat;
+    const float* c2w;
+    float fx, fy, cx, cy;
+    int H, W, block;
+};
+
+__host__ inline CamArgs to_device_camera(const gstex_camera& c) {
+    CamArgs d;
+    d.viewmat = c.viewmat; d.c2w = c.c2w;
+    d.fx = c.fx; d.fy = c.fy; d.cx = c.cx; d.cy = c.cy;
+    d.H = c.H; d.W = c.W; d.block = c.block;
+    return d;
+}
+
+// In-kernel camera: the 12 view-matrix words are wave-uniform loads (scalar cache).
+struct Camera {
+    float V[12];
+    float campos[3];
+    float fx, fy, cx, cy;
+    int H, W, block;
+};
+
+__device__ __forceinline__ Camera load_camera(const CamArgs& a) {
+    Camera c;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) c.V[i] = a.viewmat[i];
+    if (a.c2w) {
+        c.campos[0] = a.c2w[3]; c.campos[1] = a.c2w[7]; c.campos[2] = a.c2w[11];
+    } else {  // -R^T t
+        c.campos[0] = -((c.V[0] * c.V[3] + c.V[4] * c.V[7]) + c.V[8] * c.V[11]);
+        c.campos[1] = -((c.V[1] * c.V[3] + c.V[5] * c.V[7]) + c.V[9] * c.V[11]);
+        c.campos[2] = -((c.V[2] * c.V[3] + c.V[6] * c.V[7]) + c.V[10] * c.V[11]);
+    }
+    c.fx = a.fx; c.fy = a.fy; c.cx = a.cx; c.cy = a.cy;
+    c.H = a.H; c.W = a.W; c.block = a.block;
+    return c;
+}
+
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ f3 cross3(f3 a, f3 b) {
+    return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ f3 scale3(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 add3(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+
+// Normalised wxyz quaternion -> rotation columns (t_u, t_v, t_w).  Matches
+// nerfstudio/utils/rotations.py:43-72 on unit quaternions (wxyz, real part first).
+struct Frame { f3 tu, tv, tw; float qw, qx, qy, qz, qnorm; };
+
+__device__ __forceinline__ Frame quat_frame(const float* q4) {
+    Frame f;
+    float w = q4[0], x = q4[1], y = q4[2], z = q4[3];
+    float nrm = sqrtf(((w * w + x * x) + y * y) + z * z);
+    w = w / nrm; x = x / nrm; y = y / nrm; z = z / nrm;
+    f.qw = w; f.qx = x; f.qy = y; f.qz = z; f.qnorm = nrm;
+    float r00 = 1.0f - 2.0f * (y * y + z * z);
+    float r01 = 2.0f * (x * y - w * z);
+    float r02 = 2.0f * (x * z + w * y);
+    float r10 = 2.0f * (x * y + w * z);
+    float r11 = 1.0f - 2.0f * (x * x + z * z);
+    float r12 = 2.0f * (y * z - w * x);
+    float r20 = 2.0f * (x * z - w * y);
+    float r21 = 2.0f * (y * z + w * x);
+    float r22 = 1.0f - 2.0f * (x * x + y * y);
+    f.tu = f3{r00, r10, r20};
+    f.tv = f3{r01, r11, r21};
+    f.tw = f3{r02, r12, r22};
+    return f;
+}
+
+// Row r of the 3x3 rotation part of the view matrix applied to a vector.
+__device__ __forceinline__ float vrow(const Camera& c, int r, f3 a) {
+    return (c.V[4 * r + 0] * a.x + c.V[4 * r + 1] * a.y) + c.V[4 * r + 2] * a.z;
+}
+
+// Splat -> pixel homogeneous matrix M = K [R|t] [[su t_u, sv t_v, mu],[0,0,1]] (rows Tu,Tv,Tw).
+struct Homog { f3 Tu, Tv, Tw; };
+
+__device__ __forceinline__ Homog splat_homography(const Camera& c, f3 mu, float su, float sv,
+                                                  const Frame& fr) {
+    f3 a = scale3(fr.tu, su);
+    f3 b = scale3(fr.tv, sv);
+    float W0[3], W1[3], W2[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        W0[r] = vrow(c, r, a);
+        W1[r] = vrow(c, r, b);
+        W2[r] = vrow(c, r, mu) + c.V[4 * r + 3];
+    }
+    Homog h;
+    h.Tu = f3{c.fx * W0[0] + c.cx * W0[2], c.fx * W1[0] + c.cx * W1[2], c.fx * W2[0] + c.cx * W2[2]};
+    h.Tv = f3{c.fy * W0[1] + c.cy * W0[2], c.fy * W1[1] + c.cy * W1[2], c.fy * W2[1] + c.cy * W2[2]};
+    h.Tw = f3{W0[2], W1[2], W2[2]};
+    return h;
+}
+
+// dL/dM -> dL/d(mu, su, sv, t_u, t_v)
+struct HomogGrad { f3 dmu; float dsu, dsv; f3 dtu, dtv; };
+
+__device__ __forceinline__ HomogGrad splat_homography_vjp(const Camera& c, float su, float sv,
+                                                          const Frame& fr, f3 dTu, f3 dTv,
+                                                          f3 dTw) {
+    // W rows: dW[0,:] = fx dTu, dW[1,:] = fy dTv, dW[2,:] = cx dTu + cy dTv + dTw
+    f3 dW0r = scale3(dTu, c.fx);
+    f3 dW1r = scale3(dTv, c.fy);
+    f3 dW2r = add3(add3(scale3(dTu, c.cx), scale3(dTv, c.cy)), dTw);
+    // columns of dW: col k = (dW0r[k], dW1r[k], dW2r[k]); d(vec) = R_cw^T col
+    auto rt = [&](float e0, float e1, float e2) {
+        return f3{(c.V[0] * e0 + c.V[4] * e1) + c.V[8] * e2, (c.V[1] * e0 + c.V[5] * e1) + c.V[9] * e2,
+                  (c.V[2] * e0 + c.V[6] * e1) + c.V[10] * e2};
+    };
+    f3 da = rt(dW0r.x, dW1r.x, dW2r.x);
+    f3 db = rt(dW0r.y, dW1r.y, dW2r.y);
+    HomogGrad g;
+    g.dmu = rt(dW0r.z, dW1r.z, dW2r.z);
+    g.dsu = dot3(fr.tu, da);
+    g.dsv = dot3(fr.tv, db);
+    g.dtu = scale3(da, su);
+    g.dtv = scale3(db, sv);
+    return g;
+}
+
+// Anchored form of the same homography, used by the rasterizer.  With the anchor (xa, ya) = the
+// projection of the splat centre, k = px*Tw - Tu is evaluated as (px - xa)*Tw - (Tu - xa*Tw): the
+// z-component of Tu - xa*Tw is exactly 0 and nothing of size |px*Tw| is ever cancelled, which is
+// what keeps the fp32 forward and especially the backward (means / quats gradients) accurate.
+//   Tu' = Tu - xa Tw = fx (W0[0] - xn W0[2], W1[0] - xn W1[2], 0),   xn = W2[0] / W2[2]
+//   Tv' = Tv - ya Tw = fy (W0[1] - yn W0[2], W1[1] - yn W1[2], 0),   yn = W2[1] / W2[2]
+//   xa = fx xn + cx,  ya = fy yn + cy
+struct Anchored { f3 Tu, Tv, Tw; float xn, yn, xa, ya; };
+
+__device__ __forceinline__ Anchored splat_anchored(const Camera& c, f3 mu, float su, float sv,
+                                                   const Frame& fr) {
+    f3 a = scale3(fr.tu, su);
+    f3 b = scale3(fr.tv, sv);
+    float W0[3], W1[3], W2[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        W0[r] = vrow(c, r, a);
+        W1[r] = vrow(c, r, b);
+        W2[r] = vrow(c, r, mu) + c.V[4 * r + 3];
+    }
+    Anchored h;
+    h.xn = W2[0] / W2[2];
+    h.yn = W2[1] / W2[2];
+    h.Tu = f3{c.fx * (W0[0] - h.xn * W0[2]), c.fx * (W1[0] - h.xn * W1[2]), 0.0f};
+    h.Tv = f3{c.fy * (W0[1] - h.yn * W0[2]), c.fy * (W1[1] - h.yn * W1[2]), 0.0f};
+    h.Tw = f3{W0[2], W1[2], W2[2]};
+    h.xa = c.fx * h.xn + c.cx;
+    h.ya = c.fy * h.yn + c.cy;
+    return h;
+}
+
+// Gradient of the anchored form w.r.t. (mu, su, sv, t_u, t_v), treating the anchor as a constant
+// (k and l do not depend on it).  A = dL/dTu, B = dL/dTv, Pw = dL/dTw accumulated with the
+// anchored pixel offsets:  dW[0,:] = fx A,  dW[1,:] = fy B,  dW[2,:] = Pw - xn dW[0,:] - yn dW[1,:].
+__device__ __forceinline__ HomogGrad splat_anchored_vjp(const Camera& c, float su, float sv,
+                                                        const Frame& fr, float xn, float yn, f3 A,
+                                                        f3 B, f3 Pw) {
+    f3 dW0r = scale3(A, c.fx);
+    f3 dW1r = scale3(B, c.fy);
+    f3 dW2r = f3{(Pw.x - xn * dW0r.x) - yn * dW1r.x, (Pw.y - xn * dW0r.y) - yn * dW1r.y,
+                 (Pw.z - xn * dW0r.z) - yn * dW1r.z};
+    auto rt = [&](float e0, float e1, float e2) {
+        return f3{(c.V[0] * e0 + c.V[4] * e1) + c.V[8] * e2, (c.V[1] * e0 + c.V[5] * e1) + c.V[9] * e2,
+                  (c.V[2] * e0 + c.V[6] * e1) + c.V[10] * e2};
+    };
+    f3 da = rt(dW0r.x, dW1r.x, dW2r.x);
+    f3 db = rt(dW0r.y, dW1r.y, dW2r.y);
+    HomogGrad g;
+    g.dmu = rt(dW0r.z, dW1r.z, dW2r.z);
+    g.dsu = dot3(fr.tu, da);
+    g.dsv = dot3(fr.tv, db);
+    g.dtu = scale3(da, su);
+    g.dtv = scale3(db, sv);
+    return g;
+}
+
+// dL/d(rotation columns) -> dL/d(raw quaternion), through the normalisation.
+__device__ __forceinline__ void frame_vjp(const Frame& f, f3 dtu, f3 dtv, f3 dtw, float* dq) {
+    const float w = f.qw, x = f.qx, y = f.qy, z = f.qz;
+    // R[r][c]: column c = (tu, tv, tw)[c], row r = component
+    const float d00 = dtu.x, d10 = dtu.y, d20 = dtu.z;
+    const float d01 = dtv.x, d11 = dtv.y, d21 = dtv.z;
+    const float d02 = dtw.x, d12 = dtw.y, d22 = dtw.z;
+    float gw = 2.0f * (-z * d01 + y * d02 + z * d10 - x * d12 - y * d20 + x * d21);
+    float gx = 2.0f * (y * d01 + z * d02 + y * d10 - 2.0f * x * d11 - w * d12 + z * d20 + w * d21 -
+                       2.0f * x * d22);
+    float gy = 2.0f * (-2.0f * y * d00 + x * d01 + w * d02 + x * d10 + z * d12 - w * d20 + z * d21 -
+                       2.0f * y * d22);
+    float gz = 2.0f * (-2.0f * z * d00 - w * d01 + x * d02 + w * d10 - 2.0f * z * d11 + y * d12 +
+                       x * d20 + y * d21);
+    float proj = ((w * gw + x * gx) + y * gy) + z * gz;
+    float inv = 1.0f / f.qnorm;
+    dq[0] = (gw - w * proj) * inv;
+    dq[1] = (gx - x * proj) * inv;
+    dq[2] = (gy - y * proj) * inv;
+    dq[3] = (gz - z * proj) * inv;
+}
+
+// 2DGS compute_aabb (3-sigma disc) -> screen centre + per-axis half extent.  Returns false when
+// the splat must be culled (centre at/behind the near plane, or the disc crosses the camera
+// plane: d >= 0).
+__device__ __forceinline__ bool aabb_from_homog(const Homog& h, float& cxo, float& cyo,
+                                                float& exo, float& eyo) {
+    const f3 Tu = h.Tu, Tv = h.Tv, Tw = h.Tw;
+    if (!(Tw.z > kNear)) return false;
+    float d = (kCutoff2 * (Tw.x * Tw.x) + kCutoff2 * (Tw.y * Tw.y)) - Tw.z * Tw.z;
+    if (!(d < 0.0f)) return false;
+    float fxy = kCutoff2 / d;
+    float fz = -1.0f / d;
+    float px = (fxy * (Tu.x * Tw.x) + fxy * (Tu.y * Tw.y)) + fz * (Tu.z * Tw.z);
+    float py = (fxy * (Tv.x * Tw.x) + fxy * (Tv.y * Tw.y)) + fz * (Tv.z * Tw.z);
+    float qx = (fxy * (Tu.x * Tu.x) + fxy * (Tu.y * Tu.y)) + fz * (Tu.z * Tu.z);
+    float qy = (fxy * (Tv.x * Tv.x) + fxy * (Tv.y * Tv.y)) + fz * (Tv.z * Tv.z);
+    float hx = px * px - qx;
+    float hy = py * py - qy;
+    float ex = sqrtf(fmaxf(1e-4f, hx));
+    float ey = sqrtf(fmaxf(1e-4f, hy));
+    cxo = px; cyo = py;
+    exo = fmaxf(ex, kMinExtent);
+    eyo = fmaxf(ey, kMinExtent);
+    return true;
+}
+
+// Tile rectangle [x0,x1) x [y0,y1) in tile units (gsplat-0.1 get_tile_bbox convention).
+struct Rect { int x0, x1, y0, y1; };
+
+__device__ __forceinline__ Rect tile_rect(float cx, float cy, float ex, float ey, int tiles_x,
+                                          int tiles_y, int block) {
+    Rect r{0, 0, 0, 0};
+    if (!(ex > 0.0f) || !(ey > 0.0f)) return r;
+    const float b = (float)block;
+    float tcx = cx / b, tcy = cy / b, trx = ex / b, try_ = ey / b;
+    r.x0 = (int)fminf(fmaxf(tcx - trx, 0.0f), (float)tiles_x);
+    r.x1 = (int)fminf(fmaxf(tcx + trx + 1.0f, 0.0f), (float)tiles_x);
+    r.y0 = (int)fminf(fmaxf(tcy - try_, 0.0f), (float)tiles_y);
+    r.y1 = (int)fminf(fmaxf(tcy + try_ + 1.0f, 0.0f), (float)tiles_y);
+    if (r.x1 < r.x0) r.x1 = r.x0;
+    if (r.y1 < r.y0) r.y1 = r.y0;
+    return r;
+}
+
+// Raster record layout (GSTEX_REC_FLOATS = 32 floats = 128 B, one cache line).
+enum RecField {
+    R_TU = 0, R_TV = 3, R_TW = 6, R_XY = 9, R_OPAC = 11, R_RGB = 12, R_NRM = 15,
+    R_TU0 = 18, R_AUU = 19, R_AUV = 20, R_TV0 = 21, R_AVU = 22, R_AVV = 23,
+    R_H = 24, R_W = 25, R_OFF = 26, R_GID = 27, R_XA = 28, R_YA = 29
+};
+
+// Partial layout (GSTEX_PARTIAL_FLOATS = 24).
+enum PartField {
+    P_TU = 0, P_TV = 3, P_TW = 6, P_XY = 9, P_OPAC = 11, P_RGB = 12, P_NRM = 15,
+    P_TU0 = 18, P_AUU = 19, P_AUV = 20, P_TV0 = 21, P_AVU = 22, P_AVV = 23
+};
+
+// Bilinear lookup into one splat's h x w texel block (corner-aligned: texel (i,j) sits at uv
+// (i/h, j/w), matching texture_dims_to_query, jagged_texture.py:23-34; clamp to edge).
+struct Bilerp { int i0, i1, j0, j1; float ax, ay; bool in_u, in_v; };
+
+__device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w) {
+    Bilerp b;
+    const float hf = (float)h, wf = (float)w;
+    float xr = tu * hf, yr = tv * wf;
+    float x = fminf(fmaxf(xr, 0.0f), hf - 1.0f);
+    float y = fminf(fmaxf(yr, 0.0f), wf - 1.0f);
+    b.in_u = (xr > 0.0f) && (xr < hf - 1.0f);
+    b.in_v = (yr > 0.0f) && (yr < wf - 1.0f);
+    b.i0 = (int)x; b.j0 = (int)y;
+    b.i1 = min(b.i0 + 1, h - 1);
+    b.j1 = min(b.j0 + 1, w - 1);
+    b.ax = x - (float)b.i0;
+    b.ay = y - (float)b.j0;
+    return b;
+}
+
+__device__ __forceinline__ float bilerp_mix(float v00, float v01, float v10, float v11, float ax,
+                                            float ay) {
+    float top = (1.0f - ay) * v00 + ay * v01;
+    float bot = (1.0f - ay) * v10 + ay * v11;
+    return (1.0f - ax) * top + ax * bot;
+}
+
+// Bijective XCD-aware block remap: the hardware deals blocks round-robin over the 8 XCDs, so
+// blocks b and b+8 share an L2. Give each XCD a contiguous run of tiles so that neighbouring
+// tiles (which share splats and texels) hit the same L2.
+__device__ __forceinline__ int xcd_swizzle(int bid, int nblocks) {
+    const int nx = 8;
+    int q = nblocks / nx, r = nblocks % nx;
+    int xcd = bid % nx, k = bid / nx;
+    // XCD x owns tiles [start(x), start(x) + q + (x < r)).
+    int start = xcd * q + min(xcd, r);
+    return start + k;
+}
+
+}  // namespace gstex

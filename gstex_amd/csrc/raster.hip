@@ -1,0 +1,682 @@
+// raster.hip — forward / backward alpha-composite of per-primitive-textured 2D Gaussian splats.
+//
+// Replaces gstex_cuda.texture.texture_gaussians (forward at nerfstudio/models/gstex.py:1133-1162,
+// backward through autograd at engine/trainer.py:460).  Semantics: SURVEY.md Appendix A and the
+// comments of gstex_common.h; the CPU restatement is oracle/raster.py.
+//
+// MI355X layout:
+//   * one 256-thread workgroup (4 wave64) per 16x16 tile, blockIdx -> tile remapped so that each
+//     XCD owns a contiguous band of tiles (neighbouring tiles share splats and texels in its L2);
+//   * splat records are 128-B AoS lines gathered once per batch into LDS as [field][splat] float4
+//     planes (conflict-free writes, broadcast reads);
+//   * forward early-out per wave (ballot) and per workgroup (__syncthreads_count);
+//   * backward: reverse traversal, per-splat gradient partials reduced across the wave with a
+//     reduce-scatter butterfly (30 shuffles for 24 values instead of 144), combined across the 4
+//     waves in LDS in a fixed order and written with plain stores to a per-(tile,splat) slot —
+//     no float atomics for splat gradients, bitwise reproducible; texel gradients use hardware
+//     fp32 atomics (global_atomic_add_f32).
+#include "gstex_common.h"
+#include "gstex_error.h"
+
+using namespace gstex;
+
+namespace {
+
+constexpr int kThreads = kTilePixels;  // 256
+constexpr int kFwdBatch = 256;
+constexpr int kBwdBatch = 64;
+constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
+constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
+
+// ------------------------------------------------------------------------------------------
+// setup: per-splat record
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restrict__ means,
+                                                    const float* __restrict__ scales, float glob,
+                                                    const float* __restrict__ quats,
+                                                    const float* __restrict__ rgbs,
+                                                    const float* __restrict__ opacities,
+                                                    const float* __restrict__ centers,
+                                                    const float* __restrict__ uv0,
+                                                    const float* __restrict__ umap,
+                                                    const float* __restrict__ vmap,
+                                                    const int32_t* __restrict__ tdims,
+                                                    const int32_t* __restrict__ nth, CamArgs cam_args,
+                                                    float* __restrict__ rec_out) {
+    const Camera cam = load_camera(cam_args);
+    int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    if (nth[g] <= 0) return;
+    Frame fr = quat_frame(quats + 4 * g);
+    float su = scales[3 * g] * glob, sv = scales[3 * g + 1] * glob;
+    f3 mu = mk3(means[3 * g], means[3 * g + 1], means[3 * g + 2]);
+    Anchored h = splat_anchored(cam, mu, su, sv, fr);
+    f3 dir = f3{cam.campos[0] - mu.x, cam.campos[1] - mu.y, cam.campos[2] - mu.z};
+    float sgn = dot3(fr.tw, dir) < 0.0f ? -1.0f : 1.0f;
+    f3 um = mk3(umap[3 * g], umap[3 * g + 1], umap[3 * g + 2]);
+    f3 vm = mk3(vmap[3 * g], vmap[3 * g + 1], vmap[3 * g + 2]);
+    float r[GSTEX_REC_FLOATS];
+    r[R_TU + 0] = h.Tu.x; r[R_TU + 1] = h.Tu.y; r[R_TU + 2] = h.Tu.z;
+    r[R_TV + 0] = h.Tv.x; r[R_TV + 1] = h.Tv.y; r[R_TV + 2] = h.Tv.z;
+    r[R_TW + 0] = h.Tw.x; r[R_TW + 1] = h.Tw.y; r[R_TW + 2] = h.Tw.z;
+    r[R_XY + 0] = centers[2 * g]; r[R_XY + 1] = centers[2 * g + 1];
+    r[R_OPAC] = opacities[g];
+    r[R_RGB + 0] = rgbs[3 * g]; r[R_RGB + 1] = rgbs[3 * g + 1]; r[R_RGB + 2] = rgbs[3 * g + 2];
+    r[R_NRM + 0] = sgn * fr.tw.x; r[R_NRM + 1] = sgn * fr.tw.y; r[R_NRM + 2] = sgn * fr.tw.z;
+    r[R_TU0] = uv0[2 * g];
+    r[R_AUU] = su * dot3(fr.tu, um);
+    r[R_AUV] = sv * dot3(fr.tv, um);
+    r[R_TV0] = uv0[2 * g + 1];
+    r[R_AVU] = su * dot3(fr.tu, vm);
+    r[R_AVV] = sv * dot3(fr.tv, vm);
+    r[R_H] = __int_as_float(tdims[3 * g]);
+    r[R_W] = __int_as_float(tdims[3 * g + 1]);
+    r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
+    r[R_GID] = __int_as_float(g);
+    r[R_XA] = h.xa;
+    r[R_YA] = h.ya;
+    r[30] = r[31] = 0.0f;
+    float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
+#pragma unroll
+    for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// shared per-(pixel, splat) evaluation
+// ------------------------------------------------------------------------------------------
+struct Rec {
+    f3 Tu, Tv, Tw;
+    float x, y, opac;
+    float rgb[3], nrm[3];
+    float tu0, auu, auv, tv0, avu, avv;
+    int h, w, off;
+    float xa, ya;
+};
+
+template <int NB>
+__device__ __forceinline__ Rec read_rec(const float4* s, int j) {
+    float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], d = s[3 * NB + j];
+    float4 e = s[4 * NB + j], f = s[5 * NB + j], g = s[6 * NB + j], q = s[7 * NB + j];
+    Rec r;
+    r.Tu = f3{a.x, a.y, a.z};
+    r.Tv = f3{a.w, b.x, b.y};
+    r.Tw = f3{b.z, b.w, c.x};
+    r.x = c.y; r.y = c.z; r.opac = c.w;
+    r.rgb[0] = d.x; r.rgb[1] = d.y; r.rgb[2] = d.z;
+    r.nrm[0] = d.w; r.nrm[1] = e.x; r.nrm[2] = e.y;
+    r.tu0 = e.z; r.auu = e.w; r.auv = f.x; r.tv0 = f.y; r.avu = f.z; r.avv = f.w;
+    r.h = __float_as_int(g.x); r.w = __float_as_int(g.y); r.off = __float_as_int(g.z);
+    r.xa = q.x; r.ya = q.y;
+    return r;
+}
+
+struct Hit {
+    float dx, dy, u, v, rho3, rho2, z, G, a_raw, alpha;
+    f3 k, l, p;
+    bool use3;
+};
+
+// Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
+__device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool aa, Hit& h) {
+    h.dx = px - r.xa;
+    h.dy = py - r.ya;
+    h.k = f3{h.dx * r.Tw.x - r.Tu.x, h.dx * r.Tw.y - r.Tu.y, h.dx * r.Tw.z};
+    h.l = f3{h.dy * r.Tw.x - r.Tv.x, h.dy * r.Tw.y - r.Tv.y, h.dy * r.Tw.z};
+    h.p = cross3(h.k, h.l);
+    if (h.p.z == 0.0f) return false;
+    h.u = h.p.x / h.p.z;
+    h.v = h.p.y / h.p.z;
+    h.rho3 = h.u * h.u + h.v * h.v;
+    float dx = r.x - px, dy = r.y - py;
+    h.rho2 = kFilterInvSq * (dx * dx + dy * dy);
+    h.use3 = !aa || (h.rho3 <= h.rho2);
+    float rho = h.use3 ? h.rho3 : h.rho2;
+    h.z = h.use3 ? (h.u * r.Tw.x + h.v * r.Tw.y) + r.Tw.z : r.Tw.z;
+    if (h.z < kNear) return false;
+    h.G = expf(-0.5f * rho);
+    h.a_raw = r.opac * h.G;
+    h.alpha = fminf(kAlphaMax, h.a_raw);
+    return h.alpha >= kAlphaMin;
+}
+
+__device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float& tu, float& tv) {
+    tu = r.tu0 + (u * r.auu + v * r.auv);
+    tv = r.tv0 + (u * r.avu + v * r.avv);
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
+    CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
+    const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
+    const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float* __restrict__ out_img,
+    float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
+    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state) {
+    const Camera cam = load_camera(cam_args);
+    constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
+    const int Cn = (C > 0) ? C : Cdyn;
+    __shared__ float4 s_rec[kRecF4 * kFwdBatch];
+    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int tid = threadIdx.x;
+    const int pxi = tx * kTile + (tid & 15), pyi = ty * kTile + (tid >> 4);
+    const bool inside = pxi < cam.W && pyi < cam.H;
+    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
+    const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
+    const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
+    const int2 rng = tile_ranges[tile];
+    const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
+
+    float T = 1.0f;
+    float img[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 0.f};
+    float tex[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) tex[c] = 0.f;
+    float D = 0.f, M1 = 0.f, M2 = 0.f, reg = 0.f;
+    int last = -1;
+    bool done = !inside;
+
+    for (int b0 = rng.x; b0 < rng.y; b0 += kFwdBatch) {
+        if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
+        const int idx = b0 + tid;
+        if (idx < rng.y) {
+            const float4* src = records + (size_t)sorted_ids[idx] * kRecF4;
+#pragma unroll
+            for (int k = 0; k < kRecF4; ++k) s_rec[k * kFwdBatch + tid] = src[k];
+        }
+        __syncthreads();
+        const int nb = min(kFwdBatch, rng.y - b0);
+        for (int j = 0; j < nb; ++j) {
+            if (done) break;
+            const Rec r = read_rec<kFwdBatch>(s_rec, j);
+            Hit h;
+            if (!eval_hit(r, px, py, aa, h)) continue;
+            const float test_T = T * (1.0f - h.alpha);
+            if (test_T < kTMin) {
+                done = true;
+                break;
+            }
+            const float w = h.alpha * T;
+            if (r.h * r.w > 0) {
+                float tu, tv;
+                tex_coords(r, h.u, h.v, tu, tv);
+                const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
+                const size_t o00 = (size_t)(r.off + b.i0 * r.w + b.j0) * Cn;
+                const size_t o01 = (size_t)(r.off + b.i0 * r.w + b.j1) * Cn;
+                const size_t o10 = (size_t)(r.off + b.i1 * r.w + b.j0) * Cn;
+                const size_t o11 = (size_t)(r.off + b.i1 * r.w + b.j1) * Cn;
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c < Cn) {
+                        float val = bilerp_mix(texture[o00 + c], texture[o01 + c], texture[o10 + c],
+                                               texture[o11 + c], b.ax, b.ay);
+                        tex[c] = tex[c] + val * w;
+                    }
+                }
+            }
+            img[0] = img[0] + r.rgb[0] * w;
+            img[1] = img[1] + r.rgb[1] * w;
+            img[2] = img[2] + r.rgb[2] * w;
+            D = D + h.z * w;
+            nrm[0] = nrm[0] + r.nrm[0] * w;
+            nrm[1] = nrm[1] + r.nrm[1] * w;
+            nrm[2] = nrm[2] + r.nrm[2] * w;
+            if (dreg) {
+                const float A = 1.0f - T;
+                const float m = kFarRatio * (1.0f - kNear / h.z);
+                reg = reg + ((m * m * A + M2) - 2.0f * m * M1) * w;
+                M1 = M1 + m * w;
+                M2 = M2 + m * m * w;
+            }
+            T = test_T;
+            last = b0 - rng.x + j;
+        }
+    }
+    if (!inside) return;
+    const size_t pix = (size_t)pyi * cam.W + pxi;
+    out_img[3 * pix + 0] = img[0] + T * bg0;
+    out_img[3 * pix + 1] = img[1] + T * bg1;
+    out_img[3 * pix + 2] = img[2] + T * bg2;
+    out_depth[pix] = D;
+    out_reg[pix] = reg;
+    out_alpha[pix] = 1.0f - T;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+        if (c < Cn) out_tex[(size_t)Cn * pix + c] = tex[c];
+    out_normal[3 * pix + 0] = nrm[0];
+    out_normal[3 * pix + 1] = nrm[1];
+    out_normal[3 * pix + 2] = nrm[2];
+    state[pix] = make_float4(T, M1, M2, __int_as_float(last));
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+// Reduce-scatter butterfly over the 64 lanes: on return, lane l with (l & 7) == 0 holds the wave
+// sums of values [12*b5 + 6*b4 + 3*b3 + 0..2] (b5,b4,b3 = bits 5,4,3 of l) in v[0..2].
+__device__ __forceinline__ void wave_reduce24(float (&v)[kNP]) {
+    const int lane = threadIdx.x & 63;
+    {
+        const bool hi = lane & 32;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            float send = hi ? v[i] : v[i + 12];
+            float keep = hi ? v[i + 12] : v[i];
+            v[i] = keep + __shfl_xor(send, 32, 64);
+        }
+    }
+    {
+        const bool hi = lane & 16;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            float send = hi ? v[i] : v[i + 6];
+            float keep = hi ? v[i + 6] : v[i];
+            v[i] = keep + __shfl_xor(send, 16, 64);
+        }
+    }
+    {
+        const bool hi = lane & 8;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            float send = hi ? v[i] : v[i + 3];
+            float keep = hi ? v[i + 3] : v[i];
+            v[i] = keep + __shfl_xor(send, 8, 64);
+        }
+    }
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[i] = v[i] + __shfl_xor(v[i], o, 64);
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
+    CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
+    const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
+    const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots,
+    const float* __restrict__ texture, const float4* __restrict__ state, const float* __restrict__ v_img,
+    const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
+    const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
+    float* __restrict__ v_texture) {
+    const Camera cam = load_camera(cam_args);
+    constexpr int CM = (C > 0) ? C : 8;
+    const int Cn = (C > 0) ? C : Cdyn;
+    __shared__ float4 s_rec[kRecF4 * kBwdBatch];
+    __shared__ float s_part[kBwdBatch][4][kNP];
+    __shared__ int s_slot[kBwdBatch];
+    __shared__ int s_maxlast;
+
+    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pxi = tx * kTile + (tid & 15), pyi = ty * kTile + (tid >> 4);
+    const bool inside = pxi < cam.W && pyi < cam.H;
+    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
+    const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
+    const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
+    const int2 rng = tile_ranges[tile];
+    const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
+
+    float T = 1.0f, M1f = 0.f, M2f = 0.f;
+    int last = -1;
+    float Gimg[3] = {0.f, 0.f, 0.f}, Gn[3] = {0.f, 0.f, 0.f}, Gtex[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) Gtex[c] = 0.f;
+    float Gd = 0.f, Greg = 0.f, Ga = 0.f;
+    if (inside) {
+        const size_t pix = (size_t)pyi * cam.W + pxi;
+        const float4 st = state[pix];
+        T = st.x; M1f = st.y; M2f = st.z; last = __float_as_int(st.w);
+        Gimg[0] = v_img[3 * pix]; Gimg[1] = v_img[3 * pix + 1]; Gimg[2] = v_img[3 * pix + 2];
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < Cn) Gtex[c] = v_tex[(size_t)Cn * pix + c];
+        Gd = v_depth[pix];
+        Greg = dreg ? v_reg[pix] : 0.f;
+        Ga = v_alpha[pix];
+        Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2];
+    }
+    const float Af = 1.0f - T;
+    float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
+
+    if (tid == 0) s_maxlast = -1;
+    __syncthreads();
+    if (last >= 0) atomicMax(&s_maxlast, last);
+    __syncthreads();
+    const int tile_last = s_maxlast;
+    const int count = rng.y - rng.x;
+
+    // pairs after the last contributor of the tile receive zero gradient
+    for (int p = rng.x + tile_last + 1 + tid; p < rng.y; p += kThreads) {
+        float4* dst = reinterpret_cast<float4*>(partials + (size_t)sorted_slots[p] * kNP);
+#pragma unroll
+        for (int k = 0; k < kNP / 4; ++k) dst[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    (void)count;
+
+    for (int bb = tile_last / kBwdBatch; bb >= 0 && tile_last >= 0; --bb) {
+        const int b0 = rng.x + bb * kBwdBatch;
+        const int nb = min(kBwdBatch, tile_last - bb * kBwdBatch + 1);
+        for (int q = tid; q < kBwdBatch * kRecF4; q += kThreads) {
+            const int j = q >> 3, k = q & 7;
+            if (j < nb) s_rec[k * kBwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+        }
+        if (tid < nb) s_slot[tid] = sorted_slots[b0 + tid];
+        __syncthreads();
+
+        for (int j = nb - 1; j >= 0; --j) {
+            const int rel = bb * kBwdBatch + j;
+            float P[kNP];
+#pragma unroll
+            for (int i = 0; i < kNP; ++i) P[i] = 0.f;
+            bool contrib = false;
+            if (rel <= last) {
+                const Rec r = read_rec<kBwdBatch>(s_rec, j);
+                Hit h;
+                if (eval_hit(r, px, py, aa, h)) {
+                    contrib = true;
+                    const float one_m = 1.0f - h.alpha;
+                    T = T / one_m;
+                    const float w = h.alpha * T;
+                    // texture value and its uv-gradient
+                    float tau[CM];
+                    float dtu = 0.f, dtv = 0.f, tu = 0.f, tv = 0.f;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) tau[c] = 0.f;
+                    const bool has_tex = r.h * r.w > 0;
+                    Bilerp b;
+                    size_t o00 = 0, o01 = 0, o10 = 0, o11 = 0;
+                    if (has_tex) {
+                        tex_coords(r, h.u, h.v, tu, tv);
+                        b = bilerp_coords(tu, tv, r.h, r.w);
+                        o00 = (size_t)(r.off + b.i0 * r.w + b.j0) * Cn;
+                        o01 = (size_t)(r.off + b.i0 * r.w + b.j1) * Cn;
+                        o10 = (size_t)(r.off + b.i1 * r.w + b.j0) * Cn;
+                        o11 = (size_t)(r.off + b.i1 * r.w + b.j1) * Cn;
+                        const float hf = (float)r.h, wf = (float)r.w;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) {
+                            if (c < Cn) {
+                                const float v00 = texture[o00 + c], v01 = texture[o01 + c];
+                                const float v10 = texture[o10 + c], v11 = texture[o11 + c];
+                                tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay);
+                                const float gt = w * Gtex[c];
+                                if (b.in_u)
+                                    dtu += gt * (hf * ((1.0f - b.ay) * (v10 - v00) + b.ay * (v11 - v01)));
+                                if (b.in_v)
+                                    dtv += gt * (wf * ((1.0f - b.ax) * (v01 - v00) + b.ax * (v11 - v10)));
+                            }
+                        }
+                    }
+                    const float m = kFarRatio * (1.0f - kNear / h.z);
+                    const float E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
+                    float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
+#pragma unroll
+                    for (int c = 0; c < CM; ++c)
+                        if (c < Cn) g += Gtex[c] * tau[c];
+                    g += Gd * h.z;
+                    g += (Gn[0] * r.nrm[0] + Gn[1] * r.nrm[1]) + Gn[2] * r.nrm[2];
+                    g += Ga;
+                    g += Greg * E;
+                    const float dL_dalpha = T * (g - R);
+                    R = h.alpha * g + one_m * R;
+
+                    P[P_RGB + 0] = w * Gimg[0];
+                    P[P_RGB + 1] = w * Gimg[1];
+                    P[P_RGB + 2] = w * Gimg[2];
+                    P[P_NRM + 0] = w * Gn[0];
+                    P[P_NRM + 1] = w * Gn[1];
+                    P[P_NRM + 2] = w * Gn[2];
+                    // texel gradients (bilinear scatter)
+                    if (has_tex) {
+                        const float w00 = (1.0f - b.ax) * (1.0f - b.ay), w01 = (1.0f - b.ax) * b.ay;
+                        const float w10 = b.ax * (1.0f - b.ay), w11 = b.ax * b.ay;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) {
+                            if (c < Cn) {
+                                const float gt = w * Gtex[c];
+                                atomicAdd(v_texture + o00 + c, gt * w00);
+                                atomicAdd(v_texture + o01 + c, gt * w01);
+                                atomicAdd(v_texture + o10 + c, gt * w10);
+                                atomicAdd(v_texture + o11 + c, gt * w11);
+                            }
+                        }
+                    }
+                    // depth: direct + distortion (m depends on z)
+                    float dz = w * Gd;
+                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * (kFarRatio * kNear / (h.z * h.z));
+                    float drho = 0.f;
+                    if (h.a_raw < kAlphaMax) {
+                        P[P_OPAC] = dL_dalpha * h.G;
+                        drho = dL_dalpha * h.a_raw * -0.5f;
+                    }
+                    // texture coordinates
+                    P[P_TU0] = dtu; P[P_AUU] = dtu * h.u; P[P_AUV] = dtu * h.v;
+                    P[P_TV0] = dtv; P[P_AVU] = dtv * h.u; P[P_AVV] = dtv * h.v;
+                    float du = dtu * r.auu + dtv * r.avu;
+                    float dv = dtu * r.auv + dtv * r.avv;
+                    f3 dTw = f3{0.f, 0.f, 0.f};
+                    if (h.use3) {
+                        du += drho * 2.0f * h.u + dz * r.Tw.x;
+                        dv += drho * 2.0f * h.v + dz * r.Tw.y;
+                        dTw = f3{dz * h.u, dz * h.v, dz};
+                    } else {
+                        P[P_XY + 0] = drho * (2.0f * kFilterInvSq) * (r.x - px);
+                        P[P_XY + 1] = drho * (2.0f * kFilterInvSq) * (r.y - py);
+                        dTw.z = dz;
+                    }
+                    const float ipz = 1.0f / h.p.z;
+                    const f3 dp = f3{du * ipz, dv * ipz, -(du * h.u + dv * h.v) * ipz};
+                    const f3 dk = cross3(h.l, dp);
+                    const f3 dl = cross3(dp, h.k);
+                    P[P_TU + 0] = -dk.x; P[P_TU + 1] = -dk.y; P[P_TU + 2] = -dk.z;
+                    P[P_TV + 0] = -dl.x; P[P_TV + 1] = -dl.y; P[P_TV + 2] = -dl.z;
+                    P[P_TW + 0] = dTw.x + h.dx * dk.x + h.dy * dl.x;
+                    P[P_TW + 1] = dTw.y + h.dx * dk.y + h.dy * dl.y;
+                    P[P_TW + 2] = dTw.z + h.dx * dk.z + h.dy * dl.z;
+                }
+            }
+            const bool any = __any(contrib);
+            if (any) wave_reduce24(P);
+            if ((lane & 7) == 0) {
+                const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
+                s_part[j][wave][base + 0] = any ? P[0] : 0.f;
+                s_part[j][wave][base + 1] = any ? P[1] : 0.f;
+                s_part[j][wave][base + 2] = any ? P[2] : 0.f;
+            }
+        }
+        __syncthreads();
+        // combine the 4 waves in a fixed order and store the (tile, splat) partial
+        {
+            const int j = tid >> 2, c0 = (tid & 3) * 6;
+            if (j < nb) {
+                float* dst = partials + (size_t)s_slot[j] * kNP + c0;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const int c = c0 + i;
+                    dst[i] = ((s_part[j][0][c] + s_part[j][1][c]) + s_part[j][2][c]) + s_part[j][3][c];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// setup backward: sum partials per splat, chain to parameters
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void setup_bwd_kernel(
+    int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
+    const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
+    const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials,
+    CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
+    float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers,
+    float* __restrict__ v_uv0) {
+    const Camera cam = load_camera(cam_args);
+    int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    float S[kNP];
+#pragma unroll
+    for (int i = 0; i < kNP; ++i) S[i] = 0.f;
+    const int cnt = nth[g];
+    const float4* src = reinterpret_cast<const float4*>(partials) + (size_t)offsets[g] * (kNP / 4);
+    for (int e = 0; e < cnt; ++e) {
+#pragma unroll
+        for (int k = 0; k < kNP / 4; ++k) {
+            float4 v = src[(size_t)e * (kNP / 4) + k];
+            S[4 * k] += v.x; S[4 * k + 1] += v.y; S[4 * k + 2] += v.z; S[4 * k + 3] += v.w;
+        }
+    }
+    v_rgbs[3 * g + 0] = S[P_RGB + 0];
+    v_rgbs[3 * g + 1] = S[P_RGB + 1];
+    v_rgbs[3 * g + 2] = S[P_RGB + 2];
+    v_opac[g] = S[P_OPAC];
+    v_centers[2 * g + 0] = S[P_XY + 0];
+    v_centers[2 * g + 1] = S[P_XY + 1];
+    v_uv0[2 * g + 0] = S[P_TU0];
+    v_uv0[2 * g + 1] = S[P_TV0];
+    if (cnt <= 0) {
+        v_means[3 * g] = v_means[3 * g + 1] = v_means[3 * g + 2] = 0.f;
+        v_scales[3 * g] = v_scales[3 * g + 1] = v_scales[3 * g + 2] = 0.f;
+        v_quats[4 * g] = v_quats[4 * g + 1] = v_quats[4 * g + 2] = v_quats[4 * g + 3] = 0.f;
+        return;
+    }
+    Frame fr = quat_frame(quats + 4 * g);
+    const float su = scales[3 * g] * glob, sv = scales[3 * g + 1] * glob;
+    f3 mu = mk3(means[3 * g], means[3 * g + 1], means[3 * g + 2]);
+    const Anchored an = splat_anchored(cam, mu, su, sv, fr);
+    HomogGrad hg = splat_anchored_vjp(cam, su, sv, fr, an.xn, an.yn, f3{S[P_TU], S[P_TU + 1], S[P_TU + 2]},
+                                      f3{S[P_TV], S[P_TV + 1], S[P_TV + 2]},
+                                      f3{S[P_TW], S[P_TW + 1], S[P_TW + 2]});
+    const f3 um = mk3(umap[3 * g], umap[3 * g + 1], umap[3 * g + 2]);
+    const f3 vm = mk3(vmap[3 * g], vmap[3 * g + 1], vmap[3 * g + 2]);
+    const float dauu = S[P_AUU], dauv = S[P_AUV], davu = S[P_AVU], davv = S[P_AVV];
+    float dsu = hg.dsu + dauu * dot3(fr.tu, um) + davu * dot3(fr.tu, vm);
+    float dsv = hg.dsv + dauv * dot3(fr.tv, um) + davv * dot3(fr.tv, vm);
+    f3 dtu = add3(hg.dtu, add3(scale3(um, dauu * su), scale3(vm, davu * su)));
+    f3 dtv = add3(hg.dtv, add3(scale3(um, dauv * sv), scale3(vm, davv * sv)));
+    f3 dir = f3{cam.campos[0] - mu.x, cam.campos[1] - mu.y, cam.campos[2] - mu.z};
+    const float sgn = dot3(fr.tw, dir) < 0.0f ? -1.0f : 1.0f;
+    f3 dtw = f3{sgn * S[P_NRM], sgn * S[P_NRM + 1], sgn * S[P_NRM + 2]};
+    float dq[4];
+    frame_vjp(fr, dtu, dtv, dtw, dq);
+    v_means[3 * g + 0] = hg.dmu.x;
+    v_means[3 * g + 1] = hg.dmu.y;
+    v_means[3 * g + 2] = hg.dmu.z;
+    v_scales[3 * g + 0] = dsu * glob;
+    v_scales[3 * g + 1] = dsv * glob;
+    v_scales[3 * g + 2] = 0.f;
+    v_quats[4 * g + 0] = dq[0];
+    v_quats[4 * g + 1] = dq[1];
+    v_quats[4 * g + 2] = dq[2];
+    v_quats[4 * g + 3] = dq[3];
+}
+
+int check_settings(int settings) {
+    const int known = GSTEX_SETTING_AA_BLUR | GSTEX_SETTING_DIST_REG | GSTEX_SETTING_EVAL_NORMAL;
+    if (settings & ~known) {
+        set_error("texture_gaussians: unsupported settings bits 0x%x (supported: 1<<9, 1<<10, 1<<15)",
+                  settings & ~known);
+        return GSTEX_ERR_UNSUPPORTED;
+    }
+    return GSTEX_OK;
+}
+
+}  // namespace
+
+extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* scales, float glob_scale,
+                                  const float* quats, const float* rgbs, const float* opacities,
+                                  const float* centers, const float* uv0, const float* umap, const float* vmap,
+                                  const int32_t* texture_dims, const int32_t* num_tiles_hit,
+                                  const gstex_camera* cam, float* records, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup: invalid arguments");
+    if (n == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(means && scales && quats && rgbs && opacities && centers && uv0 && umap && vmap &&
+                      texture_dims && num_tiles_hit && records,
+                  "gstex_raster_setup: null pointer");
+    setup_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, means, scales, glob_scale, quats, rgbs, opacities,
+                                                                 centers, uv0, umap, vmap, texture_dims,
+                                                                 num_tiles_hit, to_device_camera(*cam), records);
+    return launch_status("gstex_raster_setup");
+}
+
+extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
+                                const float* background, const float* records, const int32_t* tile_ranges,
+                                const int32_t* sorted_ids, const float* texture, int64_t n_texels,
+                                float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
+                                float* out_normal, float* state, void* stream) {
+    GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_fwd: invalid camera");
+    GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
+    GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_fwd: channels must be in [1, 8] (got %d)",
+                  channels);
+    GSTEX_REQUIRE(n_texels >= 0, "gstex_raster_fwd: n_texels < 0");
+    int rc = check_settings(settings);
+    if (rc) return rc;
+    GSTEX_REQUIRE(tile_ranges && out_img && out_depth && out_reg && out_alpha && out_tex && out_normal && state,
+                  "gstex_raster_fwd: null pointer");
+    const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
+    CamArgs dc = to_device_camera(*cam);
+    hipStream_t st = as_stream(stream);
+    const int nblk = tiles_x * tiles_y;
+#define GSTEX_FWD(CC)                                                                                          \
+    raster_fwd_kernel<CC><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,          \
+                                                     (const float4*)records, (const int2*)tile_ranges,        \
+                                                     sorted_ids, texture, out_img, out_depth, out_reg,        \
+                                                     out_alpha, out_tex, out_normal, (float4*)state)
+    if (channels == 3) GSTEX_FWD(3);
+    else if (channels == 6) GSTEX_FWD(6);
+    else GSTEX_FWD(0);
+#undef GSTEX_FWD
+    return launch_status("gstex_raster_fwd");
+}
+
+extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
+                                const float* background, const float* records, const int32_t* tile_ranges,
+                                const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
+                                int64_t n_texels, const float* state, const float* v_img, const float* v_depth,
+                                const float* v_reg, const float* v_alpha, const float* v_tex,
+                                const float* v_normal, float* partials, float* v_texture, void* stream) {
+    GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
+    GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
+    GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
+    int rc = check_settings(settings);
+    if (rc) return rc;
+    GSTEX_REQUIRE(tile_ranges && state && v_img && v_depth && v_reg && v_alpha && v_tex && v_normal,
+                  "gstex_raster_bwd: null pointer");
+    GSTEX_REQUIRE(n_texels == 0 || (texture && v_texture), "gstex_raster_bwd: null texture");
+    const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
+    CamArgs dc = to_device_camera(*cam);
+    hipStream_t st = as_stream(stream);
+    const int nblk = tiles_x * tiles_y;
+#define GSTEX_BWD(CC)                                                                                          \
+    raster_bwd_kernel<CC><<<nblk, kThreads, 0, st>>>(                                                          \
+        dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,    \
+        sorted_ids, sorted_slots, texture, (const float4*)state, v_img, v_depth, v_reg, v_alpha, v_tex,       \
+        v_normal, partials, v_texture)
+    if (channels == 3) GSTEX_BWD(3);
+    else if (channels == 6) GSTEX_BWD(6);
+    else GSTEX_BWD(0);
+#undef GSTEX_BWD
+    return launch_status("gstex_raster_bwd");
+}
+
+extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
+                                      const float* quats, const float* opacities, const float* umap,
+                                      const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
+                                      const float* partials, const gstex_camera* cam, float* v_means,
+                                      float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities,
+                                      float* v_centers, float* v_uv0, void* stream) {
+    (void)opacities;
+    GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup_bwd: invalid arguments");
+    if (n == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
+                      v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
+                  "gstex_raster_setup_bwd: null pointer");
+    setup_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(
+        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
+        v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+    return launch_status("gstex_raster_setup_bwd");
+}

@@ -1,0 +1,186 @@
+"""GStex train-step harness around the HIP rasterizer.
+
+Reproduces the parts of the reference's GStexModel that sit either side of the hot path, so the
+"train-step ms" metric is measured on the same work the reference does per step:
+  * parameter activations            gstex.py:1059-1066
+  * UV frames (detached)             gstex.py:975-990
+  * preprocessing                    gstex.py:1077-1080   (project_points / get_aabb_2d / tiles)
+  * SH colour with the DC zeroed     gstex.py:1099-1114
+  * texture = SH2RGB(texture_dc)     gstex.py:1093-1094,1119
+  * texture_gaussians                gstex.py:1133-1162
+  * background composite             gstex.py:1204-1205
+  * loss 0.8 L1 + 0.2 (1 - SSIM)     gstex.py:1301-1322 (pytorch_msssim SSIM semantics)
+  * per-group Adam, eps 1e-15        gstex_configs.py:207-244, engine/optimizers.py:158-171
+The rechart every 100 steps (gstex.py:890-914) is provided by `recharge()`.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .charts import SH2RGB, build_charts, get_uv_mapping, texture_dims_to_query
+from .scene import Scene, View
+
+# gstex-blender-nvs optimizer settings (gstex_configs.py:207-244)
+LRS = {
+    "xyz": 5 * 1.6e-5,
+    "features_dc": 0.0025,
+    "features_rest": 0.0025 / 20,
+    "opacity": 0.05,
+    "scaling": 0.005,
+    "rotation": 0.001,
+    "texture_dc": 1e-3,
+}
+DEFAULT_SETTINGS = (1 << 9) | (1 << 10)
+
+
+def _gauss_window(size=11, sigma=1.5, device=None):
+    coords = torch.arange(size, dtype=torch.float32, device=device) - size // 2
+    g = torch.exp(-(coords**2) / (2 * sigma**2))
+    return g / g.sum()
+
+
+def ssim(x: torch.Tensor, y: torch.Tensor, data_range=1.0, win_size=11, sigma=1.5, K=(0.01, 0.03)) -> torch.Tensor:
+    """pytorch_msssim.SSIM(data_range=1, size_average=True, channel=3) on (1,C,H,W): separable
+    gaussian window, valid convolution, mean over the map (gstex.py:351,1303)."""
+    C = x.shape[1]
+    g = _gauss_window(win_size, sigma, x.device)
+    wh = g.view(1, 1, 1, -1).repeat(C, 1, 1, 1)
+    wv = g.view(1, 1, -1, 1).repeat(C, 1, 1, 1)
+
+    def filt(t):
+        return F.conv2d(F.conv2d(t, wh, groups=C), wv, groups=C)
+
+    C1 = (K[0] * data_range) ** 2
+    C2 = (K[1] * data_range) ** 2
+    mu1, mu2 = filt(x), filt(y)
+    s11 = filt(x * x) - mu1 * mu1
+    s22 = filt(y * y) - mu2 * mu2
+    s12 = filt(x * y) - mu1 * mu2
+    cs = (2 * s12 + C2) / (s11 + s22 + C2)
+    sm = ((2 * mu1 * mu2 + C1) / (mu1 * mu1 + mu2 * mu2 + C1)) * cs
+    return sm.mean()
+
+
+@dataclass
+class StepOutput:
+    loss: torch.Tensor
+    rgb: torch.Tensor
+
+
+class GStexTrainer:
+    """Holds the GStex parameters on one device and runs forward/backward/Adam steps."""
+
+    def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
+                 pixel_num: float | None = None, background=(1.0, 1.0, 1.0)):
+        self.device = torch.device(device)
+        d = self.device
+        P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
+        self.means = P(scene.means)
+        self.scales = P(scene.log_scales)
+        self.quats = P(scene.quats)
+        self.opacities = P(scene.opacity_logits)
+        self.features_dc = P(scene.features_dc)
+        self.features_rest = P(scene.features_rest)
+        # the texel parameter stores the SH-DC value; the raster reads SH2RGB of it (gstex.py:1119)
+        tex_dc = (scene.texture[:, :3] - 0.5) / 0.28209479177387814
+        self.texture_dc = P(tex_dc)
+        self.texture_dims = scene.texture_dims.to(d).contiguous()
+        self.mappings = scene.mappings.to(d).contiguous()
+        self.sh_degree = sh_degree
+        self.settings = settings
+        self.pixel_num = pixel_num if pixel_num is not None else float(scene.texture.shape[0])
+        self.background = torch.tensor(background, dtype=torch.float32, device=d)
+        self.step = 0
+        self._build_optimizer()
+
+    # ------------------------------------------------------------------ parameters
+    def param_groups(self):
+        return {
+            "xyz": [self.means],
+            "features_dc": [self.features_dc],
+            "features_rest": [self.features_rest],
+            "opacity": [self.opacities],
+            "scaling": [self.scales],
+            "rotation": [self.quats],
+            "texture_dc": [self.texture_dc],
+        }
+
+    def parameters(self):
+        return [p for ps in self.param_groups().values() for p in ps]
+
+    def _build_optimizer(self):
+        groups = [{"params": ps, "lr": LRS[name], "name": name} for name, ps in self.param_groups().items()]
+        self.optimizer = torch.optim.Adam(groups, eps=1e-15, foreach=True)
+
+    # ------------------------------------------------------------------ forward
+    def render(self, view: View, sh_degree_now: int | None = None):
+        """get_outputs (gstex.py:992-1236), training branch."""
+        means = self.means
+        quats = self.quats / self.quats.norm(dim=-1, keepdim=True)
+        s = torch.exp(self.scales[:, :-1]).clamp(min=1e-9)
+        scales = torch.cat([s, 1e-5 * s.mean(dim=-1, keepdim=True).detach()], dim=-1)
+        opacities = torch.sigmoid(self.opacities)
+        uv0, umap, vmap = get_uv_mapping(quats, self.mappings)
+        intr = (view.fx, view.fy, view.cx, view.cy)
+        _, depths = ops.project_points(means, view.viewmat, intr)
+        centers, extents = ops.get_aabb_2d(means, scales, 1, quats, view.viewmat, intr)
+        nth = ops.get_num_tiles_hit_2d(centers, extents, view.H, view.W, ops.BLOCK_WIDTH)
+        n = self.means.shape[0]
+        if self.sh_degree > 0:
+            colors = torch.cat([torch.zeros_like(self.features_dc[:, None, :]), self.features_rest], dim=1)
+            viewdirs = means.detach() - view.c2w[:3, 3]
+            viewdirs = viewdirs / viewdirs.norm(dim=-1, keepdim=True)
+            deg = self.sh_degree if sh_degree_now is None else sh_degree_now
+            rgbs = ops.spherical_harmonics(deg, viewdirs, colors)
+        else:
+            rgbs = torch.sigmoid(self.features_dc)
+        texture = SH2RGB(self.texture_dc)
+        img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
+            (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
+            uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
+            ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background))
+        rgb = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :], 0.0, 1.0)
+        return dict(rgb=rgb, depth=depth, reg=reg, alpha=alpha, normal=normal)
+
+    def loss(self, rgb: torch.Tensor, gt: torch.Tensor, ssim_lambda: float = 0.2) -> torch.Tensor:
+        l1 = torch.abs(gt - rgb).mean()
+        sim = 1 - ssim(gt.permute(2, 0, 1)[None], rgb.permute(2, 0, 1)[None])
+        return (1 - ssim_lambda) * l1 + ssim_lambda * sim
+
+    def forward_backward(self, view: View, gt: torch.Tensor) -> StepOutput:
+        out = self.render(view)
+        loss = self.loss(out["rgb"], gt)
+        loss.backward()
+        return StepOutput(loss.detach(), out["rgb"].detach())
+
+    def optimizer_step(self):
+        self.optimizer.step()
+        self.step += 1
+
+    def zero_grad(self):
+        self.optimizer.zero_grad(set_to_none=False)
+
+    # ------------------------------------------------------------------ rechart
+    @torch.no_grad()
+    def recharge(self):
+        """retexture_after (gstex.py:890-895): rebuild the charts from the current scales, resample
+        the texels onto the new grid (texture_sample, jagged_texture.py:116-143) and reset the
+        texture Adam moments (gstex.py:799-826)."""
+        new_dims, mappings, _ = build_charts(self.scales.detach(), self.pixel_num)
+        ids, uv = texture_dims_to_query(new_dims)
+        query = self.texture_dims[ids].contiguous()
+        new_tex = ops.texture_sample((1, 1, 3), query, self.texture_dc.detach().contiguous(), uv.contiguous())
+        self.texture_dims = new_dims.contiguous()
+        self.mappings.copy_(mappings)
+        old = self.texture_dc
+        self.texture_dc = torch.nn.Parameter(new_tex.contiguous())
+        for g in self.optimizer.param_groups:
+            if g["name"] == "texture_dc":
+                g["params"] = [self.texture_dc]
+        self.optimizer.state.pop(old, None)
+        return new_dims

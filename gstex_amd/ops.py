@@ -1,0 +1,425 @@
+"""torch.autograd front-ends of the libgstex_hip.so C-ABI.
+
+These mirror the `gstex_cuda` Python surface that nerfstudio/models/gstex.py imports
+(gstex.py:28-32, models/jagged_texture.py:7-8, scripts/exporter.py:40): same names, positional
+arguments and return tuples.  All work is enqueued on torch's current HIP stream.  There is no CPU
+path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_lib.py).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from . import _lib
+from ._lib import PARTIAL_FLOATS, REC_FLOATS, call, ptr
+
+BLOCK_WIDTH = 16
+
+# ----------------------------------------------------------------------------------------
+# optional per-kernel timing: HIP events recorded on the stream each kernel is launched on
+# ----------------------------------------------------------------------------------------
+_TIMING: dict | None = None
+
+
+def set_kernel_timing(enabled: bool) -> None:
+    """Record a HIP event pair around every timed C-ABI launch (bench.py / profiling only)."""
+    global _TIMING
+    _TIMING = {} if enabled else None
+
+
+def kernel_times() -> dict:
+    """{name: [ms, ...]} for the launches recorded since set_kernel_timing(True) (synchronises)."""
+    if not _TIMING:
+        return {}
+    torch.cuda.synchronize()
+    return {k: [a.elapsed_time(b) for a, b in v] for k, v in _TIMING.items()}
+
+
+def _launch(name: str, *args) -> None:
+    if _TIMING is None:
+        call(name, *args)
+        return
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    call(name, *args)
+    b.record()
+    _TIMING.setdefault(name, []).append((a, b))
+
+
+# ----------------------------------------------------------------------------------------
+# validation helpers (TORCH_CHECK-style RuntimeErrors)
+# ----------------------------------------------------------------------------------------
+def _check(cond: bool, msg: str) -> None:
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _dev(t: torch.Tensor, name: str) -> None:
+    _check(isinstance(t, torch.Tensor), f"{name} must be a tensor")
+    _check(t.is_cuda, f"{name} must be a HIP (cuda) tensor; gstex_amd has no CPU path (got {t.device})")
+
+
+def _f32(t: torch.Tensor, name: str, shape=None) -> torch.Tensor:
+    _dev(t, name)
+    _check(t.dtype == torch.float32, f"{name} must be float32 (got {t.dtype})")
+    if shape is not None:
+        _check(t.dim() == len(shape) and all(s is None or s == d for s, d in zip(shape, t.shape)),
+               f"{name} must have shape {tuple('*' if s is None else s for s in shape)} (got {tuple(t.shape)})")
+    return t.contiguous()
+
+
+def _i32(t: torch.Tensor, name: str, shape=None) -> torch.Tensor:
+    _dev(t, name)
+    _check(t.dtype == torch.int32, f"{name} must be int32 (got {t.dtype})")
+    if shape is not None:
+        _check(t.dim() == len(shape) and all(s is None or s == d for s, d in zip(shape, t.shape)),
+               f"{name} must have shape {tuple('*' if s is None else s for s in shape)} (got {tuple(t.shape)})")
+    return t.contiguous()
+
+
+def _viewmat(viewmat: torch.Tensor) -> torch.Tensor:
+    v = viewmat.detach()
+    if v.dim() == 3:
+        v = v.squeeze(0)
+    _check(v.shape in ((3, 4), (4, 4)), f"viewmat must be (3,4) or (4,4) (got {tuple(viewmat.shape)})")
+    return _f32(v[:3, :], "viewmat")
+
+
+def _c2w(c2w) -> torch.Tensor | None:
+    if c2w is None:
+        return None
+    c = c2w.detach()
+    if c.dim() == 3:
+        c = c.squeeze(0)
+    _check(c.shape == (4, 4), f"c2w must be (4,4) (got {tuple(c2w.shape)})")
+    return _f32(c, "c2w")
+
+
+def _stream(t: torch.Tensor) -> int:
+    return _lib.stream_of(t.device)
+
+
+# ----------------------------------------------------------------------------------------
+# project_points / get_aabb_2d / get_num_tiles_hit_2d
+# ----------------------------------------------------------------------------------------
+class _ProjectPoints(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means, viewmat, fx, fy, cx, cy):
+        means = _f32(means, "means", (None, 3))
+        vm = _viewmat(viewmat)
+        n = means.shape[0]
+        xys = torch.empty((n, 2), device=means.device, dtype=torch.float32)
+        depths = torch.empty((n,), device=means.device, dtype=torch.float32)
+        cam = _lib.make_camera(vm, None, fx, fy, cx, cy, 0, 0, BLOCK_WIDTH)
+        call("gstex_project_points", n, ptr(means), cam, ptr(xys), ptr(depths), _stream(means))
+        ctx.save_for_backward(means, vm)
+        ctx.intr = (fx, fy, cx, cy)
+        return xys, depths
+
+    @staticmethod
+    def backward(ctx, v_xys, v_depths):
+        means, vm = ctx.saved_tensors
+        n = means.shape[0]
+        v_means = torch.empty_like(means)
+        cam = _lib.make_camera(vm, None, *ctx.intr, 0, 0, BLOCK_WIDTH)
+        v_xys = v_xys.contiguous() if v_xys is not None else None
+        v_depths = v_depths.contiguous() if v_depths is not None else None
+        call("gstex_project_points_bwd", n, ptr(means), cam, ptr(v_xys), ptr(v_depths), ptr(v_means),
+             _stream(means))
+        return v_means, None, None, None, None, None
+
+
+def project_points(means: torch.Tensor, viewmat: torch.Tensor, intrinsics) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Pinhole projection of splat centres -> (xys (N,2), depths (N,)). gstex.py:1077."""
+    fx, fy, cx, cy = [float(v) for v in intrinsics]
+    return _ProjectPoints.apply(means, viewmat, fx, fy, cx, cy)
+
+
+class _Aabb2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means, scales, glob_scale, quats, viewmat, fx, fy, cx, cy):
+        means = _f32(means, "means", (None, 3))
+        n = means.shape[0]
+        scales = _f32(scales, "scales", (n, 3))
+        quats = _f32(quats, "quats", (n, 4))
+        vm = _viewmat(viewmat)
+        centers = torch.empty((n, 2), device=means.device, dtype=torch.float32)
+        extents = torch.empty((n, 2), device=means.device, dtype=torch.float32)
+        cam = _lib.make_camera(vm, None, fx, fy, cx, cy, 0, 0, BLOCK_WIDTH)
+        call("gstex_aabb_2d", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), cam, ptr(centers),
+             ptr(extents), _stream(means))
+        ctx.save_for_backward(means, scales, quats, vm)
+        ctx.args = (float(glob_scale), fx, fy, cx, cy)
+        ctx.mark_non_differentiable(extents)
+        return centers, extents
+
+    @staticmethod
+    def backward(ctx, v_centers, v_extents):
+        means, scales, quats, vm = ctx.saved_tensors
+        glob, fx, fy, cx, cy = ctx.args
+        n = means.shape[0]
+        v_means = torch.zeros_like(means)
+        v_scales = torch.zeros_like(scales)
+        v_quats = torch.zeros_like(quats)
+        if v_centers is not None:
+            cam = _lib.make_camera(vm, None, fx, fy, cx, cy, 0, 0, BLOCK_WIDTH)
+            call("gstex_aabb_2d_bwd", n, ptr(means), ptr(scales), glob, ptr(quats), cam,
+                 ptr(v_centers.contiguous()), ptr(v_means), ptr(v_scales), ptr(v_quats), _stream(means))
+        return v_means, v_scales, None, v_quats, None, None, None, None, None
+
+
+def get_aabb_2d(means, scales, glob_scale, quats, viewmat, intrinsics):
+    """2DGS screen-space bound -> (centers (N,2), extents (N,2)). gstex.py:1079."""
+    fx, fy, cx, cy = [float(v) for v in intrinsics]
+    return _Aabb2d.apply(means, scales, glob_scale, quats, viewmat, fx, fy, cx, cy)
+
+
+def get_num_tiles_hit_2d(centers, extents, H: int, W: int, block_width: int) -> torch.Tensor:
+    """Tiles overlapped by centre +- extent (gsplat-0.1 tile-bbox convention) -> int32 (N,).
+    gstex.py:1080."""
+    centers = _f32(centers.detach(), "centers", (None, 2))
+    n = centers.shape[0]
+    extents = _f32(extents.detach(), "extents", (n, 2))
+    out = torch.empty((n,), device=centers.device, dtype=torch.int32)
+    call("gstex_num_tiles_hit", n, ptr(centers), ptr(extents), int(H), int(W), int(block_width), ptr(out),
+         _stream(centers))
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# binning
+# ----------------------------------------------------------------------------------------
+def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_width: int = BLOCK_WIDTH):
+    """Tile binning + per-tile depth sort.  Returns (offsets (N+1,), tile_ranges (n_tiles,2),
+    sorted_ids (I,), sorted_slots (I,)), all int32.  One host sync to size the I-length buffers."""
+    n = centers.shape[0]
+    dev = centers.device
+    st = _stream(centers)
+    nth = _i32(num_tiles_hit, "num_tiles_hit", (n,))
+    offsets = torch.empty((n + 1,), device=dev, dtype=torch.int32)
+    ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=dev, dtype=torch.uint8)
+    call("gstex_scan_offsets", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), st)
+    n_isect = int(offsets[n].item())
+    tiles_x = (W + block_width - 1) // block_width
+    tiles_y = (H + block_width - 1) // block_width
+    n_tiles = tiles_x * tiles_y
+    tile_ranges = torch.empty((n_tiles, 2), device=dev, dtype=torch.int32)
+    sorted_ids = torch.empty((n_isect,), device=dev, dtype=torch.int32)
+    sorted_slots = torch.empty((n_isect,), device=dev, dtype=torch.int32)
+    wsb = int(_lib.load().gstex_bin_workspace_size(n, n_isect, n_tiles))
+    bws = torch.empty((max(wsb, 1),), device=dev, dtype=torch.uint8)
+    _launch("gstex_bin_sort", n, n_isect, ptr(centers.detach().contiguous()), ptr(extents.detach().contiguous()),
+         ptr(depths.detach().contiguous()), ptr(nth), ptr(offsets), int(H), int(W), int(block_width),
+         ptr(tile_ranges), ptr(sorted_ids), ptr(sorted_slots), ptr(bws), bws.numel(), st)
+    return offsets, tile_ranges, sorted_ids, sorted_slots
+
+
+# ----------------------------------------------------------------------------------------
+# texture_gaussians
+# ----------------------------------------------------------------------------------------
+class _TextureGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
+                scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
+                block_width, settings, background):
+        N, L, C = (int(v) for v in texture_info)
+        _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
+        _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
+        _check(int(block_width) == BLOCK_WIDTH, f"block_width must be {BLOCK_WIDTH} (got {block_width})")
+        means = _f32(means, "means", (None, 3))
+        n = means.shape[0]
+        _check(N == n, f"texture_info[0] ({N}) != number of splats ({n})")
+        dims = _i32(texture_dims, "texture_dims", (n, 3))
+        centers_c = _f32(centers, "centers", (n, 2))
+        extents_c = _f32(extents.detach(), "extents", (n, 2))
+        depths_c = _f32(depths.detach(), "depths", (n,))
+        nth = _i32(num_tiles_hit, "num_tiles_hit", (n,))
+        rgbs = _f32(rgbs, "rgbs", (n, 3))
+        opacities = _f32(opacities, "opacities", (n, 1))
+        scales = _f32(scales, "scales", (n, 3))
+        quats = _f32(quats, "quats", (n, 4))
+        uv0 = _f32(uv0, "uv0", (n, 1, 2))
+        umap = _f32(umap, "umap", (n, 1, 3))
+        vmap = _f32(vmap, "vmap", (n, 1, 3))
+        texture = _f32(texture, "texture", (None, C))
+        vm = _viewmat(viewmat)
+        cw = _c2w(c2w)
+        bg = _f32(background.detach(), "background", (3,)) if background is not None else None
+        H, W = int(H), int(W)
+        dev = means.device
+        st = _stream(means)
+        cam = _lib.make_camera(vm, cw, fx, fy, cx, cy, H, W, BLOCK_WIDTH)
+
+        offsets, tile_ranges, sorted_ids, sorted_slots = bin_and_sort(
+            centers_c.detach(), extents_c, depths_c, nth, H, W, BLOCK_WIDTH)
+        records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
+        _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
+             ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
+             st)
+        f = dict(device=dev, dtype=torch.float32)
+        img = torch.empty((H, W, 3), **f)
+        depth = torch.empty((H, W), **f)
+        reg = torch.empty((H, W), **f)
+        alpha = torch.empty((H, W), **f)
+        tex = torch.empty((H, W, C), **f)
+        normal = torch.empty((H, W, 3), **f)
+        state = torch.empty((H, W, 4), **f)
+        _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(sorted_ids),
+             ptr(texture), texture.shape[0], ptr(img), ptr(depth), ptr(reg), ptr(alpha), ptr(tex), ptr(normal),
+             ptr(state), st)
+        ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
+                              sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm, bg if bg
+                              is not None else vm)
+        ctx.has_c2w = cw is not None
+        ctx.has_bg = bg is not None
+        ctx.args = (float(glob_scale), float(fx), float(fy), float(cx), float(cy), H, W, C, int(settings))
+        return img, depth, reg, alpha, tex, normal
+
+    @staticmethod
+    def backward(ctx, v_img, v_depth, v_reg, v_alpha, v_tex, v_normal):
+        (means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges, sorted_ids, sorted_slots,
+         records, state, vm, cw, bg) = ctx.saved_tensors
+        cw = cw if ctx.has_c2w else None
+        bg = bg if ctx.has_bg else None
+        glob, fx, fy, cx, cy, H, W, C, settings = ctx.args
+        n = means.shape[0]
+        dev = means.device
+        st = _stream(means)
+        cam = _lib.make_camera(vm, cw, fx, fy, cx, cy, H, W, BLOCK_WIDTH)
+
+        def g(t, shape):
+            return torch.zeros(shape, device=dev, dtype=torch.float32) if t is None else t.contiguous()
+
+        v_img = g(v_img, (H, W, 3))
+        v_depth = g(v_depth, (H, W))
+        v_reg = g(v_reg, (H, W))
+        v_alpha = g(v_alpha, (H, W))
+        v_tex = g(v_tex, (H, W, C))
+        v_normal = g(v_normal, (H, W, 3))
+        n_isect = sorted_ids.shape[0]
+        partials = torch.empty((n_isect, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
+        v_texture = torch.zeros_like(texture)
+        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(sorted_ids),
+             ptr(sorted_slots), ptr(texture), texture.shape[0], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg),
+             ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), st)
+        v_means = torch.empty_like(means)
+        v_scales = torch.empty_like(scales)
+        v_quats = torch.empty_like(quats)
+        v_rgbs = torch.empty((n, 3), device=dev, dtype=torch.float32)
+        v_opac = torch.empty((n, 1), device=dev, dtype=torch.float32)
+        v_centers = torch.empty((n, 2), device=dev, dtype=torch.float32)
+        v_uv0 = torch.empty((n, 1, 2), device=dev, dtype=torch.float32)
+        _launch("gstex_raster_setup_bwd", n, ptr(means), ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap),
+             ptr(vmap), ptr(nth), ptr(offsets), ptr(partials), cam, ptr(v_means), ptr(v_scales), ptr(v_quats),
+             ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
+        v_bg = None
+        if ctx.needs_input_grad[26]:
+            v_bg = (v_img * state[..., 0:1]).sum((0, 1))
+        return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
+                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg)
+
+
+def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
+                      scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
+                      block_width, settings, background=None, use_torch_impl=False):
+    """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
+
+    Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
+    Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
+    uv0 and background; umap/vmap are treated as constants (detached by the caller, gstex.py:977-984).
+    """
+    if use_torch_impl:
+        raise NotImplementedError(
+            "texture_gaussians(use_torch_impl=True): gstex_amd ships no CPU rasterizer; "
+            "the CPU restatement in oracle/ is test infrastructure only")
+    return _TextureGaussians.apply(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs,
+                                   opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
+                                   c2w, fx, fy, cx, cy, H, W, block_width, settings, background)
+
+
+rasterize_gaussians = texture_gaussians  # north_star name
+
+
+# ----------------------------------------------------------------------------------------
+# spherical harmonics
+# ----------------------------------------------------------------------------------------
+def num_sh_bases(degree: int) -> int:
+    """(degree+1)^2 (gstex.py:307)."""
+    if degree < 0 or degree > 4:
+        raise ValueError(f"SH degree must be in [0, 4] (got {degree})")
+    return (degree + 1) ** 2
+
+
+class _SH(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, degree, viewdirs, coeffs):
+        viewdirs = _f32(viewdirs.detach(), "viewdirs", (None, 3))
+        n = viewdirs.shape[0]
+        coeffs = _f32(coeffs, "coeffs", (n, None, 3))
+        K = coeffs.shape[1]
+        _check(K >= num_sh_bases(degree), f"coeffs has {K} bases < (degree+1)^2 = {num_sh_bases(degree)}")
+        out = torch.empty((n, 3), device=coeffs.device, dtype=torch.float32)
+        call("gstex_sh_fwd", n, int(degree), K, ptr(viewdirs), ptr(coeffs), ptr(out), _stream(coeffs))
+        ctx.save_for_backward(viewdirs)
+        ctx.degree, ctx.K = int(degree), K
+        return out
+
+    @staticmethod
+    def backward(ctx, v_out):
+        (viewdirs,) = ctx.saved_tensors
+        n = viewdirs.shape[0]
+        v_coeffs = torch.empty((n, ctx.K, 3), device=viewdirs.device, dtype=torch.float32)
+        call("gstex_sh_bwd", n, ctx.degree, ctx.K, ptr(viewdirs), ptr(v_out.contiguous()), ptr(v_coeffs),
+             _stream(viewdirs))
+        return None, None, v_coeffs
+
+
+def spherical_harmonics(degrees_to_use: int, viewdirs: torch.Tensor, coeffs: torch.Tensor) -> torch.Tensor:
+    """View-dependent colour sum_k basis_k(dir) coeffs[:, k] (no +0.5, gstex.py:1099-1114).
+    Differentiable w.r.t. coeffs only (the caller detaches viewdirs)."""
+    return _SH.apply(int(degrees_to_use), viewdirs, coeffs)
+
+
+# ----------------------------------------------------------------------------------------
+# texture_sample
+# ----------------------------------------------------------------------------------------
+class _TextureSample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, C, query_dims, texture, uv):
+        qd = _i32(query_dims, "query_dims", (None, 3))
+        nq = qd.shape[0]
+        texture = _f32(texture, "texture", (None, C))
+        uv = _f32(uv.detach(), "uv", (nq, 2))
+        out = torch.empty((nq, C), device=texture.device, dtype=torch.float32)
+        call("gstex_texture_sample", nq, C, ptr(qd), ptr(texture), texture.shape[0], ptr(uv), ptr(out),
+             _stream(texture))
+        ctx.save_for_backward(qd, uv)
+        ctx.C, ctx.T = C, texture.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, v_out):
+        qd, uv = ctx.saved_tensors
+        v_tex = torch.zeros((ctx.T, ctx.C), device=qd.device, dtype=torch.float32)
+        call("gstex_texture_sample_bwd", qd.shape[0], ctx.C, ptr(qd), ctx.T, ptr(uv), ptr(v_out.contiguous()),
+             ptr(v_tex), _stream(qd))
+        return None, None, v_tex, None
+
+
+def texture_sample(texture_info, query_dims, texture, uv, use_torch_impl=False):
+    """Resample jagged textures at per-texel UVs (jagged_texture.py:135-138) -> (T', C).
+    use_torch_impl=True runs the reference-API pure-torch sampler gstex_cuda._torch_impl.sample_texture."""
+    C = int(texture_info[-1])
+    if use_torch_impl:
+        from gstex_cuda._torch_impl import sample_texture
+
+        return sample_texture(query_dims, texture, uv)
+    return _TextureSample.apply(C, query_dims, texture, uv)
+
+
+def texture_edit(*args, **kwargs):
+    """Viewer paint tool back-projection (gstex.py:556-585).  Out of the hot-path scope this round
+    (SURVEY.md §8f-4)."""
+    raise NotImplementedError("texture_edit is not implemented in gstex_amd yet (viewer-only, SURVEY §8f-4)")

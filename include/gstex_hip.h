@@ -1,0 +1,160 @@
+/*
+ * gstex_hip.h — C-ABI of libgstex_hip.so, the MI355X (gfx950) textured-2DGS rasterizer.
+ *
+ * This is the drop-in boundary for the `gstex_cuda` native extension that the reference
+ * (nvnhat95/GStex) imports but does not vendor (`.gitmodules:1-3`, submodules/GStex_cuda is
+ * empty).  Each entry point below replaces one native op behind a reference call site:
+ *
+ *   gstex_project_points      <- gstex_cuda.get_aabb_2d.project_points      (nerfstudio/models/gstex.py:1077)
+ *   gstex_aabb_2d(+_bwd)      <- gstex_cuda.get_aabb_2d.get_aabb_2d          (gstex.py:1079)
+ *   gstex_num_tiles_hit       <- gstex_cuda.get_aabb_2d.get_num_tiles_hit_2d (gstex.py:1080)
+ *   gstex_scan_offsets,
+ *   gstex_bin_sort            <- tile binning + per-tile depth sort inside texture_gaussians
+ *                                (args gstex.py:1136-1139,1158)
+ *   gstex_raster_setup,
+ *   gstex_raster_fwd          <- gstex_cuda.texture.texture_gaussians forward (gstex.py:1133-1162)
+ *   gstex_raster_bwd,
+ *   gstex_raster_setup_bwd    <- texture_gaussians backward (autograd, engine/trainer.py:460)
+ *   gstex_sh_fwd / _bwd       <- gstex_cuda.sh.spherical_harmonics           (gstex.py:1109,1111)
+ *   gstex_texture_sample(+_bwd) <- gstex_cuda.texture_sample.texture_sample  (models/jagged_texture.py:138)
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer to contiguous row-major fp32 / int32 memory, except
+ *     `const gstex_camera*` which is a HOST struct (read at call time) of device pointers.
+ *   - `stream` is a hipStream_t (NULL = default stream). Calls only enqueue work: no allocation,
+ *     no host synchronisation, so they are safe to capture in a hipGraph.
+ *   - Scratch memory is caller-owned: query the size with the *_workspace_size function, allocate
+ *     it (e.g. with the torch caching allocator) and pass it in.
+ *   - Return value: 0 (GSTEX_OK) or a gstex_status; the message of the last failure on the calling
+ *     thread is returned by gstex_last_error().
+ */
+#ifndef GSTEX_HIP_H
+#define GSTEX_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSTEX_ABI_VERSION 1
+
+/* Per-record layout of the splat table written by gstex_raster_setup (floats). */
+#define GSTEX_REC_FLOATS 32
+/* Per-(tile, splat) gradient partial written by gstex_raster_bwd (floats). */
+#define GSTEX_PARTIAL_FLOATS 24
+
+/* settings bitfield (GStexModelConfig.settings, gstex.py:194-197) */
+#define GSTEX_SETTING_AA_BLUR (1 << 9)   /* 2DGS screen-space low-pass */
+#define GSTEX_SETTING_DIST_REG (1 << 10) /* 2DGS NDC depth-distortion output */
+#define GSTEX_SETTING_EDIT (1 << 13)     /* texture_edit request (gstex.py:599) */
+#define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198); accepted, no-op */
+
+typedef enum {
+    GSTEX_OK = 0,
+    GSTEX_ERR_INVALID_ARG = 1,
+    GSTEX_ERR_LAUNCH = 2,
+    GSTEX_ERR_UNSUPPORTED = 3,
+    GSTEX_ERR_WORKSPACE = 4
+} gstex_status;
+
+/* Pinhole camera (a HOST struct holding DEVICE pointers, so no host sync is needed to read the
+ * model's on-GPU matrices).  viewmat = first 3 rows of world->camera (OpenCV axes, after the y/z
+ * flip of gstex.py:1031-1041), row-major DEVICE float[12].  c2w = its inverse, row-major DEVICE
+ * float[16] (only the camera centre c2w[:3,3] is read; NULL = derive it from viewmat). */
+typedef struct {
+    const float* viewmat;
+    const float* c2w;
+    float fx, fy, cx, cy;
+    int32_t H, W, block;
+} gstex_camera;
+
+const char* gstex_last_error(void);
+int gstex_abi_version(void);
+
+/* ---- per-splat preprocessing ---------------------------------------------------------- */
+int gstex_project_points(int32_t n, const float* means, const gstex_camera* cam,
+                         float* xys, float* depths, void* stream);
+int gstex_project_points_bwd(int32_t n, const float* means, const gstex_camera* cam,
+                             const float* v_xys, const float* v_depths, float* v_means,
+                             void* stream);
+int gstex_aabb_2d(int32_t n, const float* means, const float* scales, float glob_scale,
+                  const float* quats, const gstex_camera* cam, float* centers, float* extents,
+                  void* stream);
+/* Accumulates (+=) the gradient of the AABB centre into v_means / v_scales / v_quats. */
+int gstex_aabb_2d_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
+                      const float* quats, const gstex_camera* cam, const float* v_centers,
+                      float* v_means, float* v_scales, float* v_quats, void* stream);
+int gstex_num_tiles_hit(int32_t n, const float* centers, const float* extents, int32_t H,
+                        int32_t W, int32_t block, int32_t* num_tiles_hit, void* stream);
+
+/* ---- binning + per-tile depth sort ---------------------------------------------------- */
+size_t gstex_scan_workspace_size(int32_t n);
+/* offsets[0..n] = exclusive prefix sum of num_tiles_hit; offsets[n] = total intersections. */
+int gstex_scan_offsets(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets,
+                       void* workspace, size_t workspace_bytes, void* stream);
+size_t gstex_bin_workspace_size(int32_t n, int64_t n_isect, int32_t n_tiles);
+/* Emits one (tile, splat) pair per covered tile, buckets them per tile and sorts every tile's
+ * list by (depth bits, splat id).  Outputs: tile_ranges[n_tiles][2] = [start, end) into
+ * sorted_ids; sorted_ids[n_isect] = splat id; sorted_slots[n_isect] = emission index
+ * offsets[id] + k (k = row-major rank of the tile inside the splat's tile rectangle). */
+int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float* extents,
+                   const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                   int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
+                   int32_t* sorted_ids, int32_t* sorted_slots, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* ---- rasterizer --------------------------------------------------------------------- */
+/* Builds the per-splat raster record table records[n][GSTEX_REC_FLOATS]. */
+int gstex_raster_setup(int32_t n, const float* means, const float* scales, float glob_scale,
+                       const float* quats, const float* rgbs, const float* opacities,
+                       const float* centers, const float* uv0, const float* umap,
+                       const float* vmap, const int32_t* texture_dims,
+                       const int32_t* num_tiles_hit, const gstex_camera* cam, float* records,
+                       void* stream);
+/* Forward composite. Outputs are [H][W][k] row-major. state[H*W][4] = {T_final, M1, M2,
+ * last_contributor (as int bits)} is saved for the backward pass. background is a device
+ * float[3] (or NULL = black) added as T_final * background. */
+int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
+                     const float* background, const float* records, const int32_t* tile_ranges,
+                     const int32_t* sorted_ids, const float* texture, int64_t n_texels,
+                     float* out_img, float* out_depth, float* out_reg, float* out_alpha,
+                     float* out_tex, float* out_normal, float* state, void* stream);
+/* Backward composite. Writes partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of
+ * every (tile, splat) pair and accumulates (+=) texel gradients into v_texture[n_texels][C]. */
+int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
+                     const float* background, const float* records, const int32_t* tile_ranges,
+                     const int32_t* sorted_ids, const int32_t* sorted_slots,
+                     const float* texture, int64_t n_texels, const float* state,
+                     const float* v_img, const float* v_depth, const float* v_reg,
+                     const float* v_alpha, const float* v_tex, const float* v_normal,
+                     float* partials, float* v_texture, void* stream);
+/* Sums each splat's partials and chains them to the splat parameters. Outputs are overwritten. */
+int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
+                           const float* quats, const float* opacities, const float* umap,
+                           const float* vmap, const int32_t* num_tiles_hit,
+                           const int32_t* offsets, const float* partials,
+                           const gstex_camera* cam, float* v_means, float* v_scales,
+                           float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
+                           float* v_uv0, void* stream);
+
+/* ---- spherical harmonics (degree <= 4) ------------------------------------------------- */
+int gstex_sh_fwd(int32_t n, int32_t degree, int32_t n_coeffs, const float* viewdirs,
+                 const float* coeffs, float* colors, void* stream);
+int gstex_sh_bwd(int32_t n, int32_t degree, int32_t n_coeffs, const float* viewdirs,
+                 const float* v_colors, float* v_coeffs, void* stream);
+
+/* ---- jagged texture resample ------------------------------------------------------------ */
+int gstex_texture_sample(int64_t n_query, int32_t channels, const int32_t* query_dims,
+                         const float* texture, int64_t n_texels, const float* uv, float* out,
+                         void* stream);
+int gstex_texture_sample_bwd(int64_t n_query, int32_t channels, const int32_t* query_dims,
+                             int64_t n_texels, const float* uv, const float* v_out,
+                             float* v_texture, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSTEX_HIP_H */

@@ -1,0 +1,122 @@
+"""Shared case builders: one seeded synthetic case evaluated by the CPU oracle and by the HIP path."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from gstex_amd.scene import make_scene, sphere_view
+from oracle import raster as O
+
+TOL_ABS = 1e-5  # forward parity tolerance (fp32), north_star: "within 1e-5 fp32"
+TOL_REL = 1e-5
+
+
+@dataclass
+class Case:
+    inp: O.RasterInputs
+    view: object
+    C: int
+    nth: torch.Tensor
+
+
+def make_case(n=300, n_texels=20000, H=64, W=80, seed=0, view=0, opacity=None, C=3,
+              settings=(1 << 9) | (1 << 10), bg=None, cube=2.0, glob_scale=1.0):
+    sc = make_scene(n, n_texels, channels=C, seed=seed, opacity=opacity, cube=cube)
+    v = sphere_view(view, H, W)
+    means, scales, quats, opac = sc.activated()
+    cam = O.Camera(v.viewmat, v.fx, v.fy, v.cx, v.cy, H, W, 16, v.c2w[:3, 3])
+    centers, extents = O.aabb_2d(means, scales, glob_scale, quats, cam)
+    _, depths = O.project_points(means, cam)
+    nth = O.num_tiles_hit(centers, extents, H, W)
+    uv0, umap, vmap = sc.uv_mapping()
+    g = torch.Generator().manual_seed(seed + 1000)
+    rgbs = torch.rand((n, 3), generator=g)
+    inp = O.RasterInputs(sc.texture_dims, centers.detach().clone(), extents, depths, rgbs, opac.detach().clone(),
+                         means.detach().clone(), scales.detach().clone(), glob_scale, quats.detach().clone(),
+                         uv0.detach().clone(), umap, vmap, sc.texture.clone(), cam, settings,
+                         None if bg is None else torch.tensor(bg, dtype=torch.float32))
+    return Case(inp, v, C, nth)
+
+
+DIFF = ["rgbs", "opacities", "means", "scales", "quats", "texture", "centers", "uv0"]
+
+
+def upstream(H, W, C, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    return dict(img=torch.randn(H, W, 3, generator=g), depth=torch.randn(H, W, generator=g),
+                reg=torch.randn(H, W, generator=g), alpha=torch.randn(H, W, generator=g),
+                tex=torch.randn(H, W, C, generator=g), normal=torch.randn(H, W, 3, generator=g))
+
+
+def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64):
+    inp = case.inp
+    leaves = {}
+    if grads:
+        for k in DIFF:
+            t = getattr(inp, k).detach().clone().requires_grad_(True)
+            setattr(inp, k, t)
+            leaves[k] = t
+    o32, o64, aux = O.rasterize(inp, grad_dtype=grad_dtype)
+    out = {}
+    if grads:
+        up = upstream(inp.cam.H, inp.cam.W, case.C, seed)
+        loss = sum((o64[k] * up[k].to(grad_dtype)).sum() for k in up)
+        loss.backward()
+        out = {k: (v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v).detach()).float()
+               if v.grad is None else v.grad.detach().clone() for k, v in leaves.items()}
+        for k in DIFF:
+            setattr(inp, k, getattr(inp, k).detach())
+    return o32, o64, aux, out
+
+
+def gpu_run(case: Case, grads=True, seed=5, device="cuda"):
+    import gstex_cuda
+
+    inp = case.inp
+    v = case.view
+    dv = lambda t: t.detach().to(device).contiguous()  # noqa: E731
+    t = {k: dv(getattr(inp, k)) for k in DIFF}
+    if grads:
+        for k in t:
+            t[k].requires_grad_(True)
+    n = inp.means.shape[0]
+    outs = gstex_cuda.texture_gaussians(
+        (n, 1, case.C), dv(inp.texture_dims), t["centers"], dv(inp.extents), dv(inp.depths), dv(case.nth),
+        t["rgbs"], t["opacities"], t["means"], t["scales"], inp.glob_scale, t["quats"], t["uv0"], dv(inp.umap),
+        dv(inp.vmap), t["texture"], dv(v.viewmat), dv(v.c2w), v.fx, v.fy, v.cx, v.cy, inp.cam.H, inp.cam.W, 16,
+        inp.settings, background=None if inp.background is None else dv(inp.background))
+    names = ["img", "depth", "reg", "alpha", "tex", "normal"]
+    res = {k: o.detach().cpu() for k, o in zip(names, outs)}
+    gr = {}
+    if grads:
+        up = upstream(inp.cam.H, inp.cam.W, case.C, seed)
+        torch.autograd.backward(list(outs), [up[k].to(device) for k in names])
+        gr = {k: (t[k].grad.detach().cpu() if t[k].grad is not None else torch.zeros_like(t[k]).cpu()) for k in t}
+    return res, gr
+
+
+def assert_close_fwd(gpu, ref64, names=("img", "depth", "reg", "alpha", "tex", "normal")):
+    for k in names:
+        a = gpu[k].double()
+        b = ref64[k].double()
+        err = (a - b).abs()
+        bound = TOL_ABS + TOL_REL * b.abs()
+        bad = err > bound
+        assert not bool(bad.any()), (
+            f"{k}: {int(bad.sum())} / {bad.numel()} elements outside 1e-5 (+1e-5 rel); max err {err.max().item():.3e}")
+
+
+def grad_rel_err(g, ref):
+    if ref.numel() == 0:
+        return 0.0, 0.0
+    scale = ref.abs().max().item()
+    return (g.double() - ref.double()).abs().max().item() / max(scale, 1e-12), scale
+
+
+def grad_norm_err(g, ref):
+    if ref.numel() == 0:
+        return 0.0
+    n = ref.double().norm().item()
+    return (g.double() - ref.double()).norm().item() / max(n, 1e-30)
