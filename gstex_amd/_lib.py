@@ -14,7 +14,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_void_p, c_cha
 
 import torch  # noqa: F401  (load torch's HIP runtime first)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
+LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
 REC_FLOATS = 32
 PARTIAL_FLOATS = 24

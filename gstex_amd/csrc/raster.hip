@@ -24,7 +24,11 @@ namespace {
 
 constexpr int kThreads = kTilePixels;  // 256
 constexpr int kFwdBatch = 256;
-constexpr int kBwdBatch = 64;
+#ifndef GSTEX_ABLATE
+#define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction
+#endif
+constexpr int kBwdBatch = 32;
+constexpr int kTexLds = 6144;  // floats of per-workgroup LDS texel-gradient staging (24 KiB)
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -111,7 +115,7 @@ __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
 }
 
 struct Hit {
-    float dx, dy, u, v, rho3, rho2, z, G, a_raw, alpha;
+    float dx, dy, ipz, u, v, rho3, rho2, z, G, a_raw, alpha;
     f3 k, l, p;
     bool use3;
 };
@@ -124,8 +128,9 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     h.l = f3{h.dy * r.Tw.x - r.Tv.x, h.dy * r.Tw.y - r.Tv.y, h.dy * r.Tw.z};
     h.p = cross3(h.k, h.l);
     if (h.p.z == 0.0f) return false;
-    h.u = h.p.x / h.p.z;
-    h.v = h.p.y / h.p.z;
+    h.ipz = 1.0f / h.p.z;
+    h.u = h.p.x * h.ipz;
+    h.v = h.p.y * h.ipz;
     h.rho3 = h.u * h.u + h.v * h.v;
     float dx = r.x - px, dy = r.y - py;
     h.rho2 = kFilterInvSq * (dx * dx + dy * dy);
@@ -292,6 +297,51 @@ __device__ __forceinline__ void wave_reduce24(float (&v)[kNP]) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// texel-gradient pre-reduction: along each 16-lane row (16 consecutive pixels of one image row)
+// the bilinear cell of a splat's texture forms contiguous runs, so a segmented inclusive scan
+// by cell key with DPP row shifts leaves each run's sum in its last lane; only run tails issue
+// the 4*C atomics (instead of every contributing lane, which serialised on the LDS atomic unit).
+// ------------------------------------------------------------------------------------------
+template <int OFF>
+__device__ __forceinline__ int dpp_shr_i(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, 0x110 + OFF, 0xF, 0xF, false);
+}
+template <int OFF>
+__device__ __forceinline__ float dpp_shr_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x110 + OFF, 0xF, 0xF, false));
+}
+
+template <int NV, int OFF>
+__device__ __forceinline__ void seg_step(int seg, float (&v)[NV]) {
+    const int ss = dpp_shr_i<OFF>(-1, seg);
+    const bool m = (ss == seg);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float t = dpp_shr_f<OFF>(v[i]);
+        v[i] = m ? v[i] + t : v[i];
+    }
+}
+
+// Segments = maximal runs of equal key inside a 16-lane row (a lane whose key differs from its left
+// neighbour starts a segment, so a non-contributing lane splits a run instead of being bridged).
+// Returns true for the last lane of a segment with key >= 0; it then holds the segment's sums.
+template <int NV>
+__device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
+    const int left = dpp_shr_i<1>(-7, key);
+    int seg = (left != key) ? 1 : 0;  // head flag (row start reads -7: always a head)
+    seg += dpp_shr_i<1>(0, seg);
+    seg += dpp_shr_i<2>(0, seg);
+    seg += dpp_shr_i<4>(0, seg);
+    seg += dpp_shr_i<8>(0, seg);
+    seg_step<NV, 1>(seg, v);
+    seg_step<NV, 2>(seg, v);
+    seg_step<NV, 4>(seg, v);
+    seg_step<NV, 8>(seg, v);
+    const int ns = __builtin_amdgcn_update_dpp(-1, seg, 0x101, 0xF, 0xF, false);  // row_shl:1
+    return key >= 0 && ns != seg;
+}
+
 template <int C>
 __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
@@ -307,6 +357,9 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
     __shared__ float4 s_rec[kRecF4 * kBwdBatch];
     __shared__ float s_part[kBwdBatch][4][kNP];
     __shared__ int s_slot[kBwdBatch];
+    __shared__ int s_toff[kBwdBatch];  // LDS offset of each splat's texel-gradient block (-1: global)
+    __shared__ int s_nfit, s_used;
+    __shared__ float s_tex[kTexLds];
     __shared__ int s_maxlast;
 
     const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -343,6 +396,7 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
 
     if (tid == 0) s_maxlast = -1;
+    for (int i = tid; i < kTexLds; i += kThreads) s_tex[i] = 0.f;
     __syncthreads();
     if (last >= 0) atomicMax(&s_maxlast, last);
     __syncthreads();
@@ -366,6 +420,32 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
         }
         if (tid < nb) s_slot[tid] = sorted_slots[b0 + tid];
         __syncthreads();
+        // place the batch's texel blocks in LDS: prefix of h*w*C over the batch (wave 0); splats past
+        // the capacity accumulate straight into global memory
+        if (wave == 0) {
+            int sz = 0;
+            if (lane < nb) {
+                const float4 q = s_rec[6 * kBwdBatch + lane];
+                sz = __float_as_int(q.x) * __float_as_int(q.y) * Cn;
+            }
+            int incl = sz;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            const bool fits = incl <= kTexLds;
+            if (lane < kBwdBatch) s_toff[lane] = (lane < nb && fits) ? incl - sz : -1;
+            const unsigned long long fm = __ballot(fits && lane < nb);
+            if (lane == 0) {
+                const int nfit = __popcll(fm);
+                s_nfit = nfit;
+                s_used = 0;
+            }
+            const int nfit = __popcll(fm);
+            if (nfit > 0 && lane == nfit - 1) s_used = incl;
+        }
+        __syncthreads();
 
         for (int j = nb - 1; j >= 0; --j) {
             const int rel = bb * kBwdBatch + j;
@@ -373,8 +453,21 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
 #pragma unroll
             for (int i = 0; i < kNP; ++i) P[i] = 0.f;
             bool contrib = false;
+            if (!__any(rel <= last)) {  // no lane of this wave reaches splat j
+                if ((lane & 7) == 0) {
+                    const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
+                    s_part[j][wave][base + 0] = 0.f;
+                    s_part[j][wave][base + 1] = 0.f;
+                    s_part[j][wave][base + 2] = 0.f;
+                }
+                continue;
+            }
+            const Rec r = read_rec<kBwdBatch>(s_rec, j);
+            int tkey = -1, tdi = 0, tdj = 0;
+            float tg[4 * CM];
+#pragma unroll
+            for (int i = 0; i < 4 * CM; ++i) tg[i] = 0.f;
             if (rel <= last) {
-                const Rec r = read_rec<kBwdBatch>(s_rec, j);
                 Hit h;
                 if (eval_hit(r, px, py, aa, h)) {
                     contrib = true;
@@ -430,19 +523,20 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                     P[P_NRM + 0] = w * Gn[0];
                     P[P_NRM + 1] = w * Gn[1];
                     P[P_NRM + 2] = w * Gn[2];
-                    // texel gradients (bilinear scatter)
-                    if (has_tex) {
+                    // texel gradients: per-lane bilinear contributions, scattered after the branch
+                    if (has_tex && !(GSTEX_ABLATE & 1)) {
                         const float w00 = (1.0f - b.ax) * (1.0f - b.ay), w01 = (1.0f - b.ax) * b.ay;
                         const float w10 = b.ax * (1.0f - b.ay), w11 = b.ax * b.ay;
+                        tkey = b.i0 * r.w + b.j0;
+                        tdi = b.i1 - b.i0;
+                        tdj = b.j1 - b.j0;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
-                            if (c < Cn) {
-                                const float gt = w * Gtex[c];
-                                atomicAdd(v_texture + o00 + c, gt * w00);
-                                atomicAdd(v_texture + o01 + c, gt * w01);
-                                atomicAdd(v_texture + o10 + c, gt * w10);
-                                atomicAdd(v_texture + o11 + c, gt * w11);
-                            }
+                            const float gt = (c < Cn) ? w * Gtex[c] : 0.0f;
+                            tg[c] = gt * w00;
+                            tg[CM + c] = gt * w01;
+                            tg[2 * CM + c] = gt * w10;
+                            tg[3 * CM + c] = gt * w11;
                         }
                     }
                     // depth: direct + distortion (m depends on z)
@@ -468,7 +562,7 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                         P[P_XY + 1] = drho * (2.0f * kFilterInvSq) * (r.y - py);
                         dTw.z = dz;
                     }
-                    const float ipz = 1.0f / h.p.z;
+                    const float ipz = h.ipz;
                     const f3 dp = f3{du * ipz, dv * ipz, -(du * h.u + dv * h.v) * ipz};
                     const f3 dk = cross3(h.l, dp);
                     const f3 dl = cross3(dp, h.k);
@@ -479,8 +573,31 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                     P[P_TW + 2] = dTw.z + h.dx * dk.z + h.dy * dl.z;
                 }
             }
+            if (__any(tkey >= 0)) {
+                const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
+                if (tail) {
+                    const int toff = s_toff[j];
+                    const int c00 = tkey * Cn, c01 = (tkey + tdj) * Cn;
+                    const int c10 = (tkey + tdi * r.w) * Cn, c11 = (tkey + tdi * r.w + tdj) * Cn;
+                    float* base = (toff >= 0) ? (s_tex + toff) : (v_texture + (size_t)r.off * Cn);
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) {
+                        if (c < Cn) {
+                            atomicAdd(base + c00 + c, tg[c]);
+                            atomicAdd(base + c01 + c, tg[CM + c]);
+                            atomicAdd(base + c10 + c, tg[2 * CM + c]);
+                            atomicAdd(base + c11 + c, tg[3 * CM + c]);
+                        }
+                    }
+                }
+            }
             const bool any = __any(contrib);
-            if (any) wave_reduce24(P);
+            if (GSTEX_ABLATE & 2) {
+#pragma unroll
+                for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
+            } else if (any) {
+                wave_reduce24(P);
+            }
             if ((lane & 7) == 0) {
                 const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
                 s_part[j][wave][base + 0] = any ? P[0] : 0.f;
@@ -498,6 +615,24 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                 for (int i = 0; i < 6; ++i) {
                     const int c = c0 + i;
                     dst[i] = ((s_part[j][0][c] + s_part[j][1][c]) + s_part[j][2][c]) + s_part[j][3][c];
+                }
+            }
+        }
+        // flush the staged texel gradients (only touched entries) and re-zero the staging area
+        {
+            const int used = s_used, nfit = s_nfit;
+            for (int idx = tid; idx < used; idx += kThreads) {
+                const float val = s_tex[idx];
+                if (val != 0.0f) {
+                    int lo = 0, hi = nfit - 1;  // last j with s_toff[j] <= idx
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (s_toff[mid] <= idx) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    const int off = __float_as_int(s_rec[6 * kBwdBatch + lo].z);
+                    atomicAdd(v_texture + (size_t)off * Cn + (idx - s_toff[lo]), val);
+                    s_tex[idx] = 0.0f;
                 }
             }
         }

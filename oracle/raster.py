@@ -393,8 +393,9 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions):
             d = decisions["tiles"][t]
             nz = d["nz"]
         pzs = torch.where(nz, pzc, torch.ones_like(pzc))
-        u = _div(pxc, pzs)
-        v = _div(pyc, pzs)
+        ipz = _div(_c(1.0, dtype), pzs)  # raster.hip eval_hit: one reciprocal, two products
+        u = pxc * ipz
+        v = pyc * ipz
         rho3 = u * u + v * v
         dx = g["xy"][:, None, 0] - px
         dy = g["xy"][:, None, 1] - py
