@@ -67,7 +67,8 @@ SIGNATURES = {
     ),
     "gstex_raster_bwd": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+         _P, _P],
     ),
     "gstex_raster_setup_bwd": (
         c_int32,

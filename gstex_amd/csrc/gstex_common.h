@@ -280,8 +280,51 @@ __device__ __forceinline__ Rect tile_rect(float cx, float cy, float ex, float ey
 enum RecField {
     R_TU = 0, R_TV = 3, R_TW = 6, R_XY = 9, R_OPAC = 11, R_RGB = 12, R_NRM = 15,
     R_TU0 = 18, R_AUU = 19, R_AUV = 20, R_TV0 = 21, R_AVU = 22, R_AVV = 23,
-    R_H = 24, R_W = 25, R_OFF = 26, R_GID = 27, R_XA = 28, R_YA = 29
+    R_H = 24, R_W = 25, R_OFF = 26, R_GID = 27, R_XA = 28, R_YA = 29,
+    // contribution box (pixel-centre coordinates) in the slots the anchored form leaves free
+    // (Tu'.z and Tv'.z are identically 0 and never read)
+    R_BX0 = 2, R_BX1 = 5, R_BY0 = 30, R_BY1 = 31
 };
+
+// Screen box of the projected disc u^2 + v^2 <= c2 (compute_aabb with a general cutoff).
+// Returns false when the disc reaches the camera plane (unbounded projection).
+__device__ __forceinline__ bool ellipse_box(const Homog& h, float c2, float& x0, float& x1, float& y0,
+                                            float& y1) {
+    const f3 Tu = h.Tu, Tv = h.Tv, Tw = h.Tw;
+    const float d = (c2 * (Tw.x * Tw.x) + c2 * (Tw.y * Tw.y)) - Tw.z * Tw.z;
+    if (!(d < 0.0f) || !(Tw.z > 0.0f)) return false;
+    const float fxy = c2 / d, fz = -1.0f / d;
+    const float px = (fxy * (Tu.x * Tw.x) + fxy * (Tu.y * Tw.y)) + fz * (Tu.z * Tw.z);
+    const float py = (fxy * (Tv.x * Tw.x) + fxy * (Tv.y * Tw.y)) + fz * (Tv.z * Tw.z);
+    const float qx = (fxy * (Tu.x * Tu.x) + fxy * (Tu.y * Tu.y)) + fz * (Tu.z * Tu.z);
+    const float qy = (fxy * (Tv.x * Tv.x) + fxy * (Tv.y * Tv.y)) + fz * (Tv.z * Tv.z);
+    const float ex = sqrtf(fmaxf(0.0f, px * px - qx)), ey = sqrtf(fmaxf(0.0f, py * py - qy));
+    x0 = px - ex; x1 = px + ex; y0 = py - ey; y1 = py + ey;
+    return true;
+}
+
+// Conservative box of the pixels where a splat can reach alpha >= 1/255: rho <= 2 ln(255 o) for
+// rho = u^2 + v^2 (3D disc) or 2 |pix - xy|^2 (2DGS low-pass disc); union of both, +1 px margin.
+// Rasterizer waves whose pixel block misses this box skip the splat: an exact cull (the skipped
+// pairs would fail the alpha >= 1/255 test anyway).
+__device__ __forceinline__ void contribution_box(const Homog& h, float cx, float cy, float opac, float& x0,
+                                                 float& x1, float& y0, float& y1) {
+    x0 = y0 = 3.0e38f;
+    x1 = y1 = -3.0e38f;
+    if (!(opac * 255.0f > 1.0f)) return;  // can never pass the alpha test
+    const float rm = 2.0f * logf(255.0f * opac) * 1.001f + 1e-3f;
+    const float r2 = sqrtf(0.5f * rm);
+    float ex0, ex1, ey0, ey1;
+    if (!ellipse_box(h, rm, ex0, ex1, ey0, ey1)) {
+        x0 = y0 = -3.0e38f;
+        x1 = y1 = 3.0e38f;
+        return;
+    }
+    x0 = fminf(ex0, cx - r2) - 1.0f;
+    x1 = fmaxf(ex1, cx + r2) + 1.0f;
+    y0 = fminf(ey0, cy - r2) - 1.0f;
+    y1 = fmaxf(ey1, cy + r2) + 1.0f;
+}
 
 // Partial layout (GSTEX_PARTIAL_FLOATS = 24).
 enum PartField {

@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     r[R_GID] = __int_as_float(g);
     r[R_XA] = h.xa;
     r[R_YA] = h.ya;
-    r[30] = r[31] = 0.0f;
+    contribution_box(splat_homography(cam, mu, su, sv, fr), centers[2 * g], centers[2 * g + 1], opacities[g],
+                     r[R_BX0], r[R_BX1], r[R_BY0], r[R_BY1]);
     float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
 #pragma unroll
     for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
@@ -112,6 +113,14 @@ __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
     r.h = __float_as_int(g.x); r.w = __float_as_int(g.y); r.off = __float_as_int(g.z);
     r.xa = q.x; r.ya = q.y;
     return r;
+}
+
+// Does splat j's contribution box overlap this wave's 16x4 block of pixel centres?
+template <int NB>
+__device__ __forceinline__ bool wave_overlaps(const float4* s, int j, float wx0, float wx1, float wy0, float wy1) {
+    const float bx0 = s[0 * NB + j].z, bx1 = s[1 * NB + j].y;
+    const float4 q = s[7 * NB + j];
+    return bx0 <= wx1 && bx1 >= wx0 && q.z <= wy1 && q.w >= wy0;
 }
 
 struct Hit {
@@ -173,6 +182,8 @@ __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
     const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
+    const float wx0 = (float)(tx * kTile) + 0.5f, wx1 = wx0 + (float)(kTile - 1);
+    const float wy0 = (float)(ty * kTile + 4 * (tid >> 6)) + 0.5f, wy1 = wy0 + 3.0f;
 
     float T = 1.0f;
     float img[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 0.f};
@@ -195,6 +206,7 @@ __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
         const int nb = min(kFwdBatch, rng.y - b0);
         for (int j = 0; j < nb; ++j) {
             if (done) break;
+            if (!wave_overlaps<kFwdBatch>(s_rec, j, wx0, wx1, wy0, wy1)) continue;
             const Rec r = read_rec<kFwdBatch>(s_rec, j);
             Hit h;
             if (!eval_hit(r, px, py, aa, h)) continue;
@@ -259,41 +271,47 @@ __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
 // ------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------
-// Reduce-scatter butterfly over the 64 lanes: on return, lane l with (l & 7) == 0 holds the wave
-// sums of values [12*b5 + 6*b4 + 3*b3 + 0..2] (b5,b4,b3 = bits 5,4,3 of l) in v[0..2].
+// Reduce-scatter butterfly over the 64 lanes, entirely on VALU cross-lane ops (no LDS traffic):
+// xor-32 and xor-16 halvings with v_permlane32_swap / v_permlane16_swap, xor-8 with DPP row_ror:8,
+// then an 8-lane all-reduce (quad_perm xor1, xor2, row_half_mirror).  On return, lane l with
+// (l & 7) == 0 holds the wave sums of values [12*b5 + 6*b4 + 3*b3 + 0..2] (b5,b4,b3 = bits of l).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ void wave_reduce24(float (&v)[kNP]) {
     const int lane = threadIdx.x & 63;
     {
         const bool hi = lane & 32;
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
-            float send = hi ? v[i] : v[i + 12];
-            float keep = hi ? v[i + 12] : v[i];
-            v[i] = keep + __shfl_xor(send, 32, 64);
+            auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 12]), false, false);
+            v[i] = hi ? v[i + 12] + __uint_as_float(r[0]) : v[i] + __uint_as_float(r[1]);
         }
     }
     {
         const bool hi = lane & 16;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            float send = hi ? v[i] : v[i + 6];
-            float keep = hi ? v[i + 6] : v[i];
-            v[i] = keep + __shfl_xor(send, 16, 64);
+            auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 6]), false, false);
+            v[i] = hi ? v[i + 6] + __uint_as_float(r[0]) : v[i] + __uint_as_float(r[1]);
         }
     }
     {
         const bool hi = lane & 8;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            float send = hi ? v[i] : v[i + 3];
-            float keep = hi ? v[i + 3] : v[i];
-            v[i] = keep + __shfl_xor(send, 8, 64);
+            const float send = hi ? v[i] : v[i + 3];
+            const float keep = hi ? v[i + 3] : v[i];
+            v[i] = keep + dpp_f<0x128>(send);  // row_ror:8 == lane ^ 8 inside a 16-lane row
         }
     }
 #pragma unroll
-    for (int o = 4; o >= 1; o >>= 1) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) v[i] = v[i] + __shfl_xor(v[i], o, 64);
+    for (int i = 0; i < 3; ++i) {
+        v[i] = v[i] + dpp_f<0xB1>(v[i]);   // quad_perm [1,0,3,2]
+        v[i] = v[i] + dpp_f<0x4E>(v[i]);   // quad_perm [2,3,0,1]
+        v[i] = v[i] + dpp_f<0x141>(v[i]);  // row_half_mirror: the other quad of the 8-lane group
     }
 }
 
@@ -372,6 +390,8 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
     const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
+    const float wx0 = (float)(tx * kTile) + 0.5f, wx1 = wx0 + (float)(kTile - 1);
+    const float wy0 = (float)(ty * kTile + 4 * wave) + 0.5f, wy1 = wy0 + 3.0f;
 
     float T = 1.0f, M1f = 0.f, M2f = 0.f;
     int last = -1;
@@ -401,7 +421,6 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
     if (last >= 0) atomicMax(&s_maxlast, last);
     __syncthreads();
     const int tile_last = s_maxlast;
-    const int count = rng.y - rng.x;
 
     // pairs after the last contributor of the tile receive zero gradient
     for (int p = rng.x + tile_last + 1 + tid; p < rng.y; p += kThreads) {
@@ -409,7 +428,6 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < kNP / 4; ++k) dst[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    (void)count;
 
     for (int bb = tile_last / kBwdBatch; bb >= 0 && tile_last >= 0; --bb) {
         const int b0 = rng.x + bb * kBwdBatch;
@@ -453,7 +471,8 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
 #pragma unroll
             for (int i = 0; i < kNP; ++i) P[i] = 0.f;
             bool contrib = false;
-            if (!__any(rel <= last)) {  // no lane of this wave reaches splat j
+            if (!__any(rel <= last) || !wave_overlaps<kBwdBatch>(s_rec, j, wx0, wx1, wy0, wy1)) {
+                // no lane of this wave reaches splat j, or the splat cannot pass alpha >= 1/255 here
                 if ((lane & 7) == 0) {
                     const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
                     s_part[j][wave][base + 0] = 0.f;
@@ -771,8 +790,9 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                                 const float* background, const float* records, const int32_t* tile_ranges,
                                 const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
-                                int64_t n_texels, const float* state, const float* v_img, const float* v_depth,
-                                const float* v_reg, const float* v_alpha, const float* v_tex,
+                                int64_t n_texels, const float* state, const float* out_img, const float* out_depth,
+                                const float* out_tex, const float* out_normal, const float* v_img,
+                                const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, float* partials, float* v_texture, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
@@ -788,7 +808,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     const int nblk = tiles_x * tiles_y;
 #define GSTEX_BWD(CC)                                                                                          \
     raster_bwd_kernel<CC><<<nblk, kThreads, 0, st>>>(                                                          \
-        dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,    \
+        dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         sorted_ids, sorted_slots, texture, (const float4*)state, v_img, v_depth, v_reg, v_alpha, v_tex,       \
         v_normal, partials, v_texture)
     if (channels == 3) GSTEX_BWD(3);

@@ -271,7 +271,7 @@ class _TextureGaussians(torch.autograd.Function):
              ptr(state), st)
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm, bg if bg
-                              is not None else vm)
+                              is not None else vm, img, depth, tex, normal)
         ctx.has_c2w = cw is not None
         ctx.has_bg = bg is not None
         ctx.args = (float(glob_scale), float(fx), float(fy), float(cx), float(cy), H, W, C, int(settings))
@@ -280,7 +280,7 @@ class _TextureGaussians(torch.autograd.Function):
     @staticmethod
     def backward(ctx, v_img, v_depth, v_reg, v_alpha, v_tex, v_normal):
         (means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges, sorted_ids, sorted_slots,
-         records, state, vm, cw, bg) = ctx.saved_tensors
+         records, state, vm, cw, bg, o_img, o_depth, o_tex, o_normal) = ctx.saved_tensors
         cw = cw if ctx.has_c2w else None
         bg = bg if ctx.has_bg else None
         glob, fx, fy, cx, cy, H, W, C, settings = ctx.args
@@ -302,7 +302,8 @@ class _TextureGaussians(torch.autograd.Function):
         partials = torch.empty((n_isect, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
         v_texture = torch.zeros_like(texture)
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(sorted_ids),
-             ptr(sorted_slots), ptr(texture), texture.shape[0], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg),
+             ptr(sorted_slots), ptr(texture), texture.shape[0], ptr(state), ptr(o_img), ptr(o_depth), ptr(o_tex),
+             ptr(o_normal), ptr(v_img), ptr(v_depth), ptr(v_reg),
              ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), st)
         v_means = torch.empty_like(means)
         v_scales = torch.empty_like(scales)

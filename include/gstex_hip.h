@@ -121,15 +121,17 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const int32_t* sorted_ids, const float* texture, int64_t n_texels,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                      float* out_tex, float* out_normal, float* state, void* stream);
-/* Backward composite. Writes partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of
- * every (tile, splat) pair and accumulates (+=) texel gradients into v_texture[n_texels][C]. */
+/* Backward composite. Needs the forward outputs (img, depth, tex, normal) and state. Writes
+ * partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of every (tile, splat) pair and
+ * accumulates (+=) texel gradients into v_texture[n_texels][C]. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* sorted_ids, const int32_t* sorted_slots,
                      const float* texture, int64_t n_texels, const float* state,
-                     const float* v_img, const float* v_depth, const float* v_reg,
-                     const float* v_alpha, const float* v_tex, const float* v_normal,
-                     float* partials, float* v_texture, void* stream);
+                     const float* out_img, const float* out_depth, const float* out_tex,
+                     const float* out_normal, const float* v_img, const float* v_depth,
+                     const float* v_reg, const float* v_alpha, const float* v_tex,
+                     const float* v_normal, float* partials, float* v_texture, void* stream);
 /* Sums each splat's partials and chains them to the splat parameters. Outputs are overwritten. */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                            const float* quats, const float* opacities, const float* umap,

@@ -50,12 +50,16 @@ def main():
 
     nth = run()
     torch.cuda.synchronize()
+    ops.set_kernel_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.iters):
         run()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.iters
-    print(f"fwd+bwd+preprocess {dt * 1e3:.3f} ms/iter  visible={int((nth > 0).sum())} isect={int(nth.sum())}")
+    kt = {k.replace("gstex_", ""): round(sum(v) / len(v), 3) for k, v in ops.kernel_times().items()}
+    ops.set_kernel_timing(False)
+    print(f"fwd+bwd+preprocess {dt * 1e3:.3f} ms/iter  visible={int((nth > 0).sum())} isect={int(nth.sum())} "
+          f"kernel_ms={kt}")
 
 
 if __name__ == "__main__":
