@@ -4,7 +4,11 @@ Resolves every name nerfstudio/models/gstex.py:28-32, models/jagged_texture.py:7
 scripts/exporter.py:40 import from the (un-vendored) reference extension, so those files run
 unchanged.  All compute goes through libgstex_hip.so (HIP, gfx950); see include/gstex_hip.h.
 """
-from gstex_amd.ops import (  # noqa: F401
+# Load the submodules first: importing a submodule binds its name on the package, which would
+# otherwise shadow the same-named functions (texture_sample, texture_edit) re-exported below.
+from . import _torch_impl, get_aabb_2d as _m_aabb, sh, texture, texture_edit as _m_edit  # noqa: F401
+from . import texture_sample as _m_sample  # noqa: F401
+from gstex_amd.ops import (  # noqa: F401,E402
     get_aabb_2d,
     get_num_tiles_hit_2d,
     num_sh_bases,

@@ -1,0 +1,110 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every symbol include/gstex_hip.h
+declares, and rejects invalid arguments (before any HIP call) with a status and a message."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from gstex_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gstex_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gstex_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+
+        __graft_entry__.build()
+    return _lib.load()
+
+
+def test_every_header_symbol_is_exported_and_bound(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in gstex_hip.h but not exported"
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature in gstex_amd/_lib.py"
+    assert set(_lib.SIGNATURES) == set(syms), "ctypes signatures out of sync with the header"
+
+
+def test_abi_version(lib):
+    assert lib.gstex_abi_version() == 1
+
+
+def test_workspace_size_queries(lib):
+    assert lib.gstex_scan_workspace_size(0) >= 4
+    small = lib.gstex_bin_workspace_size(100, 1000, 64)
+    big = lib.gstex_bin_workspace_size(100, 100000, 64)
+    assert big > small > 0
+    # keys (8 B) + scratch (8 B) + rank (4 B) per intersection dominate
+    assert big - small >= 20 * (100000 - 1000) - 3 * 256
+
+
+def _cam(H=32, W=32, block=16):
+    return _lib.GstexCamera(None, None, 100.0, 100.0, 16.0, 16.0, H, W, block)
+
+
+def _status(lib, name, *args):
+    rc = getattr(lib, name)(*args)
+    return rc, _lib.last_error()
+
+
+def test_bin_sort_rejects_non16_block(lib):
+    rc, msg = _status(lib, "gstex_bin_sort", 10, 10, None, None, None, None, None, 32, 32, 8, None, None, None, None,
+                      0, None)
+    assert rc == 1 and "block_width must be 16" in msg
+
+
+def test_raster_rejects_bad_channels_and_settings(lib):
+    cam = _cam()
+    rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 9, 0, None, None, None, None, None, 0, None, None,
+                      None, None, None, None, None, None)
+    assert rc == 1 and "channels" in msg
+    rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 3, 1 << 2, None, None, None, None, None, 0, None,
+                      None, None, None, None, None, None, None)
+    assert rc == 3 and "unsupported settings" in msg
+    bad = _cam(block=8)
+    rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, 0, None,
+                      None, None, None, None, None, None, None, None, None, None, None, None, None)
+    assert rc == 1 and "block_width" in msg
+
+
+def test_sh_rejects_degree(lib):
+    rc, msg = _status(lib, "gstex_sh_fwd", 4, 5, 36, None, None, None, None)
+    assert rc == 1 and "degree" in msg
+    rc, msg = _status(lib, "gstex_sh_fwd", 4, 3, 9, None, None, None, None)
+    assert rc == 1 and "coefficients" in msg
+
+
+def test_empty_inputs_are_noops(lib):
+    cam = _cam()
+    # n == 0 returns before touching the device
+    assert lib.gstex_project_points(0, None, ctypes.byref(cam), None, None, None) == 0
+    assert lib.gstex_aabb_2d(0, None, None, 1.0, None, ctypes.byref(cam), None, None, None) == 0
+    assert lib.gstex_num_tiles_hit(0, None, None, 32, 32, 16, None, None) == 0
+    assert lib.gstex_sh_fwd(0, 3, 16, None, None, None, None) == 0
+    assert lib.gstex_texture_sample(0, 3, None, None, 0, None, None, None) == 0
+
+
+def test_null_pointer_is_an_error(lib):
+    cam = _cam()
+    rc, msg = _status(lib, "gstex_project_points", 5, None, ctypes.byref(cam), None, None, None)
+    assert rc == 1 and "null" in msg
+
+
+def test_python_wrappers_refuse_cpu_tensors():
+    import torch
+
+    from gstex_amd import ops
+
+    with pytest.raises(RuntimeError, match="HIP"):
+        ops.project_points(torch.zeros(4, 3), torch.eye(4)[:3], (1.0, 1.0, 0.0, 0.0))
