@@ -44,23 +44,45 @@ def _gauss_window(size=11, sigma=1.5, device=None):
     return g / g.sum()
 
 
+_BANDS: dict = {}
+
+
+def _band(n: int, win: torch.Tensor) -> torch.Tensor:
+    """(n, n-k+1) banded matrix M with M[i+j, i] = win[j]: x @ M is the valid 1-D correlation."""
+    key = (n, win.numel(), win.device, float(win[0]))
+    m = _BANDS.get(key)
+    if m is None:
+        k = win.numel()
+        out = n - k + 1
+        m = torch.zeros(n, out, device=win.device, dtype=win.dtype)
+        idx = torch.arange(out, device=win.device)
+        for j in range(k):
+            m[idx + j, idx] = win[j]
+        _BANDS[key] = m
+    return m
+
+
 def ssim(x: torch.Tensor, y: torch.Tensor, data_range=1.0, win_size=11, sigma=1.5, K=(0.01, 0.03)) -> torch.Tensor:
     """pytorch_msssim.SSIM(data_range=1, size_average=True, channel=3) on (1,C,H,W): separable
-    gaussian window, valid convolution, mean over the map (gstex.py:351,1303)."""
-    C = x.shape[1]
-    g = _gauss_window(win_size, sigma, x.device)
-    wh = g.view(1, 1, 1, -1).repeat(C, 1, 1, 1)
-    wv = g.view(1, 1, -1, 1).repeat(C, 1, 1, 1)
+    gaussian window, valid convolution, mean over the map (gstex.py:351,1303).
 
-    def filt(t):
-        return F.conv2d(F.conv2d(t, wh, groups=C), wv, groups=C)
+    The separable valid filter runs as two banded GEMMs (hipBLASLt): MIOpen serves this depthwise
+    11-tap convolution with its naive kernels, which cost more than the whole rasterizer."""
+    H, W = x.shape[-2:]
+    g = _gauss_window(win_size, sigma, x.device)
+    bw = _band(W, g)
+    bh = _band(H, g)
+
+    def filt(t):  # (..., H, W) -> (..., H-k+1, W-k+1)
+        return torch.matmul(bh.t(), torch.matmul(t, bw))
 
     C1 = (K[0] * data_range) ** 2
     C2 = (K[1] * data_range) ** 2
-    mu1, mu2 = filt(x), filt(y)
-    s11 = filt(x * x) - mu1 * mu1
-    s22 = filt(y * y) - mu2 * mu2
-    s12 = filt(x * y) - mu1 * mu2
+    maps = filt(torch.stack([x, y, x * x, y * y, x * y], 0))
+    mu1, mu2 = maps[0], maps[1]
+    s11 = maps[2] - mu1 * mu1
+    s22 = maps[3] - mu2 * mu2
+    s12 = maps[4] - mu1 * mu2
     cs = (2 * s12 + C2) / (s11 + s22 + C2)
     sm = ((2 * mu1 * mu2 + C1) / (mu1 * mu1 + mu2 * mu2 + C1)) * cs
     return sm.mean()
