@@ -23,9 +23,22 @@ using namespace gstex;
 namespace {
 
 constexpr int kThreads = kTilePixels;  // 256
-constexpr int kFwdBatch = 256;
+#ifndef GSTEX_FWD_BATCH
+#define GSTEX_FWD_BATCH 128
+#endif
+#ifndef GSTEX_SEG_W
+#define GSTEX_SEG_W 16  // texel-gradient segment width in lanes (4, 8 or 16)
+#endif
+#ifndef GSTEX_FAST_RCP
+#define GSTEX_FAST_RCP 1  // v_rcp_f32 for backward divisions that feed no threshold decision
+#endif
+#ifndef GSTEX_BWD_MINW
+#define GSTEX_BWD_MINW 1
+#endif
+constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #ifndef GSTEX_ABLATE
-#define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction
+#define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
+                        // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch
 #endif
 constexpr int kBwdBatch = 32;
 constexpr int kTexLds = 6144;  // floats of per-workgroup LDS texel-gradient staging (24 KiB)
@@ -196,11 +209,9 @@ __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
 
     for (int b0 = rng.x; b0 < rng.y; b0 += kFwdBatch) {
         if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
-        const int idx = b0 + tid;
-        if (idx < rng.y) {
-            const float4* src = records + (size_t)sorted_ids[idx] * kRecF4;
-#pragma unroll
-            for (int k = 0; k < kRecF4; ++k) s_rec[k * kFwdBatch + tid] = src[k];
+        for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
+            const int j = q / kRecF4, k = q % kRecF4;
+            if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
         }
         __syncthreads();
         const int nb = min(kFwdBatch, rng.y - b0);
@@ -216,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
                 break;
             }
             const float w = h.alpha * T;
-            if (r.h * r.w > 0) {
+            if (r.h * r.w > 0 && !(GSTEX_ABLATE & 4)) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
                 const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
@@ -346,22 +357,33 @@ __device__ __forceinline__ void seg_step(int seg, float (&v)[NV]) {
 // Returns true for the last lane of a segment with key >= 0; it then holds the segment's sums.
 template <int NV>
 __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
+    constexpr int SW = GSTEX_SEG_W;
+    const int pos = threadIdx.x & (SW - 1);
     const int left = dpp_shr_i<1>(-7, key);
-    int seg = (left != key) ? 1 : 0;  // head flag (row start reads -7: always a head)
+    int seg = (pos == 0 || left != key) ? 1 : 0;  // head flag: group start or key change
     seg += dpp_shr_i<1>(0, seg);
     seg += dpp_shr_i<2>(0, seg);
-    seg += dpp_shr_i<4>(0, seg);
-    seg += dpp_shr_i<8>(0, seg);
+    if (SW > 4) seg += dpp_shr_i<4>(0, seg);
+    if (SW > 8) seg += dpp_shr_i<8>(0, seg);
     seg_step<NV, 1>(seg, v);
     seg_step<NV, 2>(seg, v);
-    seg_step<NV, 4>(seg, v);
-    seg_step<NV, 8>(seg, v);
+    if (SW > 4) seg_step<NV, 4>(seg, v);
+    if (SW > 8) seg_step<NV, 8>(seg, v);
     const int ns = __builtin_amdgcn_update_dpp(-1, seg, 0x101, 0xF, 0xF, false);  // row_shl:1
-    return key >= 0 && ns != seg;
+    return key >= 0 && (ns != seg || pos == SW - 1);
+}
+
+// reciprocal for values that feed no threshold decision (gradients only)
+__device__ __forceinline__ float grad_rcp(float x) {
+#if GSTEX_FAST_RCP
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
 }
 
 template <int C>
-__global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
+__global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots,
@@ -491,7 +513,7 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                 if (eval_hit(r, px, py, aa, h)) {
                     contrib = true;
                     const float one_m = 1.0f - h.alpha;
-                    T = T / one_m;
+                    T = T * grad_rcp(one_m);
                     const float w = h.alpha * T;
                     // texture value and its uv-gradient
                     float tau[CM];
@@ -511,7 +533,7 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                         const float hf = (float)r.h, wf = (float)r.w;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
-                            if (c < Cn) {
+                            if (c < Cn && !(GSTEX_ABLATE & 8)) {
                                 const float v00 = texture[o00 + c], v01 = texture[o01 + c];
                                 const float v10 = texture[o10 + c], v11 = texture[o11 + c];
                                 tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay);
@@ -523,7 +545,8 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                             }
                         }
                     }
-                    const float m = kFarRatio * (1.0f - kNear / h.z);
+                    const float iz = grad_rcp(h.z);
+                    const float m = kFarRatio * (1.0f - kNear * iz);
                     const float E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
                     float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
 #pragma unroll
@@ -560,7 +583,7 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
                     }
                     // depth: direct + distortion (m depends on z)
                     float dz = w * Gd;
-                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * (kFarRatio * kNear / (h.z * h.z));
+                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
                     float drho = 0.f;
                     if (h.a_raw < kAlphaMax) {
                         P[P_OPAC] = dL_dalpha * h.G;
@@ -594,18 +617,35 @@ __global__ __launch_bounds__(kThreads) void raster_bwd_kernel(
             }
             if (__any(tkey >= 0)) {
                 const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
-                if (tail) {
+                if (GSTEX_ABLATE & 16) {
+#pragma unroll
+                    for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
+                } else if (tail) {
+                    // keep the LDS and global paths apart: a pointer that may be either compiles to
+                    // flat atomics, several times slower than ds_add_f32 on LDS
                     const int toff = s_toff[j];
                     const int c00 = tkey * Cn, c01 = (tkey + tdj) * Cn;
                     const int c10 = (tkey + tdi * r.w) * Cn, c11 = (tkey + tdi * r.w + tdj) * Cn;
-                    float* base = (toff >= 0) ? (s_tex + toff) : (v_texture + (size_t)r.off * Cn);
+                    if (toff >= 0) {
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) {
-                        if (c < Cn) {
-                            atomicAdd(base + c00 + c, tg[c]);
-                            atomicAdd(base + c01 + c, tg[CM + c]);
-                            atomicAdd(base + c10 + c, tg[2 * CM + c]);
-                            atomicAdd(base + c11 + c, tg[3 * CM + c]);
+                        for (int c = 0; c < CM; ++c) {
+                            if (c < Cn) {
+                                atomicAdd(&s_tex[toff + c00 + c], tg[c]);
+                                atomicAdd(&s_tex[toff + c01 + c], tg[CM + c]);
+                                atomicAdd(&s_tex[toff + c10 + c], tg[2 * CM + c]);
+                                atomicAdd(&s_tex[toff + c11 + c], tg[3 * CM + c]);
+                            }
+                        }
+                    } else {
+                        float* base = v_texture + (size_t)r.off * Cn;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) {
+                            if (c < Cn) {
+                                atomicAdd(base + c00 + c, tg[c]);
+                                atomicAdd(base + c01 + c, tg[CM + c]);
+                                atomicAdd(base + c10 + c, tg[2 * CM + c]);
+                                atomicAdd(base + c11 + c, tg[3 * CM + c]);
+                            }
                         }
                     }
                 }
