@@ -57,18 +57,18 @@ SIGNATURES = {
         c_int32,
         [c_int32, c_int64, _P, _P, _P, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, c_size_t, _P],
     ),
+    "gstex_tile_order": (c_int32, [c_int32, _P, _P, _P]),
     "gstex_raster_setup": (
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
     ),
     "gstex_raster_fwd": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P],
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_bwd": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-         _P, _P],
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_setup_bwd": (
         c_int32,

@@ -257,6 +257,49 @@ __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
                      sorted_slots);
 }
 
+// 5. largest-first tile order (LPT list scheduling).  The hardware hands out workgroups in
+// blockIdx order, round-robin over the 8 XCDs; launching the heaviest tiles first keeps every XCD
+// busy until the end instead of leaving a long tail behind the image centre's deep tiles.
+constexpr int kOrderCap = 16384;  // tiles sorted in one LDS pass (64 KiB of 32-bit keys)
+constexpr int kOrderThreads = 1024;
+constexpr unsigned kOrderTileBits = 14;
+constexpr unsigned kOrderMaxCount = (1u << (32 - kOrderTileBits)) - 1;
+
+__global__ __launch_bounds__(kOrderThreads) void tile_order_kernel(int n_tiles, const int32_t* __restrict__ tile_ranges,
+                                                                   int32_t* __restrict__ tile_order) {
+    __shared__ unsigned s_key[kOrderCap];
+    if (n_tiles > kOrderCap) {  // too many tiles for one LDS sort: plain row-major order
+        for (int t = threadIdx.x; t < n_tiles; t += kOrderThreads) tile_order[t] = t;
+        return;
+    }
+    int P = 1;
+    while (P < n_tiles) P <<= 1;
+    for (int t = threadIdx.x; t < P; t += kOrderThreads) {
+        unsigned key = ~0u;
+        if (t < n_tiles) {
+            const unsigned cnt = (unsigned)min((int)kOrderMaxCount, tile_ranges[2 * t + 1] - tile_ranges[2 * t]);
+            key = ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
+        }
+        s_key[t] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < (P >> 1); p += kOrderThreads) {
+                const int i = 2 * p - (p & (j - 1)), ixj = i + j;
+                const unsigned a = s_key[i], b = s_key[ixj];
+                if ((a > b) == ((i & k) == 0)) {
+                    s_key[i] = b;
+                    s_key[ixj] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int t = threadIdx.x; t < n_tiles; t += kOrderThreads)
+        tile_order[t] = (int32_t)(s_key[t] & ((1u << kOrderTileBits) - 1));
+}
+
 struct BinWorkspace {
     int32_t* tile_count;   // n_tiles + 1 (scan output reused as tile_start)
     int32_t* tile_start;   // n_tiles + 1
@@ -344,4 +387,12 @@ extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, 
                                                        ws.scratch, centers, extents, offsets, tile_ranges,
                                                        sorted_ids, sorted_slots);
     return launch_status("gstex_bin_sort");
+}
+
+extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int32_t* tile_order, void* stream) {
+    GSTEX_REQUIRE(n_tiles >= 0, "gstex_tile_order: invalid n_tiles %d", n_tiles);
+    if (n_tiles == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(tile_ranges && tile_order, "gstex_tile_order: null pointer");
+    tile_order_kernel<<<1, kOrderThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges, tile_order);
+    return launch_status("gstex_tile_order");
 }

@@ -359,16 +359,5 @@ __device__ __forceinline__ float bilerp_mix(float v00, float v01, float v10, flo
     return (1.0f - ax) * top + ax * bot;
 }
 
-// Bijective XCD-aware block remap: the hardware deals blocks round-robin over the 8 XCDs, so
-// blocks b and b+8 share an L2. Give each XCD a contiguous run of tiles so that neighbouring
-// tiles (which share splats and texels) hit the same L2.
-__device__ __forceinline__ int xcd_swizzle(int bid, int nblocks) {
-    const int nx = 8;
-    int q = nblocks / nx, r = nblocks % nx;
-    int xcd = bid % nx, k = bid / nx;
-    // XCD x owns tiles [start(x), start(x) + q + (x < r)).
-    int start = xcd * q + min(xcd, r);
-    return start + k;
-}
 
 }  // namespace gstex

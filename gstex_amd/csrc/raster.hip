@@ -32,6 +32,29 @@ constexpr int kThreads = kTilePixels;  // 256
 #ifndef GSTEX_FAST_RCP
 #define GSTEX_FAST_RCP 1  // v_rcp_f32 for backward divisions that feed no threshold decision
 #endif
+#ifndef GSTEX_FAST_EVAL
+#define GSTEX_FAST_EVAL 0  // 1: hardware v_exp_f32 / v_rcp_f32 in the pair evaluation
+#endif
+#ifndef GSTEX_STATS
+#define GSTEX_STATS 0  // diagnostic builds: count backward work (iterations, culled, active lanes)
+#endif
+#if GSTEX_STATS
+__device__ unsigned long long g_stats[8];
+extern "C" int gstex_debug_stats(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats)) == hipSuccess ? 0 : 2;
+}
+__device__ unsigned long long g_wg[4096 * 4];
+extern "C" int gstex_debug_wg(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg), sizeof(g_wg)) == hipSuccess ? 0 : 2;
+}
+#if GSTEX_STATS == 1
+#define GSTEX_STAT(i, v) do { const unsigned long long v_ = (v); if ((threadIdx.x & 63) == 0) atomicAdd(&g_stats[i], v_); } while (0)
+#else
+#define GSTEX_STAT(i, v) do { } while (0)
+#endif
+#else
+#define GSTEX_STAT(i, v) do { } while (0)
+#endif
 #ifndef GSTEX_BWD_MINW
 #define GSTEX_BWD_MINW 1
 #endif
@@ -150,7 +173,11 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     h.l = f3{h.dy * r.Tw.x - r.Tv.x, h.dy * r.Tw.y - r.Tv.y, h.dy * r.Tw.z};
     h.p = cross3(h.k, h.l);
     if (h.p.z == 0.0f) return false;
+#if GSTEX_FAST_EVAL
+    h.ipz = __builtin_amdgcn_rcpf(h.p.z);
+#else
     h.ipz = 1.0f / h.p.z;
+#endif
     h.u = h.p.x * h.ipz;
     h.v = h.p.y * h.ipz;
     h.rho3 = h.u * h.u + h.v * h.v;
@@ -160,7 +187,11 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     float rho = h.use3 ? h.rho3 : h.rho2;
     h.z = h.use3 ? (h.u * r.Tw.x + h.v * r.Tw.y) + r.Tw.z : r.Tw.z;
     if (h.z < kNear) return false;
+#if GSTEX_FAST_EVAL
+    h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);  // exp(-rho/2) = 2^(-rho/(2 ln 2))
+#else
     h.G = expf(-0.5f * rho);
+#endif
     h.a_raw = r.opac * h.G;
     h.alpha = fminf(kAlphaMax, h.a_raw);
     return h.alpha >= kAlphaMin;
@@ -177,7 +208,7 @@ __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float
 template <int C>
 __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
-    const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
+    const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
     float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state) {
@@ -185,7 +216,7 @@ __global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
-    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x;
     const int pxi = tx * kTile + (tid & 15), pyi = ty * kTile + (tid >> 4);
@@ -385,7 +416,7 @@ __device__ __forceinline__ float grad_rcp(float x) {
 template <int C>
 __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
-    const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
+    const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots,
     const float* __restrict__ texture, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
@@ -402,7 +433,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
     __shared__ float s_tex[kTexLds];
     __shared__ int s_maxlast;
 
-    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+#if GSTEX_STATS
+    const unsigned long long t_start = wall_clock64();
+#endif
+    const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pxi = tx * kTile + (tid & 15), pyi = ty * kTile + (tid >> 4);
@@ -493,6 +527,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
 #pragma unroll
             for (int i = 0; i < kNP; ++i) P[i] = 0.f;
             bool contrib = false;
+            GSTEX_STAT(0, 1);
             if (!__any(rel <= last) || !wave_overlaps<kBwdBatch>(s_rec, j, wx0, wx1, wy0, wy1)) {
                 // no lane of this wave reaches splat j, or the splat cannot pass alpha >= 1/255 here
                 if ((lane & 7) == 0) {
@@ -651,6 +686,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
                 }
             }
             const bool any = __any(contrib);
+            GSTEX_STAT(1, 1);
+            GSTEX_STAT(2, any ? 1 : 0);
+            GSTEX_STAT(3, __popcll(__ballot(contrib)));
+            GSTEX_STAT(4, __popcll(__ballot(tkey >= 0)) ? 1 : 0);
             if (GSTEX_ABLATE & 2) {
 #pragma unroll
                 for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
@@ -697,6 +736,14 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
         }
         __syncthreads();
     }
+#if GSTEX_STATS
+    if (tid == 0 && tile < 4096) {
+        g_wg[4 * tile + 0] = t_start;
+        g_wg[4 * tile + 1] = wall_clock64();
+        g_wg[4 * tile + 2] = (unsigned)__builtin_amdgcn_s_getreg(0xF804) | ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
+        g_wg[4 * tile + 3] = (unsigned long long)(rng.y - rng.x) | ((unsigned long long)blockIdx.x << 32);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -799,8 +846,8 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
 
 extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                                 const float* background, const float* records, const int32_t* tile_ranges,
-                                const int32_t* sorted_ids, const float* texture, int64_t n_texels,
-                                float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
+                                const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
+                                int64_t n_texels, float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
                                 float* out_normal, float* state, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_fwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
@@ -818,7 +865,7 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 #define GSTEX_FWD(CC)                                                                                          \
     raster_fwd_kernel<CC><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,          \
                                                      (const float4*)records, (const int2*)tile_ranges,        \
-                                                     sorted_ids, texture, out_img, out_depth, out_reg,        \
+                                                     tile_order, sorted_ids, texture, out_img, out_depth, out_reg,        \
                                                      out_alpha, out_tex, out_normal, (float4*)state)
     if (channels == 3) GSTEX_FWD(3);
     else if (channels == 6) GSTEX_FWD(6);
@@ -829,9 +876,8 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 
 extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                                 const float* background, const float* records, const int32_t* tile_ranges,
-                                const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
-                                int64_t n_texels, const float* state, const float* out_img, const float* out_depth,
-                                const float* out_tex, const float* out_normal, const float* v_img,
+                                const int32_t* tile_order, const int32_t* sorted_ids, const int32_t* sorted_slots,
+                                const float* texture, int64_t n_texels, const float* state, const float* v_img,
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, float* partials, float* v_texture, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
@@ -849,7 +895,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
 #define GSTEX_BWD(CC)                                                                                          \
     raster_bwd_kernel<CC><<<nblk, kThreads, 0, st>>>(                                                          \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
-        sorted_ids, sorted_slots, texture, (const float4*)state, v_img, v_depth, v_reg, v_alpha, v_tex,       \
+        tile_order, sorted_ids, sorted_slots, texture, (const float4*)state, v_img, v_depth, v_reg, v_alpha, v_tex,       \
         v_normal, partials, v_texture)
     if (channels == 3) GSTEX_BWD(3);
     else if (channels == 6) GSTEX_BWD(6);

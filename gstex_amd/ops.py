@@ -216,6 +216,14 @@ def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_
     return offsets, tile_ranges, sorted_ids, sorted_slots
 
 
+def tile_order(tile_ranges: torch.Tensor) -> torch.Tensor:
+    """Largest-first raster launch order (int32 (n_tiles,)) from bin_and_sort's tile_ranges."""
+    tr = _i32(tile_ranges, "tile_ranges", (None, 2))
+    order = torch.empty((tr.shape[0],), device=tr.device, dtype=torch.int32)
+    call("gstex_tile_order", tr.shape[0], ptr(tr), ptr(order), _stream(tr))
+    return order
+
+
 # ----------------------------------------------------------------------------------------
 # texture_gaussians
 # ----------------------------------------------------------------------------------------
@@ -254,6 +262,7 @@ class _TextureGaussians(torch.autograd.Function):
 
         offsets, tile_ranges, sorted_ids, sorted_slots = bin_and_sort(
             centers_c.detach(), extents_c, depths_c, nth, H, W, BLOCK_WIDTH)
+        order = tile_order(tile_ranges)
         records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
              ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
@@ -266,12 +275,13 @@ class _TextureGaussians(torch.autograd.Function):
         tex = torch.empty((H, W, C), **f)
         normal = torch.empty((H, W, 3), **f)
         state = torch.empty((H, W, 4), **f)
-        _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(sorted_ids),
+        _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
+             ptr(sorted_ids),
              ptr(texture), texture.shape[0], ptr(img), ptr(depth), ptr(reg), ptr(alpha), ptr(tex), ptr(normal),
              ptr(state), st)
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
-                              sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm, bg if bg
-                              is not None else vm, img, depth, tex, normal)
+                              order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
+                              bg if bg is not None else vm)
         ctx.has_c2w = cw is not None
         ctx.has_bg = bg is not None
         ctx.args = (float(glob_scale), float(fx), float(fy), float(cx), float(cy), H, W, C, int(settings))
@@ -279,8 +289,8 @@ class _TextureGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, v_img, v_depth, v_reg, v_alpha, v_tex, v_normal):
-        (means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges, sorted_ids, sorted_slots,
-         records, state, vm, cw, bg, o_img, o_depth, o_tex, o_normal) = ctx.saved_tensors
+        (means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges, order, sorted_ids,
+         sorted_slots, records, state, vm, cw, bg) = ctx.saved_tensors
         cw = cw if ctx.has_c2w else None
         bg = bg if ctx.has_bg else None
         glob, fx, fy, cx, cy, H, W, C, settings = ctx.args
@@ -301,10 +311,9 @@ class _TextureGaussians(torch.autograd.Function):
         n_isect = sorted_ids.shape[0]
         partials = torch.empty((n_isect, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
         v_texture = torch.zeros_like(texture)
-        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(sorted_ids),
-             ptr(sorted_slots), ptr(texture), texture.shape[0], ptr(state), ptr(o_img), ptr(o_depth), ptr(o_tex),
-             ptr(o_normal), ptr(v_img), ptr(v_depth), ptr(v_reg),
-             ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), st)
+        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
+             ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ptr(state), ptr(v_img), ptr(v_depth),
+             ptr(v_reg), ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), st)
         v_means = torch.empty_like(means)
         v_scales = torch.empty_like(scales)
         v_quats = torch.empty_like(quats)

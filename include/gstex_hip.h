@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 1
+#define GSTEX_ABI_VERSION 2
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -105,6 +105,13 @@ int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float
                    int32_t* sorted_ids, int32_t* sorted_slots, void* workspace,
                    size_t workspace_bytes, void* stream);
 
+/* Largest-first launch order of the tiles: tile_order[n_tiles] lists the tiles by descending
+ * pair count (ties by tile index).  Pass it to gstex_raster_fwd / gstex_raster_bwd, whose
+ * workgroups the hardware dispatches in launch order round-robin over the 8 XCDs; NULL there
+ * means row-major order.  Scheduling only: outputs do not depend on it.  Above 16384 tiles the
+ * order is row-major. */
+int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int32_t* tile_order, void* stream);
+
 /* ---- rasterizer --------------------------------------------------------------------- */
 /* Builds the per-splat raster record table records[n][GSTEX_REC_FLOATS]. */
 int gstex_raster_setup(int32_t n, const float* means, const float* scales, float glob_scale,
@@ -118,18 +125,18 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
  * float[3] (or NULL = black) added as T_final * background. */
 int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
-                     const int32_t* sorted_ids, const float* texture, int64_t n_texels,
+                     const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
+                     int64_t n_texels,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                      float* out_tex, float* out_normal, float* state, void* stream);
-/* Backward composite. Needs the forward outputs (img, depth, tex, normal) and state. Writes
+/* Backward composite. Needs the forward state and the same tile_order. Writes
  * partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of every (tile, splat) pair and
  * accumulates (+=) texel gradients into v_texture[n_texels][C]. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
-                     const int32_t* sorted_ids, const int32_t* sorted_slots,
-                     const float* texture, int64_t n_texels, const float* state,
-                     const float* out_img, const float* out_depth, const float* out_tex,
-                     const float* out_normal, const float* v_img, const float* v_depth,
+                     const int32_t* tile_order, const int32_t* sorted_ids,
+                     const int32_t* sorted_slots, const float* texture, int64_t n_texels,
+                     const float* state, const float* v_img, const float* v_depth,
                      const float* v_reg, const float* v_alpha, const float* v_tex,
                      const float* v_normal, float* partials, float* v_texture, void* stream);
 /* Sums each splat's partials and chains them to the splat parameters. Outputs are overwritten. */

@@ -177,6 +177,44 @@ def test_backward_is_deterministic():
         assert torch.equal(g1[k], g2[k]), f"{k} gradient not bitwise reproducible"
 
 
+
+# ---------------------------------------------------------------- launch order (scheduling only)
+@pytest.mark.parametrize("n_tiles", [1, 2500, 16384, 16385])
+def test_tile_order_is_largest_first(n_tiles):
+    from gstex_amd.ops import tile_order
+
+    g = np.random.default_rng(n_tiles)
+    counts = g.integers(0, 40, n_tiles)
+    counts[g.integers(0, n_tiles, max(1, n_tiles // 50))] = 1 << 19  # beyond the 2^18-1 clamp: ties
+    ends = np.cumsum(counts)
+    tr = np.stack([ends - counts, ends], 1).astype(np.int64)
+    tr = np.clip(tr, 0, 2**31 - 1).astype(np.int32)
+    got = tile_order(torch.from_numpy(tr).to(DEV)).cpu().numpy()
+    if n_tiles > 16384:
+        assert np.array_equal(got, np.arange(n_tiles)), "above 16384 tiles the order is row-major"
+        return
+    cnt = np.minimum(tr[:, 1] - tr[:, 0], (1 << 18) - 1)
+    expect = np.lexsort((np.arange(n_tiles), -cnt))
+    assert np.array_equal(got, expect)
+
+
+def test_outputs_independent_of_launch_order(monkeypatch):
+    from gstex_amd import ops
+
+    case = make_case(n=400, n_texels=20000, H=80, W=96, seed=13)
+    f1, g1 = gpu_run(case, grads=True)
+    monkeypatch.setattr(ops, "tile_order",
+                        lambda tr: torch.arange(tr.shape[0], device=tr.device, dtype=torch.int32).flip(0))
+    f2, g2 = gpu_run(case, grads=True)
+    for k in f1:
+        assert torch.equal(f1[k], f2[k]), k
+    for k in ["rgbs", "opacities", "means", "scales", "quats", "centers", "uv0"]:
+        assert torch.equal(g1[k], g2[k]), k
+    # texel gradients sum over tiles with float atomics: equal up to summation order
+    t1, t2 = g1["texture"].double(), g2["texture"].double()
+    assert float((t1 - t2).abs().max()) <= 1e-6 * float(t1.abs().max())
+
+
 # ---------------------------------------------------------------- SH / texture_sample
 @pytest.mark.parametrize("degree", [0, 1, 2, 3, 4])
 def test_sh_parity(degree):
