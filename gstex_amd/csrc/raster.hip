@@ -55,8 +55,16 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #else
 #define GSTEX_STAT(i, v) do { } while (0)
 #endif
-#ifndef GSTEX_BWD_MINW
-#define GSTEX_BWD_MINW 1
+#ifndef GSTEX_REC_SGPR
+#define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
+#endif
+#ifndef GSTEX_BWD_WAVES
+#define GSTEX_BWD_WAVES 0  // >0: ask the register allocator for this many waves per SIMD
+#endif
+#if GSTEX_BWD_WAVES > 0
+#define GSTEX_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSTEX_BWD_WAVES, GSTEX_BWD_WAVES)))
+#else
+#define GSTEX_BWD_ATTR
 #endif
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #ifndef GSTEX_ABLATE
@@ -64,7 +72,7 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch
 #endif
 constexpr int kBwdBatch = 32;
-constexpr int kTexLds = 6144;  // floats of per-workgroup LDS texel-gradient staging (24 KiB)
+constexpr int kTexLds = 6016;  // floats of per-workgroup LDS texel-gradient staging (23.5 KiB: four workgroups per CU)
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -134,10 +142,23 @@ struct Rec {
     float xa, ya;
 };
 
-template <int NB>
+template <bool SGPR>
+__device__ __forceinline__ float4 uni4(float4 v) {  // wave-uniform value -> SGPRs
+    if (!SGPR) return v;
+    return make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
+                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
+                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
+                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w))));
+}
+
+// SGPR: move the (wave-uniform) record into scalar registers; frees ~30 VGPRs where the register
+// file, not issue, limits occupancy (backward), at the cost of one v_readfirstlane per value
+template <int NB, bool SGPR = false>
 __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
-    float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], d = s[3 * NB + j];
-    float4 e = s[4 * NB + j], f = s[5 * NB + j], g = s[6 * NB + j], q = s[7 * NB + j];
+    const float4 a = uni4<SGPR>(s[0 * NB + j]), b = uni4<SGPR>(s[1 * NB + j]);
+    const float4 c = uni4<SGPR>(s[2 * NB + j]), d = uni4<SGPR>(s[3 * NB + j]);
+    const float4 e = uni4<SGPR>(s[4 * NB + j]), f = uni4<SGPR>(s[5 * NB + j]);
+    const float4 g = uni4<SGPR>(s[6 * NB + j]), q = uni4<SGPR>(s[7 * NB + j]);
     Rec r;
     r.Tu = f3{a.x, a.y, a.z};
     r.Tv = f3{a.w, b.x, b.y};
@@ -414,7 +435,7 @@ __device__ __forceinline__ float grad_rcp(float x) {
 }
 
 template <int C>
-__global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
+__global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots,
@@ -538,11 +559,11 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
                 }
                 continue;
             }
-            const Rec r = read_rec<kBwdBatch>(s_rec, j);
-            int tkey = -1, tdi = 0, tdj = 0;
-            float tg[4 * CM];
-#pragma unroll
-            for (int i = 0; i < 4 * CM; ++i) tg[i] = 0.f;
+            const Rec r = read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
+            // texel-gradient inputs, expanded into the 4*C bilinear contributions after P is reduced:
+            // tkey = top-left texel of the block | (i1 - i0) << 29 | (j1 - j0) << 30, -1 if none
+            int tkey = -1;
+            float tw = 0.f, tax = 0.f, tay = 0.f;
             if (rel <= last) {
                 Hit h;
                 if (eval_hit(r, px, py, aa, h)) {
@@ -602,19 +623,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
                     P[P_NRM + 2] = w * Gn[2];
                     // texel gradients: per-lane bilinear contributions, scattered after the branch
                     if (has_tex && !(GSTEX_ABLATE & 1)) {
-                        const float w00 = (1.0f - b.ax) * (1.0f - b.ay), w01 = (1.0f - b.ax) * b.ay;
-                        const float w10 = b.ax * (1.0f - b.ay), w11 = b.ax * b.ay;
-                        tkey = b.i0 * r.w + b.j0;
-                        tdi = b.i1 - b.i0;
-                        tdj = b.j1 - b.j0;
-#pragma unroll
-                        for (int c = 0; c < CM; ++c) {
-                            const float gt = (c < Cn) ? w * Gtex[c] : 0.0f;
-                            tg[c] = gt * w00;
-                            tg[CM + c] = gt * w01;
-                            tg[2 * CM + c] = gt * w10;
-                            tg[3 * CM + c] = gt * w11;
-                        }
+                        tkey = (b.i0 * r.w + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
+                        tw = w;
+                        tax = b.ax;
+                        tay = b.ay;
                     }
                     // depth: direct + distortion (m depends on z)
                     float dz = w * Gd;
@@ -650,8 +662,53 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
                     P[P_TW + 2] = dTw.z + h.dx * dk.z + h.dy * dl.z;
                 }
             }
+            const bool any = __any(contrib);
+            GSTEX_STAT(1, 1);
+            GSTEX_STAT(2, any ? 1 : 0);
+            GSTEX_STAT(3, __popcll(__ballot(contrib)));
+            GSTEX_STAT(4, __popcll(__ballot(tkey >= 0)) ? 1 : 0);
+            if (GSTEX_ABLATE & 2) {
+#pragma unroll
+                for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
+            } else if (any) {
+                wave_reduce24(P);
+            }
+            if ((lane & 7) == 0) {
+                const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
+                s_part[j][wave][base + 0] = any ? P[0] : 0.f;
+                s_part[j][wave][base + 1] = any ? P[1] : 0.f;
+                s_part[j][wave][base + 2] = any ? P[2] : 0.f;
+            }
             if (__any(tkey >= 0)) {
+                float tg[4 * CM];
+                {
+                    const float w00 = (1.0f - tax) * (1.0f - tay), w01 = (1.0f - tax) * tay;
+                    const float w10 = tax * (1.0f - tay), w11 = tax * tay;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) {
+                        const float gt = (c < Cn) ? tw * Gtex[c] : 0.0f;
+                        tg[c] = gt * w00;
+                        tg[CM + c] = gt * w01;
+                        tg[2 * CM + c] = gt * w10;
+                        tg[3 * CM + c] = gt * w11;
+                    }
+                }
                 const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
+#if GSTEX_STATS == 1
+                {
+                    unsigned long long tm = __ballot(tail), seen = 0ull;
+                    int distinct = 0;
+                    while (tm & ~seen) {
+                        const int b = __ffsll((long long)(tm & ~seen)) - 1;
+                        const int kb = __shfl(tkey, b, 64);
+                        seen |= __ballot(tail && tkey == kb);
+                        ++distinct;
+                    }
+                    GSTEX_STAT(5, __popcll(tm));
+                    GSTEX_STAT(6, distinct);
+                    GSTEX_STAT(7, 1);
+                }
+#endif
                 if (GSTEX_ABLATE & 16) {
 #pragma unroll
                     for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
@@ -659,8 +716,9 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
                     // keep the LDS and global paths apart: a pointer that may be either compiles to
                     // flat atomics, several times slower than ds_add_f32 on LDS
                     const int toff = s_toff[j];
-                    const int c00 = tkey * Cn, c01 = (tkey + tdj) * Cn;
-                    const int c10 = (tkey + tdi * r.w) * Cn, c11 = (tkey + tdi * r.w + tdj) * Cn;
+                    const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
+                    const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
+                    const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
                     if (toff >= 0) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
@@ -684,23 +742,6 @@ __global__ __launch_bounds__(kThreads, GSTEX_BWD_MINW) void raster_bwd_kernel(
                         }
                     }
                 }
-            }
-            const bool any = __any(contrib);
-            GSTEX_STAT(1, 1);
-            GSTEX_STAT(2, any ? 1 : 0);
-            GSTEX_STAT(3, __popcll(__ballot(contrib)));
-            GSTEX_STAT(4, __popcll(__ballot(tkey >= 0)) ? 1 : 0);
-            if (GSTEX_ABLATE & 2) {
-#pragma unroll
-                for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
-            } else if (any) {
-                wave_reduce24(P);
-            }
-            if ((lane & 7) == 0) {
-                const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
-                s_part[j][wave][base + 0] = any ? P[0] : 0.f;
-                s_part[j][wave][base + 1] = any ? P[1] : 0.f;
-                s_part[j][wave][base + 2] = any ? P[2] : 0.f;
             }
         }
         __syncthreads();
