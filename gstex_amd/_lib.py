@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_void_p, c_char_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_size_t, c_void_p
 
 import torch  # noqa: F401  (load torch's HIP runtime first)
 
@@ -38,6 +38,19 @@ class GstexCamera(ctypes.Structure):
     ]
 
 
+class GstexAdamTensor(ctypes.Structure):
+    _fields_ = [
+        ("param", c_void_p),
+        ("grad", c_void_p),
+        ("exp_avg", c_void_p),
+        ("exp_avg_sq", c_void_p),
+        ("numel", c_int64),
+        ("step_size", c_float),
+        ("bias_correction2_sqrt", c_float),
+    ]
+
+
+ADAM_MAX_TENSORS = 16
 _P = c_void_p
 _CAM = POINTER(GstexCamera)
 
@@ -78,6 +91,7 @@ SIGNATURES = {
     "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_texture_sample": (c_int32, [c_int64, c_int32, _P, _P, c_int64, _P, _P, _P]),
     "gstex_texture_sample_bwd": (c_int32, [c_int64, c_int32, _P, c_int64, _P, _P, _P, _P]),
+    "gstex_adam_step": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, _P]),
 }
 
 _lib = None

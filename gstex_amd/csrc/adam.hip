@@ -1,0 +1,109 @@
+// adam.hip — one-launch multi-tensor Adam for the GStex parameter groups.
+//
+//   gstex_adam_step   <- torch.optim.Adam(eps=1e-15) over the 7 GStex parameter groups
+//                        (gstex_configs.py:207-244 via engine/optimizers.py:158-171).
+//
+// Per element, in torch's foreach-Adam order (torch/optim/adam.py _multi_tensor_adam):
+//   m = lerp(m, g, 1 - beta1)                      m + (1-beta1) * (g - m)
+//   v = v * beta2 + (1 - beta2) * (g * g)
+//   p = p - step_size * m / (sqrt(v) / sqrt(bc2) + eps),  step_size = lr / bc1
+// with bc1 = 1 - beta1^t, bc2 = 1 - beta2^t computed on the host per tensor (each tensor keeps its
+// own step count: the texel store restarts at t = 1 after every rechart, gstex.py:812-815).
+// HBM-bound: 16 B read + 12 B written per element, float4 vectorised, one launch for all tensors.
+#include "gstex_common.h"
+#include "gstex_error.h"
+
+namespace {
+
+constexpr int kAdamThreads = 256;
+constexpr int kAdamPerBlock = kAdamThreads * 4 * 4;  // 4 float4 per thread
+constexpr int kAdamMaxTensors = GSTEX_ADAM_MAX_TENSORS;
+
+struct AdamArgs {
+    gstex_adam_tensor t[kAdamMaxTensors];
+    int64_t block_start[kAdamMaxTensors + 1];
+    int n;
+    float beta1, beta2, eps, one_m_beta1, one_m_beta2;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1w, float b2,
+                                          float one_m_b2, float eps, float neg_step, float bc2_sqrt) {
+    m = m + b1w * (g - m);
+    v = v * b2 + one_m_b2 * (g * g);
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + neg_step * (m / denom);
+}
+
+__global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
+    const int64_t b = blockIdx.x;
+    int k = 0;
+    while (k + 1 < a.n && a.block_start[k + 1] <= b) ++k;
+    const gstex_adam_tensor& t = a.t[k];
+    const int64_t base = (b - a.block_start[k]) * kAdamPerBlock;
+    const float neg_step = -t.step_size, bc2s = t.bias_correction2_sqrt;
+    const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
+                       reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
+    if (vec) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t i = base + 4 * ((int64_t)r * kAdamThreads + threadIdx.x);
+            if (i + 3 < t.numel) {
+                float4 p = *reinterpret_cast<const float4*>(t.param + i);
+                const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
+                float4 m = *reinterpret_cast<const float4*>(t.exp_avg + i);
+                float4 v = *reinterpret_cast<const float4*>(t.exp_avg_sq + i);
+                adam_elem(p.x, g.x, m.x, v.x, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem(p.y, g.y, m.y, v.y, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem(p.z, g.z, m.z, v.z, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem(p.w, g.w, m.w, v.w, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                *reinterpret_cast<float4*>(t.param + i) = p;
+                *reinterpret_cast<float4*>(t.exp_avg + i) = m;
+                *reinterpret_cast<float4*>(t.exp_avg_sq + i) = v;
+            } else {
+                for (int64_t e = i; e < t.numel; ++e)
+                    adam_elem(t.param[e], t.grad[e], t.exp_avg[e], t.exp_avg_sq[e], a.one_m_beta1, a.beta2,
+                              a.one_m_beta2, a.eps, neg_step, bc2s);
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < kAdamPerBlock; e += kAdamThreads) {
+            const int64_t i = base + e;
+            if (i < t.numel)
+                adam_elem(t.param[i], t.grad[i], t.exp_avg[i], t.exp_avg_sq[i], a.one_m_beta1, a.beta2,
+                          a.one_m_beta2, a.eps, neg_step, bc2s);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                               double eps, void* stream) {
+    GSTEX_REQUIRE(n_tensors >= 0 && n_tensors <= kAdamMaxTensors,
+                  "gstex_adam_step: n_tensors must be in [0, %d] (got %d)", kAdamMaxTensors, n_tensors);
+    GSTEX_REQUIRE(n_tensors == 0 || tensors, "gstex_adam_step: null tensor table");
+    AdamArgs a{};
+    int64_t blocks = 0;
+    int k = 0;
+    for (int i = 0; i < n_tensors; ++i) {
+        const gstex_adam_tensor& t = tensors[i];
+        GSTEX_REQUIRE(t.numel >= 0, "gstex_adam_step: tensor %d has numel < 0", i);
+        if (t.numel == 0) continue;
+        GSTEX_REQUIRE(t.param && t.grad && t.exp_avg && t.exp_avg_sq, "gstex_adam_step: tensor %d: null pointer", i);
+        a.t[k] = t;
+        a.block_start[k] = blocks;
+        blocks += (t.numel + kAdamPerBlock - 1) / kAdamPerBlock;
+        ++k;
+    }
+    if (k == 0) return GSTEX_OK;
+    a.block_start[k] = blocks;
+    a.n = k;
+    // scalars rounded to fp32 from double, as torch passes its python-float hyper-parameters
+    a.beta1 = (float)beta1;
+    a.beta2 = (float)beta2;
+    a.eps = (float)eps;
+    a.one_m_beta1 = (float)(1.0 - beta1);
+    a.one_m_beta2 = (float)(1.0 - beta2);
+    adam_kernel<<<(unsigned)blocks, kAdamThreads, 0, gstex::as_stream(stream)>>>(a);
+    return gstex::launch_status("gstex_adam_step");
+}

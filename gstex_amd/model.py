@@ -11,6 +11,7 @@ Reproduces the parts of the reference's GStexModel that sit either side of the h
   * background composite             gstex.py:1204-1205
   * loss 0.8 L1 + 0.2 (1 - SSIM)     gstex.py:1301-1322 (pytorch_msssim SSIM semantics)
   * per-group Adam, eps 1e-15        gstex_configs.py:207-244, engine/optimizers.py:158-171
+                                     (one fused HIP launch, gstex_amd.optim.FusedAdam)
 The rechart every 100 steps (gstex.py:890-914) is provided by `recharge()`.
 """
 from __future__ import annotations
@@ -22,6 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
+from .optim import FusedAdam
 from .charts import SH2RGB, build_charts, get_uv_mapping, texture_dims_to_query
 from .scene import Scene, View
 
@@ -98,7 +100,7 @@ class GStexTrainer:
     """Holds the GStex parameters on one device and runs forward/backward/Adam steps."""
 
     def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
-                 pixel_num: float | None = None, background=(1.0, 1.0, 1.0)):
+                 pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -118,6 +120,7 @@ class GStexTrainer:
         self.pixel_num = pixel_num if pixel_num is not None else float(scene.texture.shape[0])
         self.background = torch.tensor(background, dtype=torch.float32, device=d)
         self.step = 0
+        self.fused_adam = fused_adam
         self._build_optimizer()
 
     # ------------------------------------------------------------------ parameters
@@ -137,7 +140,10 @@ class GStexTrainer:
 
     def _build_optimizer(self):
         groups = [{"params": ps, "lr": LRS[name], "name": name} for name, ps in self.param_groups().items()]
-        self.optimizer = torch.optim.Adam(groups, eps=1e-15, foreach=True)
+        if self.fused_adam:
+            self.optimizer = FusedAdam(groups, eps=1e-15)
+        else:
+            self.optimizer = torch.optim.Adam(groups, eps=1e-15, foreach=True)
 
     # ------------------------------------------------------------------ forward
     def render(self, view: View, sh_degree_now: int | None = None):

@@ -1,0 +1,62 @@
+"""Fused multi-tensor Adam (``gstex_adam_step``) for the GStex parameter groups.
+
+Drop-in for the reference's ``torch.optim.Adam(params, lr, eps=1e-15)`` per group
+(gstex_configs.py:207-244, engine/optimizers.py:158-171): the same update, the same
+per-parameter ``state`` ({"step", "exp_avg", "exp_avg_sq"}) and ``param_groups``, so code that resets a
+parameter's moments (the rechart, gstex.py:799-826) keeps working.  All parameters of all groups are
+updated by one HIP launch (16 tensors per launch) instead of torch's ~7 foreach passes.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        if lr < 0 or eps < 0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        # one launch per (betas, eps, device, stream) family; the GStex groups all share them
+        batches: dict = {}
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad
+                if g.is_sparse:
+                    raise RuntimeError("FusedAdam does not support sparse gradients")
+                if p.dtype != torch.float32 or g.dtype != torch.float32 or not p.is_cuda:
+                    raise TypeError("FusedAdam: fp32 CUDA parameters and gradients only")
+                if not (p.is_contiguous() and g.is_contiguous()):
+                    raise ValueError("FusedAdam: parameters and gradients must be contiguous")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["step"] += 1
+                t = st["step"]
+                # python-double bias corrections, rounded to fp32 exactly where torch's foreach Adam does
+                step_size = group["lr"] / (1.0 - b1 ** t)
+                bc2_sqrt = (1.0 - b2 ** t) ** 0.5
+                desc = _lib.GstexAdamTensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                            st["exp_avg_sq"].data_ptr(), p.numel(), step_size, bc2_sqrt)
+                key = (b1, b2, group["eps"], p.device)
+                batches.setdefault(key, []).append((desc, p))
+        for (b1, b2, eps, dev), items in batches.items():
+            st = _lib.stream_of(dev)
+            for i in range(0, len(items), _lib.ADAM_MAX_TENSORS):
+                chunk = items[i:i + _lib.ADAM_MAX_TENSORS]
+                arr = (_lib.GstexAdamTensor * len(chunk))(*[d for d, _ in chunk])
+                _lib.call("gstex_adam_step", len(chunk), arr, float(b1), float(b2), float(eps), st)
+        return loss

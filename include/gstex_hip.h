@@ -162,6 +162,24 @@ int gstex_texture_sample_bwd(int64_t n_query, int32_t channels, const int32_t* q
                              int64_t n_texels, const float* uv, const float* v_out,
                              float* v_texture, void* stream);
 
+/* ---- optimizer (train-step support) ----------------------------------- */
+/* One launch of torch.optim.Adam (no weight decay, no amsgrad) over up to GSTEX_ADAM_MAX_TENSORS
+ * fp32 tensors.  Per tensor the host supplies step_size = lr / (1 - beta1^t) and
+ * bias_correction2_sqrt = sqrt(1 - beta2^t) for that tensor's own step t.  Updates param,
+ * exp_avg and exp_avg_sq in place. */
+#define GSTEX_ADAM_MAX_TENSORS 16
+typedef struct gstex_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    float step_size;
+    float bias_correction2_sqrt;
+} gstex_adam_tensor;
+int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                    double eps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,7 +29,7 @@ def lib():
 
 def test_every_header_symbol_is_exported_and_bound(lib):
     syms = declared_symbols()
-    assert len(syms) >= 20
+    assert len(syms) >= 21
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in gstex_hip.h but not exported"
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature in gstex_amd/_lib.py"
@@ -108,3 +108,15 @@ def test_python_wrappers_refuse_cpu_tensors():
 
     with pytest.raises(RuntimeError, match="HIP"):
         ops.project_points(torch.zeros(4, 3), torch.eye(4)[:3], (1.0, 1.0, 0.0, 0.0))
+
+
+def test_adam_rejects_bad_tables(lib):
+    from gstex_amd import _lib
+
+    rc, msg = _status(lib, "gstex_adam_step", 17, None, 0.9, 0.999, 1e-15, None)
+    assert rc == 1 and "n_tensors" in msg
+    t = (_lib.GstexAdamTensor * 1)(_lib.GstexAdamTensor(None, None, None, None, 10, 1e-3, 1.0))
+    rc, msg = _status(lib, "gstex_adam_step", 1, t, 0.9, 0.999, 1e-15, None)
+    assert rc == 1 and "null pointer" in msg
+    t = (_lib.GstexAdamTensor * 1)(_lib.GstexAdamTensor(None, None, None, None, 0, 1e-3, 1.0))
+    assert _status(lib, "gstex_adam_step", 1, t, 0.9, 0.999, 1e-15, None)[0] == 0  # empty: no launch
