@@ -55,14 +55,24 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #else
 #define GSTEX_STAT(i, v) do { } while (0)
 #endif
+#ifndef GSTEX_FWD_WAVES
+#define GSTEX_FWD_WAVES 0
+#endif
+#if GSTEX_FWD_WAVES > 0
+#define GSTEX_FWD_ATTR __attribute__((amdgpu_num_vgpr((512 / GSTEX_FWD_WAVES) / 8 * 8 / 2)))
+#else
+#define GSTEX_FWD_ATTR
+#endif
 #ifndef GSTEX_REC_SGPR
 #define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
 #endif
 #ifndef GSTEX_BWD_WAVES
-#define GSTEX_BWD_WAVES 0  // >0: ask the register allocator for this many waves per SIMD
+#define GSTEX_BWD_WAVES 4  // register cap for this many waves per SIMD (a few scratch spills)
 #endif
 #if GSTEX_BWD_WAVES > 0
-#define GSTEX_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSTEX_BWD_WAVES, GSTEX_BWD_WAVES)))
+// gfx950's unified register file: the amdgpu_num_vgpr budget is doubled (arch VGPRs + AGPRs), so a
+// cap of 512/waves registers (allocation granule 8) is requested as half that
+#define GSTEX_BWD_ATTR __attribute__((amdgpu_num_vgpr((512 / GSTEX_BWD_WAVES) / 8 * 8 / 2)))
 #else
 #define GSTEX_BWD_ATTR
 #endif
@@ -71,8 +81,14 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch
 #endif
-constexpr int kBwdBatch = 32;
-constexpr int kTexLds = 6016;  // floats of per-workgroup LDS texel-gradient staging (23.5 KiB: four workgroups per CU)
+#ifndef GSTEX_BWD_BATCH
+#define GSTEX_BWD_BATCH 32
+#endif
+constexpr int kBwdBatch = GSTEX_BWD_BATCH;
+#ifndef GSTEX_TEX_LDS
+#define GSTEX_TEX_LDS 6016
+#endif
+constexpr int kTexLds = GSTEX_TEX_LDS;  // floats of per-workgroup LDS texel-gradient staging (23.5 KiB: four workgroups per CU)
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -227,7 +243,7 @@ __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float
 // forward
 // ------------------------------------------------------------------------------------------
 template <int C>
-__global__ __launch_bounds__(kThreads) void raster_fwd_kernel(
+__global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float* __restrict__ out_img,
@@ -453,6 +469,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     __shared__ int s_nfit, s_used;
     __shared__ float s_tex[kTexLds];
     __shared__ int s_maxlast;
+    __shared__ unsigned s_live[4];  // per wave: batch splats whose s_part row this wave wrote
 
 #if GSTEX_STATS
     const unsigned long long t_start = wall_clock64();
@@ -498,6 +515,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     if (last >= 0) atomicMax(&s_maxlast, last);
     __syncthreads();
     const int tile_last = s_maxlast;
+    int wave_last = last;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wave_last = max(wave_last, __shfl_xor(wave_last, o, 64));
+    wave_last = __builtin_amdgcn_readfirstlane(wave_last);
 
     // pairs after the last contributor of the tile receive zero gradient
     for (int p = rng.x + tile_last + 1 + tid; p < rng.y; p += kThreads) {
@@ -542,23 +563,24 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         }
         __syncthreads();
 
-        for (int j = nb - 1; j >= 0; --j) {
+        // the batch splats this wave must visit, tested all at once (lane j <-> splat j): some lane
+        // of the wave reaches it (rel <= last) and its contribution box meets the wave's 16x4 block
+        unsigned todo;
+        {
+            const bool need = lane < nb && bb * kBwdBatch + lane <= wave_last &&
+                              wave_overlaps<kBwdBatch>(s_rec, lane < nb ? lane : 0, wx0, wx1, wy0, wy1);
+            todo = (unsigned)__ballot(need);
+        }
+        unsigned live = 0u;
+        GSTEX_STAT(0, nb);
+        while (todo) {
+            const int j = 31 - __builtin_clz(todo);
+            todo &= ~(1u << j);
             const int rel = bb * kBwdBatch + j;
             float P[kNP];
 #pragma unroll
             for (int i = 0; i < kNP; ++i) P[i] = 0.f;
             bool contrib = false;
-            GSTEX_STAT(0, 1);
-            if (!__any(rel <= last) || !wave_overlaps<kBwdBatch>(s_rec, j, wx0, wx1, wy0, wy1)) {
-                // no lane of this wave reaches splat j, or the splat cannot pass alpha >= 1/255 here
-                if ((lane & 7) == 0) {
-                    const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
-                    s_part[j][wave][base + 0] = 0.f;
-                    s_part[j][wave][base + 1] = 0.f;
-                    s_part[j][wave][base + 2] = 0.f;
-                }
-                continue;
-            }
             const Rec r = read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
             // texel-gradient inputs, expanded into the 4*C bilinear contributions after P is reduced:
             // tkey = top-left texel of the block | (i1 - i0) << 29 | (j1 - j0) << 30, -1 if none
@@ -578,20 +600,22 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     for (int c = 0; c < CM; ++c) tau[c] = 0.f;
                     const bool has_tex = r.h * r.w > 0;
                     Bilerp b;
-                    size_t o00 = 0, o01 = 0, o10 = 0, o11 = 0;
+                    // wave-uniform block base (scalar) + 32-bit per-lane offsets
+                    const float* tblk = texture + (size_t)r.off * Cn;
+                    int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
                     if (has_tex) {
                         tex_coords(r, h.u, h.v, tu, tv);
                         b = bilerp_coords(tu, tv, r.h, r.w);
-                        o00 = (size_t)(r.off + b.i0 * r.w + b.j0) * Cn;
-                        o01 = (size_t)(r.off + b.i0 * r.w + b.j1) * Cn;
-                        o10 = (size_t)(r.off + b.i1 * r.w + b.j0) * Cn;
-                        o11 = (size_t)(r.off + b.i1 * r.w + b.j1) * Cn;
+                        o00 = (b.i0 * r.w + b.j0) * Cn;
+                        o01 = (b.i0 * r.w + b.j1) * Cn;
+                        o10 = (b.i1 * r.w + b.j0) * Cn;
+                        o11 = (b.i1 * r.w + b.j1) * Cn;
                         const float hf = (float)r.h, wf = (float)r.w;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn && !(GSTEX_ABLATE & 8)) {
-                                const float v00 = texture[o00 + c], v01 = texture[o01 + c];
-                                const float v10 = texture[o10 + c], v11 = texture[o11 + c];
+                                const float v00 = tblk[o00 + c], v01 = tblk[o01 + c];
+                                const float v10 = tblk[o10 + c], v11 = tblk[o11 + c];
                                 tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay);
                                 const float gt = w * Gtex[c];
                                 if (b.in_u)
@@ -666,18 +690,21 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             GSTEX_STAT(1, 1);
             GSTEX_STAT(2, any ? 1 : 0);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
-            GSTEX_STAT(4, __popcll(__ballot(tkey >= 0)) ? 1 : 0);
+            GSTEX_STAT(4, (__popcll(__ballot(tkey >= 0)) && s_toff[j] < 0) ? 1 : 0);  // texel grads via global
             if (GSTEX_ABLATE & 2) {
 #pragma unroll
                 for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
             } else if (any) {
                 wave_reduce24(P);
             }
-            if ((lane & 7) == 0) {
-                const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
-                s_part[j][wave][base + 0] = any ? P[0] : 0.f;
-                s_part[j][wave][base + 1] = any ? P[1] : 0.f;
-                s_part[j][wave][base + 2] = any ? P[2] : 0.f;
+            if (any) {
+                live |= 1u << j;
+                if ((lane & 7) == 0) {
+                    const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
+                    s_part[j][wave][base + 0] = P[0];
+                    s_part[j][wave][base + 1] = P[1];
+                    s_part[j][wave][base + 2] = P[2];
+                }
             }
             if (__any(tkey >= 0)) {
                 float tg[4 * CM];
@@ -744,16 +771,22 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 }
             }
         }
+        if (lane == 0) s_live[wave] = live;
         __syncthreads();
-        // combine the 4 waves in a fixed order and store the (tile, splat) partial
+        // combine the 4 waves in a fixed order (a wave that skipped the splat adds +0) and store the
+        // (tile, splat) partial
         {
             const int j = tid >> 2, c0 = (tid & 3) * 6;
             if (j < nb) {
+                const bool l0 = (s_live[0] >> j) & 1, l1 = (s_live[1] >> j) & 1;
+                const bool l2 = (s_live[2] >> j) & 1, l3 = (s_live[3] >> j) & 1;
                 float* dst = partials + (size_t)s_slot[j] * kNP + c0;
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
                     const int c = c0 + i;
-                    dst[i] = ((s_part[j][0][c] + s_part[j][1][c]) + s_part[j][2][c]) + s_part[j][3][c];
+                    const float p0 = l0 ? s_part[j][0][c] : 0.f, p1 = l1 ? s_part[j][1][c] : 0.f;
+                    const float p2 = l2 ? s_part[j][2][c] : 0.f, p3 = l3 ? s_part[j][3][c] : 0.f;
+                    dst[i] = ((p0 + p1) + p2) + p3;
                 }
             }
         }
