@@ -283,9 +283,20 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
         }
         __syncthreads();
         const int nb = min(kFwdBatch, rng.y - b0);
-        for (int j = 0; j < nb; ++j) {
+        // the batch splats whose contribution box meets this wave's 16x4 block, tested all at once
+        const int lane = tid & 63;
+        unsigned long long todo[kFwdBatch / 64];
+#pragma unroll
+        for (int hb = 0; hb < kFwdBatch / 64; ++hb) {
+            const int jj = hb * 64 + lane;
+            todo[hb] = __ballot(jj < nb && wave_overlaps<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1));
+        }
+        for (int hb = 0; hb < kFwdBatch / 64 && !done; ++hb) {
+          unsigned long long m = todo[hb];
+          while (m) {
             if (done) break;
-            if (!wave_overlaps<kFwdBatch>(s_rec, j, wx0, wx1, wy0, wy1)) continue;
+            const int j = hb * 64 + __builtin_ctzll(m);
+            m &= m - 1;
             const Rec r = read_rec<kFwdBatch>(s_rec, j);
             Hit h;
             if (!eval_hit(r, px, py, aa, h)) continue;
@@ -299,15 +310,14 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
                 const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
-                const size_t o00 = (size_t)(r.off + b.i0 * r.w + b.j0) * Cn;
-                const size_t o01 = (size_t)(r.off + b.i0 * r.w + b.j1) * Cn;
-                const size_t o10 = (size_t)(r.off + b.i1 * r.w + b.j0) * Cn;
-                const size_t o11 = (size_t)(r.off + b.i1 * r.w + b.j1) * Cn;
+                const float* tblk = texture + (size_t)r.off * Cn;  // wave-uniform block base
+                const int o00 = (b.i0 * r.w + b.j0) * Cn, o01 = (b.i0 * r.w + b.j1) * Cn;
+                const int o10 = (b.i1 * r.w + b.j0) * Cn, o11 = (b.i1 * r.w + b.j1) * Cn;
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < Cn) {
-                        float val = bilerp_mix(texture[o00 + c], texture[o01 + c], texture[o10 + c],
-                                               texture[o11 + c], b.ax, b.ay);
+                        float val = bilerp_mix(tblk[o00 + c], tblk[o01 + c], tblk[o10 + c], tblk[o11 + c], b.ax,
+                                               b.ay);
                         tex[c] = tex[c] + val * w;
                     }
                 }
@@ -328,6 +338,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             }
             T = test_T;
             last = b0 - rng.x + j;
+          }
         }
     }
     if (!inside) return;
