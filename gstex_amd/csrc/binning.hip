@@ -131,6 +131,51 @@ __global__ __launch_bounds__(256) void count_kernel(int n, const float* __restri
         for (int tx = r.x0; tx < r.x1; ++tx) rank[e++] = atomicAdd(&tile_count[ty * tiles_x + tx], 1);
 }
 
+// 1'. the same count + rank with the tile histogram privatised in LDS: each workgroup ranks its
+// 1024 splats' pairs with LDS atomics, then reserves one global range per touched tile (one global
+// atomic per (workgroup, tile) instead of one per pair: the image centre's tiles receive ~2000 pairs
+// each, which serialised on their counters).  Ranks are scattered positions inside a tile's bucket
+// only; the per-tile sort by (depth, id) makes the final order independent of them.
+constexpr int kCountSplatsPerThread = 4;
+constexpr int kCountLdsTiles = 16384;  // 64 KiB histogram
+
+__global__ __launch_bounds__(256) void count_lds_kernel(int n, const float* __restrict__ centers,
+                                                        const float* __restrict__ extents,
+                                                        const int32_t* __restrict__ offsets, int tiles_x,
+                                                        int tiles_y, int block, int32_t* __restrict__ tile_count,
+                                                        int32_t* __restrict__ rank) {
+    __shared__ int s_hist[kCountLdsTiles];
+    const int n_tiles = tiles_x * tiles_y;
+    for (int t = threadIdx.x; t < n_tiles; t += 256) s_hist[t] = 0;
+    __syncthreads();
+    const int g0 = blockIdx.x * (256 * kCountSplatsPerThread) + threadIdx.x;
+    Rect rr[kCountSplatsPerThread];
+#pragma unroll
+    for (int k = 0; k < kCountSplatsPerThread; ++k) {
+        const int g = g0 + k * 256;
+        rr[k] = Rect{0, 0, 0, 0};
+        if (g < n)
+            rr[k] = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
+                              tiles_y, block);
+        int e = g < n ? offsets[g] : 0;
+        for (int ty = rr[k].y0; ty < rr[k].y1; ++ty)
+            for (int tx = rr[k].x0; tx < rr[k].x1; ++tx) rank[e++] = atomicAdd(&s_hist[ty * tiles_x + tx], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n_tiles; t += 256) {
+        const int c = s_hist[t];
+        if (c > 0) s_hist[t] = atomicAdd(&tile_count[t], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kCountSplatsPerThread; ++k) {
+        const int g = g0 + k * 256;
+        int e = g < n ? offsets[g] : 0;
+        for (int ty = rr[k].y0; ty < rr[k].y1; ++ty)
+            for (int tx = rr[k].x0; tx < rr[k].x1; ++tx) rank[e++] += s_hist[ty * tiles_x + tx];
+    }
+}
+
 // 3. place keys
 __global__ __launch_bounds__(256) void place_kernel(int n, const float* __restrict__ centers,
                                                     const float* __restrict__ extents,
@@ -377,8 +422,12 @@ extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, 
     BinWorkspace ws;
     bin_layout(n_tiles, n_isect, (char*)workspace, &ws);
     (void)hipMemsetAsync(ws.tile_count, 0, (size_t)(n_tiles + 1) * sizeof(int32_t), st);
-    count_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, offsets, tiles_x, tiles_y, block,
-                                                  ws.tile_count, ws.rank);
+    if (n_tiles <= kCountLdsTiles)
+        count_lds_kernel<<<div_up(n, 256 * kCountSplatsPerThread), 256, 0, st>>>(
+            n, centers, extents, offsets, tiles_x, tiles_y, block, ws.tile_count, ws.rank);
+    else
+        count_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, offsets, tiles_x, tiles_y, block,
+                                                      ws.tile_count, ws.rank);
     int rc = run_scan(n_tiles, ws.tile_count, ws.tile_start, ws.scan_ws, st);
     if (rc) return rc;
     place_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, depths, offsets, tiles_x, tiles_y, block,

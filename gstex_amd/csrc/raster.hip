@@ -372,21 +372,17 @@ __device__ __forceinline__ float dpp_f(float v) {
 
 __device__ __forceinline__ void wave_reduce24(float (&v)[kNP]) {
     const int lane = threadIdx.x & 63;
-    {
-        const bool hi = lane & 32;
+    // permlane32_swap(a, b) leaves a = [a_lo, b_lo], b = [a_hi, b_hi]: a + b holds a's half-sum in
+    // lanes 0-31 and b's in lanes 32-63 (likewise per row pair for permlane16_swap)
 #pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 12]), false, false);
-            v[i] = hi ? v[i + 12] + __uint_as_float(r[0]) : v[i] + __uint_as_float(r[1]);
-        }
+    for (int i = 0; i < 12; ++i) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 12]), false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
-    {
-        const bool hi = lane & 16;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 6]), false, false);
-            v[i] = hi ? v[i + 6] + __uint_as_float(r[0]) : v[i] + __uint_as_float(r[1]);
-        }
+    for (int i = 0; i < 6; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 6]), false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
     {
         const bool hi = lane & 8;

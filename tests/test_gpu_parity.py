@@ -106,6 +106,13 @@ def test_binning_bit_exact():
     assert (tr[:, 1] - tr[:, 0]).max() > 0
 
 
+def test_binning_many_tiles_global_count_path():
+    # > 16384 tiles: the LDS-privatised tile histogram does not fit, counting falls back to global atomics
+    case = make_case(n=1500, n_texels=0, H=2080, W=2080, seed=8)
+    tr = _bins_equal(case)
+    assert tr.shape[0] > 16384 and (tr[:, 1] - tr[:, 0]).max() > 0
+
+
 def test_binning_large_bucket_merge_path():
     # many splats piled on few tiles -> buckets > 4096 keys exercise the merge-path sort
     case = make_case(n=20000, n_texels=0, H=32, W=32, seed=6, cube=0.3)
