@@ -118,7 +118,10 @@ def main():
     setup_s = time.perf_counter() - t_scene
 
     def step():
-        trainer.zero_grad()
+        if sync is not None:
+            sync.zero()  # one fill of the flat gradient buffer the .grad views live in
+        else:
+            trainer.zero_grad()
         trainer.forward_backward(view, gt)
         if sync is not None:
             sync.all_reduce()

@@ -9,7 +9,8 @@ Reproduces the parts of the reference's GStexModel that sit either side of the h
   * texture = SH2RGB(texture_dc)     gstex.py:1093-1094,1119
   * texture_gaussians                gstex.py:1133-1162
   * background composite             gstex.py:1204-1205
-  * loss 0.8 L1 + 0.2 (1 - SSIM)     gstex.py:1301-1322 (pytorch_msssim SSIM semantics)
+  * loss 0.8 L1 + 0.2 (1 - SSIM)     gstex.py:1301-1322 (pytorch_msssim SSIM semantics; fused HIP
+                                     kernels in gstex_amd.loss, eager torch path kept for reference)
   * per-group Adam, eps 1e-15        gstex_configs.py:207-244, engine/optimizers.py:158-171
                                      (one fused HIP launch, gstex_amd.optim.FusedAdam)
 The rechart every 100 steps (gstex.py:890-914) is provided by `recharge()`.
@@ -23,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
+from .loss import gaussian_window, photometric_loss
 from .optim import FusedAdam
 from .charts import SH2RGB, build_charts, get_uv_mapping, texture_dims_to_query
 from .scene import Scene, View
@@ -41,9 +43,7 @@ DEFAULT_SETTINGS = (1 << 9) | (1 << 10)
 
 
 def _gauss_window(size=11, sigma=1.5, device=None):
-    coords = torch.arange(size, dtype=torch.float32, device=device) - size // 2
-    g = torch.exp(-(coords**2) / (2 * sigma**2))
-    return g / g.sum()
+    return gaussian_window(size, sigma).to(device)  # the same fp32 weights the fused kernels use
 
 
 _BANDS: dict = {}
@@ -100,7 +100,8 @@ class GStexTrainer:
     """Holds the GStex parameters on one device and runs forward/backward/Adam steps."""
 
     def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
-                 pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True):
+                 pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
+                 fused_loss: bool = True):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -121,6 +122,7 @@ class GStexTrainer:
         self.background = torch.tensor(background, dtype=torch.float32, device=d)
         self.step = 0
         self.fused_adam = fused_adam
+        self.fused_loss = fused_loss
         self._build_optimizer()
 
     # ------------------------------------------------------------------ parameters
@@ -146,7 +148,7 @@ class GStexTrainer:
             self.optimizer = torch.optim.Adam(groups, eps=1e-15, foreach=True)
 
     # ------------------------------------------------------------------ forward
-    def render(self, view: View, sh_degree_now: int | None = None):
+    def render(self, view: View, sh_degree_now: int | None = None, composite: bool = True):
         """get_outputs (gstex.py:992-1236), training branch."""
         means = self.means
         quats = self.quats / self.quats.norm(dim=-1, keepdim=True)
@@ -172,8 +174,11 @@ class GStexTrainer:
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
             ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background))
-        rgb = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :], 0.0, 1.0)
-        return dict(rgb=rgb, depth=depth, reg=reg, alpha=alpha, normal=normal)
+        out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
+        if composite:
+            out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
+                                     0.0, 1.0)
+        return out
 
     def loss(self, rgb: torch.Tensor, gt: torch.Tensor, ssim_lambda: float = 0.2) -> torch.Tensor:
         l1 = torch.abs(gt - rgb).mean()
@@ -181,17 +186,24 @@ class GStexTrainer:
         return (1 - ssim_lambda) * l1 + ssim_lambda * sim
 
     def forward_backward(self, view: View, gt: torch.Tensor) -> StepOutput:
-        out = self.render(view)
-        loss = self.loss(out["rgb"], gt)
+        out = self.render(view, composite=not self.fused_loss)
+        if self.fused_loss:  # composite + clamp + L1/SSIM in one HIP launch pair (gstex_amd.loss)
+            loss, rgb = photometric_loss(out["img"], out["tex"], out["alpha"], self.background, gt.contiguous())
+        else:
+            rgb = out["rgb"]
+            loss = self.loss(rgb, gt)
         loss.backward()
-        return StepOutput(loss.detach(), out["rgb"].detach())
+        return StepOutput(loss.detach(), rgb.detach())
 
     def optimizer_step(self):
         self.optimizer.step()
         self.step += 1
 
-    def zero_grad(self):
-        self.optimizer.zero_grad(set_to_none=False)
+    def zero_grad(self, set_to_none: bool = True):
+        """Optimizers.zero_grad_all (engine/optimizers.py): torch's default set_to_none=True, so backward
+        writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
+        when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead)."""
+        self.optimizer.zero_grad(set_to_none=set_to_none)
 
     # ------------------------------------------------------------------ rechart
     @torch.no_grad()

@@ -162,6 +162,24 @@ int gstex_texture_sample_bwd(int64_t n_query, int32_t channels, const int32_t* q
                              int64_t n_texels, const float* uv, const float* v_out,
                              float* v_texture, void* stream);
 
+/* ---- photometric loss (train-step support) --------------------------------- */
+/* rgb = clamp(img + tex[..., 0:3] + (1 - alpha) * background, 0, 1)      (gstex.py:1204-1205)
+ * loss = (1 - ssim_lambda) * mean|gt - rgb| + ssim_lambda * (1 - SSIM(gt, rgb))  (gstex.py:1301-1322)
+ * SSIM as pytorch_msssim: separable 11-tap window (window[11], host fp32), valid filtering,
+ * C1 = 0.01^2, C2 = 0.03^2, mean over the (H-10) x (W-10) x 3 map.  Images are [H][W][k] row-major
+ * device fp32; tex has C >= 3 channels (only 0..2 enter the loss).  loss_out (device float[3]) =
+ * {loss, L1, SSIM}; rgb_out may be NULL.  The forward leaves in the workspace what the backward reads:
+ * pass the same workspace to gstex_loss_bwd.  grad_loss is a device scalar (the loss's upstream
+ * gradient); d_img, d_tex (channels >= 3 zero) and d_alpha are overwritten. */
+size_t gstex_loss_workspace_size(int32_t H, int32_t W);
+int gstex_loss_fwd(int32_t H, int32_t W, int32_t C, const float* img, const float* tex, const float* alpha,
+                   const float* background, const float* gt, const float* window, float ssim_lambda,
+                   float* rgb_out, float* loss_out, void* workspace, size_t workspace_bytes, void* stream);
+int gstex_loss_bwd(int32_t H, int32_t W, int32_t C, const float* img, const float* tex, const float* alpha,
+                   const float* background, const float* gt, const float* window, float ssim_lambda,
+                   const float* grad_loss, float* d_img, float* d_tex, float* d_alpha, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
 /* ---- optimizer (train-step support) ----------------------------------- */
 /* One launch of torch.optim.Adam (no weight decay, no amsgrad) over up to GSTEX_ADAM_MAX_TENSORS
  * fp32 tensors.  Per tensor the host supplies step_size = lr / (1 - beta1^t) and

@@ -29,7 +29,7 @@ def lib():
 
 def test_every_header_symbol_is_exported_and_bound(lib):
     syms = declared_symbols()
-    assert len(syms) >= 21
+    assert len(syms) >= 24
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in gstex_hip.h but not exported"
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature in gstex_amd/_lib.py"
@@ -120,3 +120,15 @@ def test_adam_rejects_bad_tables(lib):
     assert rc == 1 and "null pointer" in msg
     t = (_lib.GstexAdamTensor * 1)(_lib.GstexAdamTensor(None, None, None, None, 0, 1e-3, 1.0))
     assert _status(lib, "gstex_adam_step", 1, t, 0.9, 0.999, 1e-15, None)[0] == 0  # empty: no launch
+
+
+def test_loss_rejects_small_images_and_channels(lib):
+    assert lib.gstex_loss_workspace_size(10, 64) == 0
+    assert lib.gstex_loss_workspace_size(64, 64) > 9 * 54 * 54 * 4
+    win = (ctypes.c_float * 11)()
+    rc, msg = _status(lib, "gstex_loss_fwd", 8, 64, 3, None, None, None, None, None, win, 0.2, None, None, None, 0,
+                      None)
+    assert rc == 1 and "window" in msg
+    rc, msg = _status(lib, "gstex_loss_bwd", 64, 64, 2, None, None, None, None, None, win, 0.2, None, None, None,
+                      None, None, 0, None)
+    assert rc == 1 and "channels" in msg

@@ -296,3 +296,37 @@ def test_fused_adam_matches_torch_adam():
             torch.testing.assert_close(pa.detach(), pb.detach(), rtol=2e-6, atol=1e-7)
     for pa, pb in zip(a, b):
         torch.testing.assert_close(opt_a.state[pa]["exp_avg_sq"], opt_b.state[pb]["exp_avg_sq"], rtol=1e-5, atol=0)
+
+
+# ---------------------------------------------------------------- fused photometric loss (train-step support)
+@pytest.mark.parametrize("C", [3, 4])
+def test_fused_loss_matches_eager_torch(C):
+    from gstex_amd.loss import photometric_loss
+    from gstex_amd.model import ssim
+
+    g = torch.Generator().manual_seed(40 + C)
+    H, W = 70, 93
+    img = (torch.rand(H, W, 3, generator=g) * 1.4 - 0.2)
+    tex = torch.rand(H, W, C, generator=g) * 0.3
+    alpha = torch.rand(H, W, generator=g)
+    bg = torch.rand(3, generator=g)
+    gt = torch.rand(H, W, 3, generator=g)
+    gt[:5, :5] = 1.0  # with img saturated there too: |gt - rgb| = 0 ties (sign 0)
+    img[:5, :5] = 2.0
+    leaves = [t.to(DEV).requires_grad_(True) for t in (img, tex, alpha)]
+    loss, rgb = photometric_loss(leaves[0], leaves[1], leaves[2], bg.to(DEV), gt.to(DEV))
+    loss.backward(torch.tensor(1.7, device=DEV))
+    ref_leaves = [t.to(DEV).requires_grad_(True) for t in (img, tex, alpha)]
+    r_img, r_tex, r_alpha = ref_leaves
+    ref_rgb = torch.clamp(r_img + r_tex[:, :, 0:3] + (1 - r_alpha[:, :, None]) * bg.to(DEV)[None, None, :], 0.0, 1.0)
+    gtd = gt.to(DEV)
+    ref = 0.8 * torch.abs(gtd - ref_rgb).mean() + 0.2 * (1 - ssim(gtd.permute(2, 0, 1)[None],
+                                                               ref_rgb.permute(2, 0, 1)[None]))
+    ref.backward(torch.tensor(1.7, device=DEV))
+    assert torch.equal(rgb, ref_rgb.detach()), "composite must match the eager expression bit for bit"
+    assert abs(float(loss.detach()) - float(ref.detach())) <= 2e-6 * abs(float(ref.detach()))
+    for a, b, name in zip(leaves, ref_leaves, ("img", "tex", "alpha")):
+        err = float((a.grad - b.grad).abs().max())
+        scale = float(b.grad.abs().max())
+        assert err <= 1e-5 * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+    assert float(leaves[1].grad[:, :, 3:].abs().sum()) == 0.0
