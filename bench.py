@@ -30,6 +30,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PROFILE_TAG = "r01"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+
+
+def pmc_row(kernel):
+    """`kernel`'s row of the committed rocprofv3 PMC summary: HBM bytes per launch (2 x FETCH_SIZE +
+    WRITE_SIZE, separate passes, gfx950 FETCH_SIZE halving corrected) and VALU instructions per launch;
+    None if not profiled."""
+    path = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_traffic.json")
+    try:
+        rows = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for r in rows:
+        if r["kernel"].startswith(kernel + "_kernel") and r.get("hbm_bytes_per_launch"):
+            return r
+    return None
 
 
 def parse():
@@ -167,8 +183,17 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                    traffic_source=f"profiles/{PROFILE_TAG}_traffic.json",
                     bytes_per_launch=dom_bytes, launch_ms=round(dom_ms, 4),
                     fwd_bwd_frac=round((ab["fwd"] + ab["bwd"]) / ((f_ms + b_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+
+    prow = pmc_row(dom)
+    if prow is not None:
+        roofline["traffic"] = int(prow["hbm_bytes_per_launch"])
+        if prow.get("valu_insts"):
+            # the kernel is VALU-issue/latency bound, not HBM bound: its issue roofline, live time
+            roofline["valu_insts_per_launch"] = int(prow["valu_insts"])
+            roofline["valu_issue_frac"] = round(prow["valu_insts"] / (dom_ms * 1e-3 * 1024 * 2.4e9 / 2), 4)
 
     if rank != 0:
         if world > 1:

@@ -45,6 +45,8 @@ def main(tag):
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = pmc(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    vpath = os.path.join(src, "valu", "run_counter_collection.csv")
+    valu = pmc(vpath, "SQ_INSTS_VALU") if os.path.exists(vpath) else {}
     rows = []
     total = sum(float(r["TotalDurationNs"]) for r in stats)
     for r in sorted(stats, key=lambda r: -float(r["TotalDurationNs"])):
@@ -52,19 +54,27 @@ def main(tag):
         f = fetch.get(k)
         w = write.get(k)
         traffic = (2 * f + w) * 1024 if f is not None and w is not None else None
+        v = valu.get(k)
+        # VALU issue roofline: a wave64 VALU op occupies its SIMD 2 cycles (32 lanes/cycle); 1024 SIMDs at
+        # 2.4 GHz issue at most 1.2288e12 wave-instructions/s chip-wide
+        vfrac = v / (float(r["AverageNs"]) * 1e-9 * 1024 * 2.4e9 / 2) if v else None
         rows.append(dict(kernel=k, calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
                          pct=100 * float(r["TotalDurationNs"]) / total, fetch_kib=f, write_kib=w,
-                         hbm_bytes_per_launch=traffic))
+                         hbm_bytes_per_launch=traffic, valu_insts=v, valu_issue_frac=vfrac))
     json.dump({"tag": tag, "kernels": rows}, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary `{tag}`\n\nCommand: `tools/profile_bench.sh {tag}` = rocprofv3 over "
                  "`python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline` (cfg3: 200k splats, 1e7 texels, "
                  "800x800, full train step).\nTraffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch "
-                 "(separate --pmc passes; gfx950 FETCH_SIZE halving corrected).\n\n")
-        fh.write("| kernel | calls | avg us | % time | HBM MB/launch |\n|---|---|---|---|---|\n")
+                 "(separate --pmc passes; gfx950 FETCH_SIZE halving corrected).\nVALU issue = SQ_INSTS_VALU "
+                 "per launch / (avg duration x 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction).\n\n")
+        fh.write("| kernel | calls | avg us | % time | HBM MB/launch | VALU instr/launch | VALU issue |\n"
+                 "|---|---|---|---|---|---|---|\n")
         for r in rows[:25]:
             t = "" if r["hbm_bytes_per_launch"] is None else f"{r['hbm_bytes_per_launch'] / 1e6:.1f}"
-            fh.write(f"| {r['kernel'][:60]} | {r['calls']} | {r['avg_us']:.1f} | {r['pct']:.1f} | {t} |\n")
+            v = "" if not r.get("valu_insts") else f"{r['valu_insts']:.3g}"
+            vf = "" if not r.get("valu_issue_frac") else f"{100 * r['valu_issue_frac']:.0f}%"
+            fh.write(f"| {r['kernel'][:60]} | {r['calls']} | {r['avg_us']:.1f} | {r['pct']:.1f} | {t} | {v} | {vf} |\n")
     print(open(os.path.join(dst, f"{tag}_summary.md")).read())
 
 
