@@ -26,8 +26,11 @@ constexpr int kThreads = kTilePixels;  // 256
 #ifndef GSTEX_FWD_BATCH
 #define GSTEX_FWD_BATCH 128
 #endif
+#ifndef GSTEX_WAVE_8X8
+#define GSTEX_WAVE_8X8 1  // each wave covers an 8x8 quadrant of the tile (0: 16x4 rows)
+#endif
 #ifndef GSTEX_SEG_W
-#define GSTEX_SEG_W 16  // texel-gradient segment width in lanes (4, 8 or 16)
+#define GSTEX_SEG_W (GSTEX_WAVE_8X8 ? 8 : 16)  // texel-gradient segment width in lanes = one pixel row
 #endif
 #ifndef GSTEX_FAST_RCP
 #define GSTEX_FAST_RCP 1  // v_rcp_f32 for backward divisions that feed no threshold decision
@@ -62,6 +65,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #define GSTEX_FWD_ATTR __attribute__((amdgpu_num_vgpr((512 / GSTEX_FWD_WAVES) / 8 * 8 / 2)))
 #else
 #define GSTEX_FWD_ATTR
+#endif
+#ifndef GSTEX_CONIC_CULL
+#define GSTEX_CONIC_CULL 1  // per-wave ellipse-vs-rectangle cull on top of the contribution box
 #endif
 #ifndef GSTEX_REC_SGPR
 #define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
@@ -167,6 +173,23 @@ __device__ __forceinline__ float4 uni4(float4 v) {  // wave-uniform value -> SGP
                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w))));
 }
 
+// Pixel of thread tid inside a 16x16 tile and the wave's block of pixel centres.
+struct WaveBlock { int px, py; float wx0, wx1, wy0, wy1; };
+__device__ __forceinline__ WaveBlock wave_block(int tx, int ty, int tid) {
+    WaveBlock b;
+    const int w = tid >> 6, l = tid & 63;
+    int ox, oy, bw, bh;
+    if (GSTEX_WAVE_8X8) { ox = (w & 1) * 8 + (l & 7); oy = (w >> 1) * 8 + (l >> 3); bw = 8; bh = 8; }
+    else { ox = l & 15; oy = 4 * w + (l >> 4); bw = 16; bh = 4; }
+    b.px = tx * kTile + ox;
+    b.py = ty * kTile + oy;
+    b.wx0 = (float)(tx * kTile + (GSTEX_WAVE_8X8 ? (w & 1) * 8 : 0)) + 0.5f;
+    b.wy0 = (float)(ty * kTile + (GSTEX_WAVE_8X8 ? (w >> 1) * 8 : 4 * w)) + 0.5f;
+    b.wx1 = b.wx0 + (float)(bw - 1);
+    b.wy1 = b.wy0 + (float)(bh - 1);
+    return b;
+}
+
 // SGPR: move the (wave-uniform) record into scalar registers; frees ~30 VGPRs where the register
 // file, not issue, limits occupancy (backward), at the cost of one v_readfirstlane per value
 template <int NB, bool SGPR = false>
@@ -194,6 +217,56 @@ __device__ __forceinline__ bool wave_overlaps(const float4* s, int j, float wx0,
     const float bx0 = s[0 * NB + j].z, bx1 = s[1 * NB + j].y;
     const float4 q = s[7 * NB + j];
     return bx0 <= wx1 && bx1 >= wx0 && q.z <= wy1 && q.w >= wy0;
+}
+
+// min over t in [lo, hi] of f(t) = |Q.xy + t A.xy|^2 - rm (Q.z + t A.z)^2 is <= 0?  (true when the slice
+// is not convex in t: the conic is then not an ellipse there and nothing is culled)
+__device__ __forceinline__ bool conic_edge(float ax, float ay, float az, float qx, float qy, float qz, float rm,
+                                           float lo, float hi) {
+    const float a = (ax * ax + ay * ay) - rm * (az * az);
+    if (!(a > 0.0f)) return true;
+    const float b = (qx * ax + qy * ay) - rm * (qz * az);
+    const float t = fminf(fmaxf(-b / a, lo), hi);
+    const float px = qx + t * ax, py = qy + t * ay, pz = qz + t * az;
+    return (px * px + py * py) - rm * (pz * pz) <= 0.0f;
+}
+
+// Can splat j reach alpha >= 1/255 anywhere in the wave's block of pixel centres [wx0, wx1] x [wy0, wy1]?
+// With the anchored record (Tu.z = Tv.z = 0) the homogeneous point p = k x l is affine in the pixel offset
+// d = pixel - anchor: p = (d.x A + d.y B) + (0, 0, Pz).  The pair passes iff rho3 = |p.xy|^2 / p.z^2 <= rm
+// = 2 ln(255 o) (or, with the AA filter, the disc 2 |pixel - centre|^2 <= rm): an ellipse (splats whose
+// disc crosses the camera plane were culled upstream), tested exactly against the rectangle -- anchor
+// inside, or an edge meeting it -- with a 1 % threshold margin and a 0.05 px larger rectangle, so the fp32
+// evaluation can never accept a pair the test rejected.
+template <int NB>
+__device__ __forceinline__ bool conic_overlaps(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
+                                               bool aa) {
+    const float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], q = s[7 * NB + j];
+    const float opac = c.w;
+    if (!(opac * 255.0f > 1.0f)) return false;
+    const float rm = 2.0f * logf(255.0f * opac) * 1.01f + 1e-2f;
+    const float x0 = wx0 - 0.05f, x1 = wx1 + 0.05f, y0 = wy0 - 0.05f, y1 = wy1 + 0.05f;
+    if (aa) {
+        const float ex = c.y - fminf(fmaxf(c.y, x0), x1), ey = c.z - fminf(fmaxf(c.z, y0), y1);
+        if (2.0f * (ex * ex + ey * ey) <= rm) return true;
+    }
+    const float xa = q.x, ya = q.y;
+    if (xa >= x0 && xa <= x1 && ya >= y0 && ya <= y1) return true;
+    const float tux = a.x, tuy = a.y, tvx = a.w, tvy = b.x, twx = b.z, twy = b.w, twz = c.x;
+    const float Ax = twz * tvy, Ay = -(twz * tvx), Az = twy * tvx - twx * tvy;  // -(Tw x Tv)
+    const float Bx = -(tuy * twz), By = tux * twz, Bz = tuy * twx - tux * twy;  // -(Tu x Tw)
+    const float Pz = tux * tvy - tuy * tvx;                                     // (Tu x Tv).z
+    const float dx0 = x0 - xa, dx1 = x1 - xa, dy0 = y0 - ya, dy1 = y1 - ya;
+    return conic_edge(Ax, Ay, Az, dy0 * Bx, dy0 * By, Pz + dy0 * Bz, rm, dx0, dx1) ||
+           conic_edge(Ax, Ay, Az, dy1 * Bx, dy1 * By, Pz + dy1 * Bz, rm, dx0, dx1) ||
+           conic_edge(Bx, By, Bz, dx0 * Ax, dx0 * Ay, Pz + dx0 * Az, rm, dy0, dy1) ||
+           conic_edge(Bx, By, Bz, dx1 * Ax, dx1 * Ay, Pz + dx1 * Az, rm, dy0, dy1);
+}
+
+template <int NB>
+__device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
+                                             bool aa) {
+    return wave_overlaps<NB>(s, j, wx0, wx1, wy0, wy1) && (!GSTEX_CONIC_CULL || conic_overlaps<NB>(s, j, wx0, wx1, wy0, wy1, aa));
 }
 
 struct Hit {
@@ -256,15 +329,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x;
-    const int pxi = tx * kTile + (tid & 15), pyi = ty * kTile + (tid >> 4);
+    const WaveBlock wb = wave_block(tx, ty, tid);
+    const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
     const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
     const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
     const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
-    const float wx0 = (float)(tx * kTile) + 0.5f, wx1 = wx0 + (float)(kTile - 1);
-    const float wy0 = (float)(ty * kTile + 4 * (tid >> 6)) + 0.5f, wy1 = wy0 + 3.0f;
+    const float wx0 = wb.wx0, wx1 = wb.wx1, wy0 = wb.wy0, wy1 = wb.wy1;
 
     float T = 1.0f;
     float img[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 0.f};
@@ -289,7 +362,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
 #pragma unroll
         for (int hb = 0; hb < kFwdBatch / 64; ++hb) {
             const int jj = hb * 64 + lane;
-            todo[hb] = __ballot(jj < nb && wave_overlaps<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1));
+            todo[hb] = __ballot(jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa));
         }
         for (int hb = 0; hb < kFwdBatch / 64 && !done; ++hb) {
           unsigned long long m = todo[hb];
@@ -436,10 +509,12 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     const int pos = threadIdx.x & (SW - 1);
     const int left = dpp_shr_i<1>(-7, key);
     int seg = (pos == 0 || left != key) ? 1 : 0;  // head flag: group start or key change
+    // segment id = inclusive prefix count of heads over the whole 16-lane DPP row (a shorter window would
+    // give two lanes of one segment different counts); the forced head at pos 0 separates groups
     seg += dpp_shr_i<1>(0, seg);
     seg += dpp_shr_i<2>(0, seg);
-    if (SW > 4) seg += dpp_shr_i<4>(0, seg);
-    if (SW > 8) seg += dpp_shr_i<8>(0, seg);
+    seg += dpp_shr_i<4>(0, seg);
+    seg += dpp_shr_i<8>(0, seg);
     seg_step<NV, 1>(seg, v);
     seg_step<NV, 2>(seg, v);
     if (SW > 4) seg_step<NV, 4>(seg, v);
@@ -484,15 +559,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int pxi = tx * kTile + (tid & 15), pyi = ty * kTile + (tid >> 4);
+    const WaveBlock wb = wave_block(tx, ty, tid);
+    const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
     const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
     const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
     const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
-    const float wx0 = (float)(tx * kTile) + 0.5f, wx1 = wx0 + (float)(kTile - 1);
-    const float wy0 = (float)(ty * kTile + 4 * wave) + 0.5f, wy1 = wy0 + 3.0f;
+    const float wx0 = wb.wx0, wx1 = wb.wx1, wy0 = wb.wy0, wy1 = wb.wy1;
 
     float T = 1.0f, M1f = 0.f, M2f = 0.f;
     int last = -1;
@@ -575,7 +650,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         unsigned todo;
         {
             const bool need = lane < nb && bb * kBwdBatch + lane <= wave_last &&
-                              wave_overlaps<kBwdBatch>(s_rec, lane < nb ? lane : 0, wx0, wx1, wy0, wy1);
+                              wave_may_hit<kBwdBatch>(s_rec, lane < nb ? lane : 0, wx0, wx1, wy0, wy1, aa);
             todo = (unsigned)__ballot(need);
         }
         unsigned live = 0u;
