@@ -972,6 +972,84 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     v_quats[4 * g + 3] = dq[3];
 }
 
+// ------------------------------------------------------------------------------------------
+// texture_edit (gstex.py:579-606, viewer paint tool): splat a screen-space RGBA stroke into the
+// texel store.  Same front-to-back traversal as the forward (same cull, termination and weights
+// w = alpha * T); a pair whose hit depth lies inside the pixel's [depth_lo, depth_hi] window (the
+// caller passes the rendered depth +- 1e-2) adds, for each of its 4 bilinear texels with weight b,
+//   out[texel] += b * w * (a * r, a * g, a * b, a, 1)
+// so out[:, :3] / out[:, 3] is the stroke colour and out[:, 3] / out[:, 4] the blend weight the caller
+// forms (gstex.py:602-605).  Viewer path: global float atomics, no LDS staging.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void texture_edit_kernel(
+    CamArgs cam_args, int tiles_x, int settings, const float4* __restrict__ records,
+    const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order, const int32_t* __restrict__ sorted_ids,
+    const float* __restrict__ edit_rgb, const float* __restrict__ edit_a, const float* __restrict__ depth_lo,
+    const float* __restrict__ depth_hi, float* __restrict__ out) {
+    const Camera cam = load_camera(cam_args);
+    __shared__ float4 s_rec[kRecF4 * kFwdBatch];
+    const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int tid = threadIdx.x;
+    const WaveBlock wb = wave_block(tx, ty, tid);
+    const int pxi = wb.px, pyi = wb.py;
+    const bool inside = pxi < cam.W && pyi < cam.H;
+    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
+    const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
+    const int2 rng = tile_ranges[tile];
+    float er = 0.f, eg = 0.f, eb = 0.f, ea = 0.f, dlo = 1.0f, dhi = 0.0f;
+    if (inside) {
+        const size_t pix = (size_t)pyi * cam.W + pxi;
+        er = edit_rgb[3 * pix]; eg = edit_rgb[3 * pix + 1]; eb = edit_rgb[3 * pix + 2];
+        ea = edit_a[pix];
+        dlo = depth_lo[pix];
+        dhi = depth_hi[pix];
+    }
+    float T = 1.0f;
+    bool done = !inside;
+    for (int b0 = rng.x; b0 < rng.y; b0 += kFwdBatch) {
+        if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
+        for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
+            const int j = q / kRecF4, k = q % kRecF4;
+            if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+        }
+        __syncthreads();
+        const int nb = min(kFwdBatch, rng.y - b0);
+        for (int j = 0; j < nb && !done; ++j) {
+            if (!wave_may_hit<kFwdBatch>(s_rec, j, wb.wx0, wb.wx1, wb.wy0, wb.wy1, aa)) continue;
+            const Rec r = read_rec<kFwdBatch>(s_rec, j);
+            Hit h;
+            if (!eval_hit(r, px, py, aa, h)) continue;
+            const float test_T = T * (1.0f - h.alpha);
+            if (test_T < kTMin) {
+                done = true;
+                break;
+            }
+            const float w = h.alpha * T;
+            if (r.h * r.w > 0 && h.z >= dlo && h.z <= dhi) {
+                float tu, tv;
+                tex_coords(r, h.u, h.v, tu, tv);
+                const Bilerp bl = bilerp_coords(tu, tv, r.h, r.w);
+                const float wc[4] = {(1.0f - bl.ax) * (1.0f - bl.ay), (1.0f - bl.ax) * bl.ay,
+                                     bl.ax * (1.0f - bl.ay), bl.ax * bl.ay};
+                const int tc[4] = {bl.i0 * r.w + bl.j0, bl.i0 * r.w + bl.j1, bl.i1 * r.w + bl.j0, bl.i1 * r.w + bl.j1};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float bw = wc[k] * w, baw = bw * ea;
+                    float* o = out + (size_t)(r.off + tc[k]) * 5;
+                    atomicAdd(o + 0, baw * er);
+                    atomicAdd(o + 1, baw * eg);
+                    atomicAdd(o + 2, baw * eb);
+                    atomicAdd(o + 3, baw);
+                    atomicAdd(o + 4, bw);
+                }
+            }
+            T = test_T;
+        }
+        __syncthreads();
+    }
+}
+
 int check_settings(int settings) {
     const int known = GSTEX_SETTING_AA_BLUR | GSTEX_SETTING_DIST_REG | GSTEX_SETTING_EVAL_NORMAL;
     if (settings & ~known) {
@@ -1076,4 +1154,26 @@ extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float
         n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
         v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     return launch_status("gstex_raster_setup_bwd");
+}
+
+extern "C" int gstex_texture_edit(const gstex_camera* cam, int32_t settings, const float* records,
+                                  const int32_t* tile_ranges, const int32_t* tile_order, const int32_t* sorted_ids,
+                                  const float* edit_rgb, const float* edit_alpha, const float* depth_lo,
+                                  const float* depth_hi, int64_t n_texels, float* out, void* stream) {
+    GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_texture_edit: invalid camera");
+    GSTEX_REQUIRE(cam->block == kTile, "gstex_texture_edit: block_width must be %d (got %d)", kTile, cam->block);
+    const int known = GSTEX_SETTING_AA_BLUR | GSTEX_SETTING_DIST_REG | GSTEX_SETTING_EDIT | GSTEX_SETTING_EVAL_NORMAL;
+    if (settings & ~known) {
+        set_error("texture_edit: unsupported settings bits 0x%x", settings & ~known);
+        return GSTEX_ERR_UNSUPPORTED;
+    }
+    GSTEX_REQUIRE(n_texels >= 0, "gstex_texture_edit: n_texels < 0");
+    GSTEX_REQUIRE(tile_ranges && edit_rgb && edit_alpha && depth_lo && depth_hi && (out || n_texels == 0),
+                  "gstex_texture_edit: null pointer");
+    const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
+    CamArgs dc = to_device_camera(*cam);
+    texture_edit_kernel<<<tiles_x * tiles_y, kThreads, 0, as_stream(stream)>>>(
+        dc, tiles_x, settings, (const float4*)records, (const int2*)tile_ranges, tile_order, sorted_ids, edit_rgb,
+        edit_alpha, depth_lo, depth_hi, out);
+    return launch_status("gstex_texture_edit");
 }

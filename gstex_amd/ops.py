@@ -429,7 +429,54 @@ def texture_sample(texture_info, query_dims, texture, uv, use_torch_impl=False):
     return _TextureSample.apply(C, query_dims, texture, uv)
 
 
-def texture_edit(*args, **kwargs):
-    """Viewer paint tool back-projection (gstex.py:556-585).  Out of the hot-path scope this round
-    (SURVEY.md §8f-4)."""
-    raise NotImplementedError("texture_edit is not implemented in gstex_amd yet (viewer-only, SURVEY §8f-4)")
+@torch.no_grad()
+def texture_edit(texture_info, texture_dims, edit_rgb, edit_alpha, depth_lower, depth_upper, centers, extents, depths,
+                 num_tiles_hit, opacities, means, scales, glob_scale, quats, uv0, umap, vmap, viewmat, c2w, fx, fy,
+                 cx, cy, H, W, block_width, settings, background=None, use_torch_impl=False):
+    """gstex_cuda.texture_edit.texture_edit (gstex.py:579-600): back-project a screen-space RGBA stroke
+    onto the texels.  Returns (T, 5) = per texel sum of  b * w * (a*rgb, a, 1)  over the pixel-splat
+    pairs whose hit depth lies in [depth_lower, depth_upper] (b: bilinear weight, w = alpha * T, a: the
+    stroke alpha); the caller forms colour = out[:, :3] / out[:, 3] and weight = out[:, 3] / out[:, 4]
+    (gstex.py:602-605).  texture_info = (N, 1, 5)."""
+    if use_torch_impl:
+        raise NotImplementedError("texture_edit(use_torch_impl=True): gstex_amd has no CPU rasterizer")
+    N, L, K = (int(v) for v in texture_info)
+    _check(L == 1 and K == 5, f"texture_info must be (N, 1, 5) for texture_edit (got {tuple(texture_info)})")
+    _check(int(block_width) == BLOCK_WIDTH, f"block_width must be {BLOCK_WIDTH} (got {block_width})")
+    means = _f32(means, "means", (None, 3))
+    n = means.shape[0]
+    _check(N == n, f"texture_info[0] ({N}) != number of splats ({n})")
+    H, W = int(H), int(W)
+    dims = _i32(texture_dims, "texture_dims", (n, 3))
+    centers_c = _f32(centers, "centers", (n, 2))
+    extents_c = _f32(extents, "extents", (n, 2))
+    depths_c = _f32(depths, "depths", (n,))
+    nth = _i32(num_tiles_hit, "num_tiles_hit", (n,))
+    opacities = _f32(opacities, "opacities", (n, 1))
+    scales = _f32(scales, "scales", (n, 3))
+    quats = _f32(quats, "quats", (n, 4))
+    uv0 = _f32(uv0, "uv0", (n, 1, 2))
+    umap = _f32(umap, "umap", (n, 1, 3))
+    vmap = _f32(vmap, "vmap", (n, 1, 3))
+    rgb = _f32(edit_rgb, "edit_rgb", (H, W, 3))
+    a = _f32(edit_alpha.reshape(H, W), "edit_alpha", (H, W))
+    dlo = _f32(depth_lower, "depth_lower", (H, W))
+    dhi = _f32(depth_upper, "depth_upper", (H, W))
+    vm = _viewmat(viewmat)
+    cw = _c2w(c2w)
+    dev = means.device
+    st = _stream(means)
+    cam = _lib.make_camera(vm, cw, fx, fy, cx, cy, H, W, BLOCK_WIDTH)
+    n_texels = int((dims[:, 0].long() * dims[:, 1].long()).sum()) if n else 0
+    if n:
+        n_texels = max(n_texels, int((dims[:, 2].long() + dims[:, 0].long() * dims[:, 1].long()).max()))
+    out = torch.zeros((n_texels, 5), device=dev, dtype=torch.float32)
+    offsets, tile_ranges, sorted_ids, _ = bin_and_sort(centers_c, extents_c, depths_c, nth, H, W, BLOCK_WIDTH)
+    order = tile_order(tile_ranges)
+    records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
+    zeros3 = torch.zeros((n, 3), device=dev, dtype=torch.float32)  # colours do not enter the edit
+    _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(zeros3),
+            ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records), st)
+    _launch("gstex_texture_edit", cam, int(settings), ptr(records), ptr(tile_ranges), ptr(order), ptr(sorted_ids),
+            ptr(rgb), ptr(a), ptr(dlo), ptr(dhi), n_texels, ptr(out), st)
+    return out

@@ -162,6 +162,16 @@ int gstex_texture_sample_bwd(int64_t n_query, int32_t channels, const int32_t* q
                              int64_t n_texels, const float* uv, const float* v_out,
                              float* v_texture, void* stream);
 
+/* texture_edit (gstex.py:579-606, viewer paint tool): traverse each pixel's splats as
+ * gstex_raster_fwd does (records from gstex_raster_setup, same tile lists/order); every counted pair
+ * whose hit depth z satisfies depth_lo <= z <= depth_hi adds, to each of its 4 bilinear texels with
+ * weight b and compositing weight w = alpha * T,  b * w * (a*r, a*g, a*b, a, 1)  to out[texel][5]
+ * (ACCUMULATES: zero out first).  edit_rgb [H][W][3], edit_alpha/depth_lo/depth_hi [H][W]. */
+int gstex_texture_edit(const gstex_camera* cam, int32_t settings, const float* records,
+                       const int32_t* tile_ranges, const int32_t* tile_order, const int32_t* sorted_ids,
+                       const float* edit_rgb, const float* edit_alpha, const float* depth_lo,
+                       const float* depth_hi, int64_t n_texels, float* out, void* stream);
+
 /* ---- photometric loss (train-step support) --------------------------------- */
 /* rgb = clamp(img + tex[..., 0:3] + (1 - alpha) * background, 0, 1)      (gstex.py:1204-1205)
  * loss = (1 - ssim_lambda) * mean|gt - rgb| + ssim_lambda * (1 - SSIM(gt, rgb))  (gstex.py:1301-1322)

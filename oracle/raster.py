@@ -328,7 +328,7 @@ def rasterize(inp: RasterInputs, grad_dtype=F64, bins=None):
     return dec["out"], hi["out"], aux
 
 
-def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions):
+def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=None):
     cam = inp.cam
     H, W = cam.H, cam.W
     C = inp.texture.shape[1]
@@ -492,6 +492,19 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions):
             reg = torch.zeros(P, dtype=dtype)
             M1 = torch.zeros(P, dtype=dtype)
             M2 = torch.zeros(P, dtype=dtype)
+        if edit is not None:  # texture_edit (raster.hip texture_edit_kernel): fp32 per-pair products, fp64 sums
+            pid = torch.from_numpy(pyi * W + pxi)
+            erg = edit["rgb"].reshape(-1, 3)[pid].to(dtype)
+            ea = edit["a"].reshape(-1)[pid].to(dtype)
+            sel = texm & (zz >= edit["lo"].reshape(-1)[pid].to(dtype)[None, :]) & \
+                (zz <= edit["hi"].reshape(-1)[pid].to(dtype)[None, :])
+            wcs = [(1.0 - ax) * (1.0 - ay), (1.0 - ax) * ay, ax * (1.0 - ay), ax * ay]
+            for (ii, jj), wc in zip(((i0, j0), (i0, j1), (i1, j0), (i1, j1)), wcs):
+                bw = wc * w
+                baw = bw * ea[None, :]
+                vals = torch.stack([baw * erg[None, :, 0], baw * erg[None, :, 1], baw * erg[None, :, 2], baw, bw], -1)
+                idx = (off + ii * w_ + jj)[sel]
+                edit["out"].index_add_(0, idx, vals[sel].to(torch.float64))
         kk = torch.arange(K)[:, None].expand(K, P)
         last = torch.where(incl, kk, torch.full_like(kk, -1)).max(0).values
         rows["img"].append(img); rows["depth"].append(depth); rows["reg"].append(reg)
@@ -523,6 +536,21 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions):
     if new_dec is not None:
         res["decisions"] = new_dec
     return res
+
+
+def texture_edit(inp: RasterInputs, edit_rgb, edit_alpha, depth_lo, depth_hi, bins=None):
+    """raster.hip:texture_edit_kernel (gstex.py:579-606).  The fp32 decision pass of the forward
+    (same inclusion, weights w = alpha * T, hit depth, texel cell) with the stroke scattered to the
+    texels: out[texel] += b * w * (a*rgb, a, 1) for pairs with depth_lo <= z <= depth_hi.  Per-pair
+    products in fp32 (the kernel's operation order), sums in fp64; returns (T, 5) float64."""
+    cam = inp.cam
+    if bins is None:
+        bins = bin_and_sort(inp.centers, inp.extents, inp.depths, cam.H, cam.W, cam.block)
+    n_tex = inp.texture.shape[0]
+    edit = dict(rgb=edit_rgb, a=edit_alpha, lo=depth_lo, hi=depth_hi,
+                out=torch.zeros((n_tex, 5), dtype=torch.float64))
+    _render(inp, F32, bins[1], bins[2], None, edit=edit)
+    return edit["out"]
 
 
 # ----------------------------------------------------------------------------------------

@@ -330,3 +330,34 @@ def test_fused_loss_matches_eager_torch(C):
         scale = float(b.grad.abs().max())
         assert err <= 1e-5 * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
     assert float(leaves[1].grad[:, :, 3:].abs().sum()) == 0.0
+
+
+# ---------------------------------------------------------------- texture_edit (viewer paint tool, §8f-4)
+@pytest.mark.parametrize("seed", [31, 32])
+def test_texture_edit_matches_oracle(seed):
+    import gstex_cuda
+
+    case = make_case(n=400, n_texels=30000, H=64, W=80, seed=seed, settings=1 << 13)
+    inp, v = case.inp, case.view
+    H, W = inp.cam.H, inp.cam.W
+    g = torch.Generator().manual_seed(seed)
+    rgb = torch.rand(H, W, 3, generator=g)
+    a = (torch.rand(H, W, generator=g) > 0.3).float() * torch.rand(H, W, generator=g)
+    depth = O.rasterize(inp)[0]["depth"]  # the caller's depth render (gstex.py:572-574)
+    dlo, dhi = depth - 1e-2, depth + 1e-2
+    ref = O.texture_edit(inp, rgb, a, dlo, dhi)
+    dv = lambda t: t.detach().to(DEV).contiguous()  # noqa: E731
+    n = inp.means.shape[0]
+    out = gstex_cuda.texture_edit(
+        (n, 1, 5), dv(inp.texture_dims), dv(rgb), dv(a[..., None]), dv(dlo), dv(dhi), dv(inp.centers),
+        dv(inp.extents), dv(inp.depths), dv(case.nth), dv(inp.opacities), dv(inp.means), dv(inp.scales), 1.0,
+        dv(inp.quats), dv(inp.uv0), dv(inp.umap), dv(inp.vmap), dv(v.viewmat), dv(v.c2w), v.fx, v.fy, v.cx, v.cy,
+        H, W, 16, 1 << 13, background=torch.zeros(3, device=DEV))
+    got = out.double().cpu()
+    assert got.shape == ref.shape
+    assert float(ref[:, 4].sum()) > 1.0, "the stroke must reach texels"
+    touched_ref, touched = ref[:, 4] > 0, got[:, 4] > 0
+    assert torch.equal(touched_ref, touched), "the same texels are painted (integer decisions)"
+    err = (got - ref).abs().max(0).values
+    scale = ref.abs().max(0).values
+    assert bool((err <= 1e-5 * scale + 1e-9).all()), (err, scale)  # float atomics: summation order only

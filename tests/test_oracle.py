@@ -226,3 +226,27 @@ def test_sh_low_orders():
     out1 = O.spherical_harmonics(1, dirs, coeffs)
     expect_z = torch.tensor([1.0, 0.0, 0.0])[:, None] * float(O.SH_C1)
     assert torch.allclose(out1, float(O.SH_C0) + expect_z, atol=1e-6)
+
+
+def test_texture_edit_uniform_stroke_known_answer():
+    # one opaque-ish splat facing the camera, 4x4 texels; a uniform stroke (a = 1, rgb = c) over the
+    # whole image with an open depth window: every touched texel gets colour c and blend weight 1
+    inp = facing_camera_case([((0.0, 0.0, 2.0), 0.05, 0.8, (0.1, 0.2, 0.3))], tex_hw=(4, 4), settings=1 << 13)
+    H, W = inp.cam.H, inp.cam.W
+    c = torch.tensor([0.2, 0.4, 0.6])
+    rgb = c.expand(H, W, 3).clone()
+    a = torch.ones(H, W)
+    out = O.texture_edit(inp, rgb, a, torch.full((H, W), -1e9), torch.full((H, W), 1e9))
+    touched = out[:, 4] > 0
+    assert int(touched.sum()) == 16, "every texel of the block is reached"
+    assert torch.allclose(out[touched, 3] / out[touched, 4], torch.ones(16, dtype=F64), atol=1e-6)
+    col = out[touched, :3] / out[touched, 3:4]
+    assert torch.allclose(col, c.to(F64).expand_as(col), atol=1e-6)
+    # half-transparent stroke: weight a; closed depth window: nothing
+    out2 = O.texture_edit(inp, rgb, torch.full((H, W), 0.25), torch.full((H, W), -1e9), torch.full((H, W), 1e9))
+    assert torch.allclose(out2[touched, 3] / out2[touched, 4], torch.full((16,), 0.25, dtype=F64), atol=1e-6)
+    out3 = O.texture_edit(inp, rgb, a, torch.full((H, W), 2.5), torch.full((H, W), 3.0))
+    assert float(out3.abs().sum()) == 0.0
+    # total weight: sum_texels out[:, 4] = sum_pixels w (bilinear weights sum to 1 per pair)
+    fwd = O._render(inp, torch.float32, *O.bin_and_sort(inp.centers, inp.extents, inp.depths, H, W)[1:3], None)
+    assert abs(float(out[:, 4].sum()) - float(fwd["out"]["alpha"].double().sum())) < 1e-4

@@ -41,7 +41,7 @@ def test_no_cpu_rasterizer():
     with pytest.raises(NotImplementedError):
         gstex_cuda.texture_gaussians(*([None] * 26), use_torch_impl=True)
     with pytest.raises(NotImplementedError):
-        gstex_cuda.texture_edit()
+        gstex_cuda.texture_edit(*([None] * 28), use_torch_impl=True)
 
 
 def test_torch_impl_rotation_matches_nerfstudio_convention():
