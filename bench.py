@@ -114,9 +114,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        # "nccl" is RCCL on ROCm; GSTEX_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        dist.init_process_group(os.environ.get("GSTEX_DIST_BACKEND", "nccl"), init_method="env://")
+    dev_idx = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
 
     from gstex_amd import ops
     from gstex_amd.dist import GradSync

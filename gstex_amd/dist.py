@@ -21,12 +21,22 @@ import torch.distributed as dist
 
 
 class GradSync:
-    def __init__(self, trainer, world_size: int, group=None):
+    """overlap_tail: the last parameter (the texel store, ~73 % of the bytes at cfg3) gets its own
+    asynchronous all-reduce from a post-accumulate-grad hook, i.e. as soon as the raster backward has
+    produced it, overlapping the collective with the rest of the backward (setup_bwd, SH, activations);
+    all_reduce() then reduces the head of the buffer and waits for both."""
+
+    def __init__(self, trainer, world_size: int, group=None, overlap_tail: bool = True):
         self.trainer = trainer
         self.world = world_size
         self.group = group
+        self.overlap_tail = overlap_tail
         self._shapes = None
         self.flat = None
+        self._tail_off = 0
+        self._hook = None
+        self._hooked = None
+        self._work = None
         self.rebuild()
 
     def _params(self):
@@ -46,7 +56,23 @@ class GradSync:
             p.grad = self.flat[off:off + n].view_as(p)
             off += n
         self._shapes = shapes
+        self._tail_off = total - params[-1].numel()
+        self._install_hook(params[-1])
         return True
+
+    def _install_hook(self, tail):
+        if not self.overlap_tail or self._hooked is tail:
+            return
+        if self._hook is not None:
+            self._hook.remove()
+        self._hooked = tail
+        self._hook = tail.register_post_accumulate_grad_hook(self._tail_ready)
+
+    def _tail_ready(self, param):
+        # fires once the texel gradient is final for this backward; the view is still the flat buffer's
+        if self._work is None and param.grad is not None and param.grad.data_ptr() == self.flat[self._tail_off:].data_ptr():
+            self._work = dist.all_reduce(self.flat[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
+                                         async_op=True)
 
     @property
     def nbytes(self) -> int:
@@ -57,9 +83,16 @@ class GradSync:
         self.flat.zero_()
 
     def all_reduce(self):
-        """Average the flat gradient buffer over all ranks (one collective)."""
-        self.rebuild_if_detached()
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        """Average the flat gradient buffer over all ranks (the tail's collective may already be running)."""
+        work, self._work = self._work, None
+        if work is not None and [tuple(p.shape) for p in self._params()] == self._shapes:
+            dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
+            work.wait()
+        else:
+            if work is not None:
+                work.wait()
+            self.rebuild_if_detached()
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
 
     def rebuild_if_detached(self):

@@ -31,16 +31,17 @@ class _Params:
         return [self.means, self.unused, self.texture]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         p = _Params(rank, 6)
-        sync = GradSync(p, world)
+        sync = GradSync(p, world, overlap_tail=overlap)
         sync.zero()
         # rank-dependent "loss": gradients differ per rank (independent cameras)
         ((rank + 1) * p.means.sum() + (rank + 2) * (p.texture ** 2).sum()).backward()
         assert p.means.grad.data_ptr() == sync.flat.data_ptr(), "grads must be views of the flat buffer"
+        assert (sync._work is not None) == overlap, "the texel-gradient collective starts inside backward"
         sync.all_reduce()
         exp_means = torch.full((10, 3), (1 + 2) / 2.0)
         exp_tex = 2 * p.texture.detach() * ((2 + 3) / 2.0)
@@ -57,11 +58,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_grad_all_reduce_world2():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_grad_all_reduce_world2(overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=120) for _ in procs]
