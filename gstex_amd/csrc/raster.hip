@@ -87,14 +87,31 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch
 #endif
+#ifndef GSTEX_TEX_FIXED
+#define GSTEX_TEX_FIXED 1  // stage texel gradients as int64 fixed point (ds_add_u64) instead of ds_add_f32
+#endif
 #ifndef GSTEX_BWD_BATCH
-#define GSTEX_BWD_BATCH 32
+#define GSTEX_BWD_BATCH (GSTEX_TEX_FIXED ? 16 : 32)  // fixed point: 8-B slots, half the splats per batch
 #endif
 constexpr int kBwdBatch = GSTEX_BWD_BATCH;
 #ifndef GSTEX_TEX_LDS
-#define GSTEX_TEX_LDS 6016
+#define GSTEX_TEX_LDS (GSTEX_TEX_FIXED ? 8064 : 6016)  // what four workgroups per CU leave of the 160 KiB
 #endif
-constexpr int kTexLds = GSTEX_TEX_LDS;  // floats of per-workgroup LDS texel-gradient staging (23.5 KiB: four workgroups per CU)
+constexpr int kTexLds = GSTEX_TEX_LDS;  // 4-B words of per-workgroup LDS texel-gradient staging
+constexpr int kTexCap = GSTEX_TEX_FIXED ? kTexLds / 2 : kTexLds;  // staged values per batch
+
+// Texel-gradient fixed point.  The LDS float-atomic path costs the CU ~2 LDS cycles per active lane
+// (the shared bottleneck of the backward: ~90 % of its LDS-busy cycles); 64-bit integer adds cost a
+// fraction of that and are order-independent.  Per tile, e = exponent of max|dL/dtex| over its pixels;
+// one staged value (a per-(tile, splat) texel sum) is bounded by 4 corners x 256 pixels x that max
+// < 2^(e+10), so values are held as round(v * 2^S) with S = 41 - e (|x| < 2^51, resolution 2^-41 of
+// the tile's largest upstream texel gradient).  The conversion rounds through fp64: x + 1.5*2^52 puts
+// the integer in the low mantissa bits (exact for |x| < 2^51).
+__device__ __forceinline__ long long fixed_from(float v, int S) {
+    const double d = __builtin_ldexp((double)v, S);
+    return __double_as_longlong(d + 0x1.8p52) - __double_as_longlong(0x1.8p52);
+}
+__device__ __forceinline__ float fixed_to(long long q, int S) { return __builtin_ldexpf((float)q, -S); }
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -548,8 +565,9 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     __shared__ float s_part[kBwdBatch][4][kNP];
     __shared__ int s_slot[kBwdBatch];
     __shared__ int s_toff[kBwdBatch];  // LDS offset of each splat's texel-gradient block (-1: global)
-    __shared__ int s_nfit, s_used;
-    __shared__ float s_tex[kTexLds];
+    __shared__ int s_nfit, s_used, s_gexp;
+    __shared__ unsigned long long s_texq[kTexLds / 2];
+    float* s_tex = reinterpret_cast<float*>(s_texq);  // float staging (GSTEX_TEX_FIXED = 0)
     __shared__ int s_maxlast;
     __shared__ unsigned s_live[4];  // per wave: batch splats whose s_part row this wave wrote
 
@@ -591,12 +609,28 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
 
-    if (tid == 0) s_maxlast = -1;
-    for (int i = tid; i < kTexLds; i += kThreads) s_tex[i] = 0.f;
+    if (tid == 0) {
+        s_maxlast = -1;
+        s_gexp = 0;  // bits of max |dL/dtex| over the tile (non-negative floats order as ints)
+    }
+    for (int i = tid; i < kTexLds / 2; i += kThreads) s_texq[i] = 0ull;
     __syncthreads();
     if (last >= 0) atomicMax(&s_maxlast, last);
+    if (GSTEX_TEX_FIXED) {
+        float gm = 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) gm = fmaxf(gm, fabsf(Gtex[c]));
+        if (gm > 0.f) atomicMax(&s_gexp, __float_as_int(gm));
+    }
     __syncthreads();
     const int tile_last = s_maxlast;
+    int tex_S = 0;
+    if (GSTEX_TEX_FIXED) {
+        int e = 0;
+        const float gmax = __int_as_float(s_gexp);
+        if (gmax > 0.f) (void)frexpf(gmax, &e);  // gmax < 2^e
+        tex_S = 41 - e;
+    }
     int wave_last = last;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wave_last = max(wave_last, __shfl_xor(wave_last, o, 64));
@@ -632,7 +666,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 const int t = __shfl_up(incl, o, 64);
                 if (lane >= o) incl += t;
             }
-            const bool fits = incl <= kTexLds;
+            const bool fits = incl <= kTexCap;
             if (lane < kBwdBatch) s_toff[lane] = (lane < nb && fits) ? incl - sz : -1;
             const unsigned long long fm = __ballot(fits && lane < nb);
             if (lane == 0) {
@@ -828,7 +862,17 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
                     const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
                     const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
-                    if (toff >= 0) {
+                    if (GSTEX_TEX_FIXED && toff >= 0) {
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) {
+                            if (c < Cn) {
+                                atomicAdd(&s_texq[toff + c00 + c], (unsigned long long)fixed_from(tg[c], tex_S));
+                                atomicAdd(&s_texq[toff + c01 + c], (unsigned long long)fixed_from(tg[CM + c], tex_S));
+                                atomicAdd(&s_texq[toff + c10 + c], (unsigned long long)fixed_from(tg[2 * CM + c], tex_S));
+                                atomicAdd(&s_texq[toff + c11 + c], (unsigned long long)fixed_from(tg[3 * CM + c], tex_S));
+                            }
+                        }
+                    } else if (toff >= 0) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
@@ -876,7 +920,14 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         {
             const int used = s_used, nfit = s_nfit;
             for (int idx = tid; idx < used; idx += kThreads) {
-                const float val = s_tex[idx];
+                float val;
+                if (GSTEX_TEX_FIXED) {
+                    const long long q = (long long)s_texq[idx];
+                    val = fixed_to(q, tex_S);
+                    if (q != 0) s_texq[idx] = 0ull;
+                } else {
+                    val = s_tex[idx];
+                }
                 if (val != 0.0f) {
                     int lo = 0, hi = nfit - 1;  // last j with s_toff[j] <= idx
                     while (lo < hi) {
@@ -886,7 +937,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     }
                     const int off = __float_as_int(s_rec[6 * kBwdBatch + lo].z);
                     atomicAdd(v_texture + (size_t)off * Cn + (idx - s_toff[lo]), val);
-                    s_tex[idx] = 0.0f;
+                    if (!GSTEX_TEX_FIXED) s_tex[idx] = 0.0f;
                 }
             }
         }
