@@ -324,6 +324,22 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     return h.alpha >= kAlphaMin;
 }
 
+// One texel's channels: with C == 3 a single 12-B global_load_dwordx3 (the three channels share a cache
+// line; three dword loads would look the same lines up three times in the vL1D).
+struct __attribute__((aligned(4))) Texel3 { float v[3]; };
+template <int CM>
+__device__ __forceinline__ void load_texel(const float* __restrict__ p, int Cn, float (&out)[CM]) {
+    if constexpr (CM == 3) {
+        const Texel3 t = *reinterpret_cast<const Texel3*>(p);
+        out[0] = t.v[0];
+        out[1] = t.v[1];
+        out[2] = t.v[2];
+    } else {
+#pragma unroll
+        for (int c = 0; c < CM; ++c) out[c] = (c < Cn) ? p[c] : 0.0f;
+    }
+}
+
 __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float& tu, float& tv) {
     tu = r.tu0 + (u * r.auu + v * r.auv);
     tv = r.tv0 + (u * r.avu + v * r.avv);
@@ -403,11 +419,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
                 const float* tblk = texture + (size_t)r.off * Cn;  // wave-uniform block base
                 const int o00 = (b.i0 * r.w + b.j0) * Cn, o01 = (b.i0 * r.w + b.j1) * Cn;
                 const int o10 = (b.i1 * r.w + b.j0) * Cn, o11 = (b.i1 * r.w + b.j1) * Cn;
+                float t00[CM], t01[CM], t10[CM], t11[CM];
+                load_texel<CM>(tblk + o00, Cn, t00);
+                load_texel<CM>(tblk + o01, Cn, t01);
+                load_texel<CM>(tblk + o10, Cn, t10);
+                load_texel<CM>(tblk + o11, Cn, t11);
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < Cn) {
-                        float val = bilerp_mix(tblk[o00 + c], tblk[o01 + c], tblk[o10 + c], tblk[o11 + c], b.ax,
-                                               b.ay);
+                        float val = bilerp_mix(t00[c], t01[c], t10[c], t11[c], b.ax, b.ay);
                         tex[c] = tex[c] + val * w;
                     }
                 }
@@ -727,11 +747,18 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                         o10 = (b.i1 * r.w + b.j0) * Cn;
                         o11 = (b.i1 * r.w + b.j1) * Cn;
                         const float hf = (float)r.h, wf = (float)r.w;
+                        float t00[CM], t01[CM], t10[CM], t11[CM];
+                        if (!(GSTEX_ABLATE & 8)) {
+                            load_texel<CM>(tblk + o00, Cn, t00);
+                            load_texel<CM>(tblk + o01, Cn, t01);
+                            load_texel<CM>(tblk + o10, Cn, t10);
+                            load_texel<CM>(tblk + o11, Cn, t11);
+                        }
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn && !(GSTEX_ABLATE & 8)) {
-                                const float v00 = tblk[o00 + c], v01 = tblk[o01 + c];
-                                const float v10 = tblk[o10 + c], v11 = tblk[o11 + c];
+                                const float v00 = t00[c], v01 = t01[c];
+                                const float v10 = t10[c], v11 = t11[c];
                                 tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay);
                                 const float gt = w * Gtex[c];
                                 if (b.in_u)
