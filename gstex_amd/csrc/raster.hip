@@ -352,7 +352,8 @@ template <int C>
 __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
-    const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float* __restrict__ out_img,
+    const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float tex_scale, float tex_bias,
+    float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
     float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state) {
     const Camera cam = load_camera(cam_args);
@@ -427,7 +428,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < Cn) {
-                        float val = bilerp_mix(t00[c], t01[c], t10[c], t11[c], b.ax, b.ay);
+                        // texel value = tex_scale * stored + tex_bias (affine, so applied after interpolation)
+                        const float val = bilerp_mix(t00[c], t01[c], t10[c], t11[c], b.ax, b.ay) * tex_scale + tex_bias;
                         tex[c] = tex[c] + val * w;
                     }
                 }
@@ -574,7 +576,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots,
-    const float* __restrict__ texture, const float4* __restrict__ state, const float* __restrict__ v_img,
+    const float* __restrict__ texture, float tex_scale, float tex_bias, const float4* __restrict__ state,
+    const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
     float* __restrict__ v_texture) {
@@ -640,6 +643,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         float gm = 0.f;
 #pragma unroll
         for (int c = 0; c < CM; ++c) gm = fmaxf(gm, fabsf(Gtex[c]));
+        gm *= fabsf(tex_scale);
         if (gm > 0.f) atomicMax(&s_gexp, __float_as_int(gm));
     }
     __syncthreads();
@@ -759,7 +763,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                             if (c < Cn && !(GSTEX_ABLATE & 8)) {
                                 const float v00 = t00[c], v01 = t01[c];
                                 const float v10 = t10[c], v11 = t11[c];
-                                tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay);
+                                tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay) * tex_scale + tex_bias;
                                 const float gt = w * Gtex[c];
                                 if (b.in_u)
                                     dtu += gt * (hf * ((1.0f - b.ay) * (v10 - v00) + b.ay * (v11 - v01)));
@@ -791,7 +795,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     // texel gradients: per-lane bilinear contributions, scattered after the branch
                     if (has_tex && !(GSTEX_ABLATE & 1)) {
                         tkey = (b.i0 * r.w + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
-                        tw = w;
+                        tw = w * tex_scale;  // d value / d stored texel
                         tax = b.ax;
                         tay = b.ay;
                     }
@@ -804,6 +808,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                         drho = dL_dalpha * h.a_raw * -0.5f;
                     }
                     // texture coordinates
+                    dtu *= tex_scale;  // the raw-value differences above, in value units
+                    dtv *= tex_scale;
                     P[P_TU0] = dtu; P[P_AUU] = dtu * h.u; P[P_AUV] = dtu * h.v;
                     P[P_TV0] = dtv; P[P_AVU] = dtv * h.u; P[P_AVV] = dtv * h.v;
                     float du = dtu * r.auu + dtv * r.avu;
@@ -1159,7 +1165,7 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
 extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                                 const float* background, const float* records, const int32_t* tile_ranges,
                                 const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
-                                int64_t n_texels, float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
+                                int64_t n_texels, float tex_scale, float tex_bias, float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
                                 float* out_normal, float* state, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_fwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
@@ -1177,7 +1183,8 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 #define GSTEX_FWD(CC)                                                                                          \
     raster_fwd_kernel<CC><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,          \
                                                      (const float4*)records, (const int2*)tile_ranges,        \
-                                                     tile_order, sorted_ids, texture, out_img, out_depth, out_reg,        \
+                                                     tile_order, sorted_ids, texture, tex_scale, tex_bias, out_img,       \
+                                                     out_depth, out_reg,                                                  \
                                                      out_alpha, out_tex, out_normal, (float4*)state)
     if (channels == 3) GSTEX_FWD(3);
     else if (channels == 6) GSTEX_FWD(6);
@@ -1189,7 +1196,8 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                                 const float* background, const float* records, const int32_t* tile_ranges,
                                 const int32_t* tile_order, const int32_t* sorted_ids, const int32_t* sorted_slots,
-                                const float* texture, int64_t n_texels, const float* state, const float* v_img,
+                                const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
+                                const float* state, const float* v_img,
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, float* partials, float* v_texture, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
@@ -1207,7 +1215,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
 #define GSTEX_BWD(CC)                                                                                          \
     raster_bwd_kernel<CC><<<nblk, kThreads, 0, st>>>(                                                          \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
-        tile_order, sorted_ids, sorted_slots, texture, (const float4*)state, v_img, v_depth, v_reg, v_alpha, v_tex,       \
+        tile_order, sorted_ids, sorted_slots, texture, tex_scale, tex_bias, (const float4*)state, v_img, v_depth,      \
+        v_reg, v_alpha, v_tex,                                                                                  \
         v_normal, partials, v_texture)
     if (channels == 3) GSTEX_BWD(3);
     else if (channels == 6) GSTEX_BWD(6);

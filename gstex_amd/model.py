@@ -40,6 +40,7 @@ LRS = {
     "texture_dc": 1e-3,
 }
 DEFAULT_SETTINGS = (1 << 9) | (1 << 10)
+SH_C0 = 0.28209479177387814  # SH2RGB(x) = SH_C0 * x + 0.5 (gstex.py:94-99)
 
 
 def _gauss_window(size=11, sigma=1.5, device=None):
@@ -169,11 +170,13 @@ class GStexTrainer:
             rgbs = ops.spherical_harmonics(deg, viewdirs, colors)
         else:
             rgbs = torch.sigmoid(self.features_dc)
-        texture = SH2RGB(self.texture_dc)
+        # SH2RGB(texture_dc) (gstex.py:1119) applied by the raster on read instead of materialised
+        texture = self.texture_dc
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
-            ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background))
+            ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
+            texture_transform=(SH_C0, 0.5))
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],

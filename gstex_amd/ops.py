@@ -231,7 +231,7 @@ class _TextureGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
-                block_width, settings, background):
+                block_width, settings, background, texture_transform=None):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -267,6 +267,8 @@ class _TextureGaussians(torch.autograd.Function):
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
              ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
              st)
+        ctx_scale, ctx_bias = (1.0, 0.0) if texture_transform is None else (float(texture_transform[0]),
+                                                                             float(texture_transform[1]))
         f = dict(device=dev, dtype=torch.float32)
         img = torch.empty((H, W, 3), **f)
         depth = torch.empty((H, W), **f)
@@ -277,7 +279,8 @@ class _TextureGaussians(torch.autograd.Function):
         state = torch.empty((H, W, 4), **f)
         _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
-             ptr(texture), texture.shape[0], ptr(img), ptr(depth), ptr(reg), ptr(alpha), ptr(tex), ptr(normal),
+             ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), ptr(depth), ptr(reg), ptr(alpha),
+             ptr(tex), ptr(normal),
              ptr(state), st)
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
@@ -285,6 +288,7 @@ class _TextureGaussians(torch.autograd.Function):
         ctx.has_c2w = cw is not None
         ctx.has_bg = bg is not None
         ctx.args = (float(glob_scale), float(fx), float(fy), float(cx), float(cy), H, W, C, int(settings))
+        ctx.tex_affine = (ctx_scale, ctx_bias)
         return img, depth, reg, alpha, tex, normal
 
     @staticmethod
@@ -312,7 +316,8 @@ class _TextureGaussians(torch.autograd.Function):
         partials = torch.empty((n_isect, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
         v_texture = torch.zeros_like(texture)
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
-             ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ptr(state), ptr(v_img), ptr(v_depth),
+             ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0], ctx.tex_affine[1],
+             ptr(state), ptr(v_img), ptr(v_depth),
              ptr(v_reg), ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), st)
         v_means = torch.empty_like(means)
         v_scales = torch.empty_like(scales)
@@ -328,13 +333,17 @@ class _TextureGaussians(torch.autograd.Function):
         if ctx.needs_input_grad[26]:
             v_bg = (v_img * state[..., 0:1]).sum((0, 1))
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
-                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg)
+                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
-                      block_width, settings, background=None, use_torch_impl=False):
+                      block_width, settings, background=None, use_torch_impl=False, texture_transform=None):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
+
+    texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
+    texel values s * texture + b, so SH2RGB(texture_dc) (gstex.py:1119) need not be materialised: pass
+    texture_dc with (0.28209479177387814, 0.5); the texture gradient is then w.r.t. the stored values.
 
     Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
     Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
@@ -346,7 +355,7 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
             "the CPU restatement in oracle/ is test infrastructure only")
     return _TextureGaussians.apply(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs,
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
-                                   c2w, fx, fy, cx, cy, H, W, block_width, settings, background)
+                                   c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform)
 
 
 rasterize_gaussians = texture_gaussians  # north_star name

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 2
+#define GSTEX_ABI_VERSION 3
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -120,13 +120,16 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
                        const float* vmap, const int32_t* texture_dims,
                        const int32_t* num_tiles_hit, const gstex_camera* cam, float* records,
                        void* stream);
+/* Texel values: the texels are read as tex_scale * texture + tex_bias (1, 0 = as stored), so a caller
+ * that keeps SH-DC coefficients (gstex.py:1119 passes SH2RGB(texture_dc) = 0.28209 x + 0.5) can pass the
+ * store itself; the backward's v_texture is then the gradient w.r.t. the stored values. */
 /* Forward composite. Outputs are [H][W][k] row-major. state[H*W][4] = {T_final, M1, M2,
  * last_contributor (as int bits)} is saved for the backward pass. background is a device
  * float[3] (or NULL = black) added as T_final * background. */
 int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
-                     int64_t n_texels,
+                     int64_t n_texels, float tex_scale, float tex_bias,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                      float* out_tex, float* out_normal, float* state, void* stream);
 /* Backward composite. Needs the forward state and the same tile_order. Writes
@@ -136,7 +139,8 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* tile_order, const int32_t* sorted_ids,
                      const int32_t* sorted_slots, const float* texture, int64_t n_texels,
-                     const float* state, const float* v_img, const float* v_depth,
+                     float tex_scale, float tex_bias, const float* state, const float* v_img,
+                     const float* v_depth,
                      const float* v_reg, const float* v_alpha, const float* v_tex,
                      const float* v_normal, float* partials, float* v_texture, void* stream);
 /* Sums each splat's partials and chains them to the splat parameters. Outputs are overwritten. */

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import DIFF, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, oracle_run
+from helpers import DIFF, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, oracle_run, upstream
 from oracle import raster as O
 
 pytestmark = pytest.mark.gpu
@@ -361,3 +361,36 @@ def test_texture_edit_matches_oracle(seed):
     err = (got - ref).abs().max(0).values
     scale = ref.abs().max(0).values
     assert bool((err <= 1e-5 * scale + 1e-9).all()), (err, scale)  # float atomics: summation order only
+
+
+# ---------------------------------------------------------------- texel affine (SH2RGB on read)
+def test_texture_transform_equals_materialised_sh2rgb():
+    from gstex_amd import ops
+
+    case = make_case(n=400, n_texels=30000, H=64, W=80, seed=17)
+    inp, v = case.inp, case.view
+    C0 = 0.28209479177387814
+    g = torch.Generator().manual_seed(3)
+    dc = torch.randn(inp.texture.shape, generator=g)
+    dv = lambda t: t.detach().to(DEV).contiguous()  # noqa: E731
+    n = inp.means.shape[0]
+
+    def run(tex_leaf, transform):
+        args = ((n, 1, 3), dv(inp.texture_dims), dv(inp.centers), dv(inp.extents), dv(inp.depths), dv(case.nth),
+                dv(inp.rgbs), dv(inp.opacities), dv(inp.means), dv(inp.scales), 1.0, dv(inp.quats), dv(inp.uv0),
+                dv(inp.umap), dv(inp.vmap))
+        outs = ops.texture_gaussians(*args, tex_leaf, dv(v.viewmat), dv(v.c2w), v.fx, v.fy, v.cx, v.cy,
+                                     inp.cam.H, inp.cam.W, 16, inp.settings, texture_transform=transform)
+        up = upstream(inp.cam.H, inp.cam.W, 3, 5)
+        names = ["img", "depth", "reg", "alpha", "tex", "normal"]
+        torch.autograd.backward(list(outs), [up[k].to(DEV) for k in names])
+        return [o.detach().cpu() for o in outs]
+
+    leaf_dc = dv(dc).requires_grad_(True)
+    o1 = run(leaf_dc, (C0, 0.5))
+    leaf_tex = (dv(dc) * C0 + 0.5).detach().requires_grad_(True)  # charts.SH2RGB, materialised
+    o2 = run(leaf_tex, None)
+    for a, b in zip(o1, o2):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+    gd, gt = leaf_dc.grad.double().cpu(), leaf_tex.grad.double().cpu() * C0
+    assert float((gd - gt).norm() / gt.norm()) < 1e-6
