@@ -138,6 +138,8 @@ CASES = {
     "opaque": dict(n=300, n_texels=20000, H=64, W=64, seed=7, opacity=0.98),
     "background": dict(n=200, n_texels=10000, H=50, W=70, seed=8, bg=(0.2, 0.5, 0.9)),
     "ragged_17x33": dict(n=150, n_texels=5000, H=17, W=33, seed=9),
+    # ~1000 texels per splat: 16-splat batches overflow the LDS staging -> global-atomic texel path
+    "big_texel_blocks": dict(n=60, n_texels=60000, H=64, W=64, seed=10),
 }
 
 
@@ -394,3 +396,33 @@ def test_texture_transform_equals_materialised_sh2rgb():
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
     gd, gt = leaf_dc.grad.double().cpu(), leaf_tex.grad.double().cpu() * C0
     assert float((gd - gt).norm() / gt.norm()) < 1e-6
+
+
+@pytest.mark.parametrize("gscale", [1e-20, 1e12])
+def test_texel_fixed_point_scale_invariance(gscale):
+    # the backward's per-tile fixed-point scale follows the upstream texel-gradient magnitude: scaling
+    # dL/dtex by any factor scales v_texture by the same factor to fp32 accuracy
+    case = make_case(n=300, n_texels=20000, H=64, W=80, seed=12)
+    import helpers
+
+    orig = helpers.upstream
+
+    def scaled(H, W, C, seed=5):
+        up = orig(H, W, C, seed)
+        up = {k: torch.zeros_like(v) for k, v in up.items()} | {"tex": up["tex"] * gscale}
+        return up
+
+    def unit(H, W, C, seed=5):
+        up = orig(H, W, C, seed)
+        return {k: torch.zeros_like(v) for k, v in up.items()} | {"tex": up["tex"]}
+
+    try:
+        helpers.upstream = unit
+        _, gu = gpu_run(case, grads=True, seed=5)
+        helpers.upstream = scaled
+        _, gs = gpu_run(case, grads=True, seed=5)
+    finally:
+        helpers.upstream = orig
+    a, b = gs["texture"].double() / gscale, gu["texture"].double()
+    assert float(b.abs().max()) > 0
+    assert float((a - b).norm() / b.norm()) < 1e-6
