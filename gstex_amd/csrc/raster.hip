@@ -733,52 +733,64 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     const float one_m = 1.0f - h.alpha;
                     T = T * grad_rcp(one_m);
                     const float w = h.alpha * T;
-                    // texture value and its uv-gradient
-                    float tau[CM];
-                    float dtu = 0.f, dtv = 0.f, tu = 0.f, tv = 0.f;
-#pragma unroll
-                    for (int c = 0; c < CM; ++c) tau[c] = 0.f;
+                    // issue the texel gathers first, then everything that does not need them, so the loads'
+                    // latency overlaps that work
                     const bool has_tex = r.h * r.w > 0;
                     Bilerp b;
                     // wave-uniform block base (scalar) + 32-bit per-lane offsets
                     const float* tblk = texture + (size_t)r.off * Cn;
-                    int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
+                    float t00[CM], t01[CM], t10[CM], t11[CM];
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
                     if (has_tex) {
+                        float tu, tv;
                         tex_coords(r, h.u, h.v, tu, tv);
                         b = bilerp_coords(tu, tv, r.h, r.w);
-                        o00 = (b.i0 * r.w + b.j0) * Cn;
-                        o01 = (b.i0 * r.w + b.j1) * Cn;
-                        o10 = (b.i1 * r.w + b.j0) * Cn;
-                        o11 = (b.i1 * r.w + b.j1) * Cn;
-                        const float hf = (float)r.h, wf = (float)r.w;
-                        float t00[CM], t01[CM], t10[CM], t11[CM];
                         if (!(GSTEX_ABLATE & 8)) {
-                            load_texel<CM>(tblk + o00, Cn, t00);
-                            load_texel<CM>(tblk + o01, Cn, t01);
-                            load_texel<CM>(tblk + o10, Cn, t10);
-                            load_texel<CM>(tblk + o11, Cn, t11);
-                        }
-#pragma unroll
-                        for (int c = 0; c < CM; ++c) {
-                            if (c < Cn && !(GSTEX_ABLATE & 8)) {
-                                const float v00 = t00[c], v01 = t01[c];
-                                const float v10 = t10[c], v11 = t11[c];
-                                tau[c] = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay) * tex_scale + tex_bias;
-                                const float gt = w * Gtex[c];
-                                if (b.in_u)
-                                    dtu += gt * (hf * ((1.0f - b.ay) * (v10 - v00) + b.ay * (v11 - v01)));
-                                if (b.in_v)
-                                    dtv += gt * (wf * ((1.0f - b.ax) * (v01 - v00) + b.ax * (v11 - v10)));
-                            }
+                            load_texel<CM>(tblk + (b.i0 * r.w + b.j0) * Cn, Cn, t00);
+                            load_texel<CM>(tblk + (b.i0 * r.w + b.j1) * Cn, Cn, t01);
+                            load_texel<CM>(tblk + (b.i1 * r.w + b.j0) * Cn, Cn, t10);
+                            load_texel<CM>(tblk + (b.i1 * r.w + b.j1) * Cn, Cn, t11);
                         }
                     }
                     const float iz = grad_rcp(h.z);
                     const float m = kFarRatio * (1.0f - kNear * iz);
                     const float E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
                     float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
+                    P[P_RGB + 0] = w * Gimg[0];
+                    P[P_RGB + 1] = w * Gimg[1];
+                    P[P_RGB + 2] = w * Gimg[2];
+                    P[P_NRM + 0] = w * Gn[0];
+                    P[P_NRM + 1] = w * Gn[1];
+                    P[P_NRM + 2] = w * Gn[2];
+                    // depth: direct + distortion (m depends on z)
+                    float dz = w * Gd;
+                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
+                    // texel gradients: per-lane bilinear contributions, scattered after the P reduction
+                    if (has_tex && !(GSTEX_ABLATE & 1)) {
+                        tkey = (b.i0 * r.w + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
+                        tw = w * tex_scale;  // d value / d stored texel
+                        tax = b.ax;
+                        tay = b.ay;
+                    }
+                    // texture value (tex_scale * stored + tex_bias) and its uv-gradient
+                    float dtu = 0.f, dtv = 0.f;
+                    if (has_tex) {
+                        const float hf = (float)r.h, wf = (float)r.w;
 #pragma unroll
-                    for (int c = 0; c < CM; ++c)
-                        if (c < Cn) g += Gtex[c] * tau[c];
+                        for (int c = 0; c < CM; ++c) {
+                            if (c < Cn) {
+                                const float v00 = t00[c], v01 = t01[c], v10 = t10[c], v11 = t11[c];
+                                const float tau = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay) * tex_scale + tex_bias;
+                                g += Gtex[c] * tau;
+                                const float gt = w * Gtex[c];
+                                const float eu = gt * (hf * ((1.0f - b.ay) * (v10 - v00) + b.ay * (v11 - v01)));
+                                const float ev = gt * (wf * ((1.0f - b.ax) * (v01 - v00) + b.ax * (v11 - v10)));
+                                dtu += b.in_u ? eu : 0.0f;
+                                dtv += b.in_v ? ev : 0.0f;
+                            }
+                        }
+                    }
                     g += Gd * h.z;
                     g += (Gn[0] * r.nrm[0] + Gn[1] * r.nrm[1]) + Gn[2] * r.nrm[2];
                     g += Ga;
@@ -786,22 +798,6 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     const float dL_dalpha = T * (g - R);
                     R = h.alpha * g + one_m * R;
 
-                    P[P_RGB + 0] = w * Gimg[0];
-                    P[P_RGB + 1] = w * Gimg[1];
-                    P[P_RGB + 2] = w * Gimg[2];
-                    P[P_NRM + 0] = w * Gn[0];
-                    P[P_NRM + 1] = w * Gn[1];
-                    P[P_NRM + 2] = w * Gn[2];
-                    // texel gradients: per-lane bilinear contributions, scattered after the branch
-                    if (has_tex && !(GSTEX_ABLATE & 1)) {
-                        tkey = (b.i0 * r.w + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
-                        tw = w * tex_scale;  // d value / d stored texel
-                        tax = b.ax;
-                        tay = b.ay;
-                    }
-                    // depth: direct + distortion (m depends on z)
-                    float dz = w * Gd;
-                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
                     float drho = 0.f;
                     if (h.a_raw < kAlphaMax) {
                         P[P_OPAC] = dL_dalpha * h.G;
