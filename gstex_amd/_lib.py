@@ -93,6 +93,10 @@ SIGNATURES = {
     "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_texture_sample": (c_int32, [c_int64, c_int32, _P, _P, c_int64, _P, _P, _P]),
     "gstex_texture_sample_bwd": (c_int32, [c_int64, c_int32, _P, c_int64, _P, _P, _P, _P]),
+    "gstex_activate_fwd": (c_int32, [c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gstex_activate_bwd": (c_int32, [c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gstex_sh_rest_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
+    "gstex_sh_rest_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_texture_edit": (c_int32, [_CAM, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, c_int64, _P, _P]),
     "gstex_loss_workspace_size": (c_size_t, [c_int32, c_int32]),
     "gstex_loss_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, POINTER(c_float), c_float, _P, _P,

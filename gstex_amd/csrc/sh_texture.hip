@@ -63,16 +63,18 @@ __device__ __forceinline__ void sh_basis(int degree, float x, float y, float z, 
     b[24] = SH_C4[8] * (xx * (xx - 3.0f * yy) - yy * (3.0f * xx - yy));
 }
 
-__global__ __launch_bounds__(256) void sh_fwd_kernel(int n, int degree, int K, const float* __restrict__ dirs,
+// coeffs[i][k - k0] holds basis k (k0 = 1: the DC coefficient is implicitly zero, gstex.py:1100 zeroes it;
+// starting the sum at +0 without the zero DC product gives the same bits as with it)
+__global__ __launch_bounds__(256) void sh_fwd_kernel(int n, int degree, int k0, int K, const float* __restrict__ dirs,
                                                      const float* __restrict__ coeffs, float* __restrict__ out) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     float b[25];
     sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
     const int nb = (degree + 1) * (degree + 1);
-    const float* c = coeffs + (size_t)i * K * 3;
+    const float* c = coeffs + (size_t)i * K * 3 - 3 * k0;
     float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-    for (int k = 0; k < nb; ++k) {
+    for (int k = k0; k < nb; ++k) {
         r0 = r0 + b[k] * c[3 * k];
         r1 = r1 + b[k] * c[3 * k + 1];
         r2 = r2 + b[k] * c[3 * k + 2];
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256) void sh_fwd_kernel(int n, int degree, int K, c
     out[3 * i + 2] = r2;
 }
 
-__global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int K, const float* __restrict__ dirs,
+__global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int k0, int K, const float* __restrict__ dirs,
                                                      const float* __restrict__ v_out, float* __restrict__ v_coeffs) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int K, c
     const float g0 = v_out[3 * i], g1 = v_out[3 * i + 1], g2 = v_out[3 * i + 2];
     float* vc = v_coeffs + (size_t)i * K * 3;
     for (int k = 0; k < K; ++k) {
-        const float bk = (k < nb) ? b[k] : 0.0f;
+        const float bk = (k + k0 < nb) ? b[k + k0] : 0.0f;
         vc[3 * k] = bk * g0;
         vc[3 * k + 1] = bk * g1;
         vc[3 * k + 2] = bk * g2;
@@ -148,7 +150,7 @@ extern "C" int gstex_sh_fwd(int32_t n, int32_t degree, int32_t n_coeffs, const f
                   n_coeffs, (degree + 1) * (degree + 1));
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(viewdirs && coeffs && colors, "gstex_sh_fwd: null pointer");
-    sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, n_coeffs, viewdirs, coeffs, colors);
+    sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, coeffs, colors);
     return launch_status("gstex_sh_fwd");
 }
 
@@ -158,8 +160,30 @@ extern "C" int gstex_sh_bwd(int32_t n, int32_t degree, int32_t n_coeffs, const f
     GSTEX_REQUIRE(n_coeffs >= (degree + 1) * (degree + 1), "gstex_sh_bwd: too few coefficients");
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(viewdirs && v_colors && v_coeffs, "gstex_sh_bwd: null pointer");
-    sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, n_coeffs, viewdirs, v_colors, v_coeffs);
+    sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, v_colors, v_coeffs);
     return launch_status("gstex_sh_bwd");
+}
+
+extern "C" int gstex_sh_rest_fwd(int32_t n, int32_t degree, int32_t n_rest, const float* viewdirs,
+                                 const float* coeffs_rest, float* colors, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && degree >= 0 && degree <= 4, "gstex_sh_rest_fwd: degree must be in [0, 4] (got %d)", degree);
+    GSTEX_REQUIRE(n_rest >= (degree + 1) * (degree + 1) - 1, "gstex_sh_rest_fwd: %d coefficients < (degree+1)^2 - 1",
+                  n_rest);
+    if (n == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(viewdirs && colors && (coeffs_rest || n_rest == 0), "gstex_sh_rest_fwd: null pointer");
+    sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, coeffs_rest, colors);
+    return launch_status("gstex_sh_rest_fwd");
+}
+
+extern "C" int gstex_sh_rest_bwd(int32_t n, int32_t degree, int32_t n_rest, const float* viewdirs,
+                                 const float* v_colors, float* v_coeffs_rest, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && degree >= 0 && degree <= 4, "gstex_sh_rest_bwd: degree must be in [0, 4]");
+    GSTEX_REQUIRE(n_rest >= 0, "gstex_sh_rest_bwd: n_rest < 0");
+    if (n == 0 || n_rest == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(viewdirs && v_colors && v_coeffs_rest, "gstex_sh_rest_bwd: null pointer");
+    sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, v_colors,
+                                                                  v_coeffs_rest);
+    return launch_status("gstex_sh_rest_bwd");
 }
 
 extern "C" int gstex_texture_sample(int64_t n_query, int32_t channels, const int32_t* query_dims,

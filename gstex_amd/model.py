@@ -24,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
+from .activations import activate, sh_rest
 from .loss import gaussian_window, photometric_loss
 from .optim import FusedAdam
 from .charts import SH2RGB, build_charts, get_uv_mapping, texture_dims_to_query
@@ -102,7 +103,7 @@ class GStexTrainer:
 
     def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
-                 fused_loss: bool = True):
+                 fused_loss: bool = True, fused_activations: bool = True):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -124,6 +125,7 @@ class GStexTrainer:
         self.step = 0
         self.fused_adam = fused_adam
         self.fused_loss = fused_loss
+        self.fused_activations = fused_activations
         self._build_optimizer()
 
     # ------------------------------------------------------------------ parameters
@@ -152,22 +154,29 @@ class GStexTrainer:
     def render(self, view: View, sh_degree_now: int | None = None, composite: bool = True):
         """get_outputs (gstex.py:992-1236), training branch."""
         means = self.means
-        quats = self.quats / self.quats.norm(dim=-1, keepdim=True)
-        s = torch.exp(self.scales[:, :-1]).clamp(min=1e-9)
-        scales = torch.cat([s, 1e-5 * s.mean(dim=-1, keepdim=True).detach()], dim=-1)
-        opacities = torch.sigmoid(self.opacities)
-        uv0, umap, vmap = get_uv_mapping(quats, self.mappings)
+        deg = self.sh_degree if sh_degree_now is None else sh_degree_now
+        if self.fused_activations:  # one HIP launch each way (gstex_amd.activations)
+            quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
+                means, self.quats, self.scales, self.opacities, self.mappings, view.c2w[:3, 3])
+        else:
+            quats = self.quats / self.quats.norm(dim=-1, keepdim=True)
+            s = torch.exp(self.scales[:, :-1]).clamp(min=1e-9)
+            scales = torch.cat([s, 1e-5 * s.mean(dim=-1, keepdim=True).detach()], dim=-1)
+            opacities = torch.sigmoid(self.opacities)
+            uv0, umap, vmap = get_uv_mapping(quats, self.mappings)
+            viewdirs = means.detach() - view.c2w[:3, 3]
+            viewdirs = viewdirs / viewdirs.norm(dim=-1, keepdim=True)
         intr = (view.fx, view.fy, view.cx, view.cy)
         _, depths = ops.project_points(means, view.viewmat, intr)
         centers, extents = ops.get_aabb_2d(means, scales, 1, quats, view.viewmat, intr)
         nth = ops.get_num_tiles_hit_2d(centers, extents, view.H, view.W, ops.BLOCK_WIDTH)
         n = self.means.shape[0]
         if self.sh_degree > 0:
-            colors = torch.cat([torch.zeros_like(self.features_dc[:, None, :]), self.features_rest], dim=1)
-            viewdirs = means.detach() - view.c2w[:3, 3]
-            viewdirs = viewdirs / viewdirs.norm(dim=-1, keepdim=True)
-            deg = self.sh_degree if sh_degree_now is None else sh_degree_now
-            rgbs = ops.spherical_harmonics(deg, viewdirs, colors)
+            if self.fused_activations:  # the zeroed DC term (gstex.py:1100) without the cat
+                rgbs = sh_rest(deg, viewdirs, self.features_rest)
+            else:
+                colors = torch.cat([torch.zeros_like(self.features_dc[:, None, :]), self.features_rest], dim=1)
+                rgbs = ops.spherical_harmonics(deg, viewdirs, colors)
         else:
             rgbs = torch.sigmoid(self.features_dc)
         # SH2RGB(texture_dc) (gstex.py:1119) applied by the raster on read instead of materialised

@@ -176,6 +176,27 @@ int gstex_texture_edit(const gstex_camera* cam, int32_t settings, const float* r
                        const float* edit_rgb, const float* edit_alpha, const float* depth_lo,
                        const float* depth_hi, int64_t n_texels, float* out, void* stream);
 
+/* ---- splat activations (train-step support) ---------------------------- */
+/* Per splat: quats_n = q/|q|; scales = (clamp(exp(s0),1e-9), clamp(exp(s1),1e-9), 1e-5*mean of those);
+ * opacities = sigmoid(o); uv0 = 0.5, umap/vmap = mappings[:,0/1] * R(normalize(quats_n))[:, 0/1];
+ * viewdirs = normalize(means - campos).  mappings is [n][mappings_stride] (>= 2); campos a device float[3];
+ * quats / quats_n / v_quats 16-byte aligned.  The backward writes v_quats (raw quaternions), v_log_scales
+ * (third axis 0: detached) and v_opac_logits; a NULL upstream gradient counts as zero and a NULL output
+ * is skipped. */
+int gstex_activate_fwd(int32_t n, const float* means, const float* quats, const float* log_scales,
+                       const float* opac_logits, const float* mappings, int32_t mappings_stride,
+                       const float* campos, float* quats_n, float* scales, float* opacities, float* uv0,
+                       float* umap, float* vmap, float* viewdirs, void* stream);
+int gstex_activate_bwd(int32_t n, const float* quats, const float* log_scales, const float* opacities,
+                       const float* v_quats_n, const float* v_scales, const float* v_opacities,
+                       float* v_quats, float* v_log_scales, float* v_opac_logits, void* stream);
+/* SH colour from the non-DC coefficients only (the caller zeroes the DC term, gstex.py:1100):
+ * coeffs_rest[n][n_rest][3] holds bases 1..n_rest; same result as gstex_sh_fwd on [0, coeffs_rest]. */
+int gstex_sh_rest_fwd(int32_t n, int32_t degree, int32_t n_rest, const float* viewdirs,
+                      const float* coeffs_rest, float* colors, void* stream);
+int gstex_sh_rest_bwd(int32_t n, int32_t degree, int32_t n_rest, const float* viewdirs,
+                      const float* v_colors, float* v_coeffs_rest, void* stream);
+
 /* ---- photometric loss (train-step support) --------------------------------- */
 /* rgb = clamp(img + tex[..., 0:3] + (1 - alpha) * background, 0, 1)      (gstex.py:1204-1205)
  * loss = (1 - ssim_lambda) * mean|gt - rgb| + ssim_lambda * (1 - SSIM(gt, rgb))  (gstex.py:1301-1322)

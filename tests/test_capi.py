@@ -29,7 +29,7 @@ def lib():
 
 def test_every_header_symbol_is_exported_and_bound(lib):
     syms = declared_symbols()
-    assert len(syms) >= 25
+    assert len(syms) >= 29
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in gstex_hip.h but not exported"
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature in gstex_amd/_lib.py"
@@ -132,3 +132,18 @@ def test_loss_rejects_small_images_and_channels(lib):
     rc, msg = _status(lib, "gstex_loss_bwd", 64, 64, 2, None, None, None, None, None, win, 0.2, None, None, None,
                       None, None, 0, None)
     assert rc == 1 and "channels" in msg
+
+
+def test_activate_and_sh_rest_reject_bad_args(lib):
+    rc, msg = _status(lib, "gstex_activate_fwd", 10, None, None, None, None, None, 1, None, None, None, None, None,
+                      None, None, None, None)
+    assert rc == 1 and "mappings_stride" in msg
+    rc, msg = _status(lib, "gstex_activate_fwd", 10, None, None, None, None, None, 2, None, None, None, None, None,
+                      None, None, None, None)
+    assert rc == 1 and "null pointer" in msg
+    rc, msg = _status(lib, "gstex_sh_rest_fwd", 4, 5, 35, None, None, None, None)
+    assert rc == 1 and "degree" in msg
+    rc, msg = _status(lib, "gstex_sh_rest_fwd", 4, 3, 14, None, None, None, None)
+    assert rc == 1 and "coefficients" in msg
+    assert lib.gstex_activate_fwd(0, None, None, None, None, None, 2, None, None, None, None, None, None, None, None,
+                                  None) == 0

@@ -426,3 +426,45 @@ def test_texel_fixed_point_scale_invariance(gscale):
     a, b = gs["texture"].double() / gscale, gu["texture"].double()
     assert float(b.abs().max()) > 0
     assert float((a - b).norm() / b.norm()) < 1e-6
+
+
+# ---------------------------------------------------------------- fused activations / SH without the DC cat
+def test_sh_rest_equals_sh_on_concatenated_coeffs():
+    import gstex_cuda
+    from gstex_amd.activations import sh_rest
+
+    g = torch.Generator().manual_seed(4)
+    n = 3000
+    dirs = torch.randn(n, 3, generator=g).to(DEV)
+    rest = torch.randn(n, 15, 3, generator=g).to(DEV)
+    a = rest.clone().requires_grad_(True)
+    b = rest.clone().requires_grad_(True)
+    for deg in (1, 3):
+        out_a = sh_rest(deg, dirs, a)
+        out_b = gstex_cuda.spherical_harmonics(deg, dirs, torch.cat([torch.zeros_like(b[:, :1]), b], 1))
+        assert torch.equal(out_a, out_b)
+        vo = torch.randn(n, 3, generator=g).to(DEV)
+        ga, = torch.autograd.grad(out_a, a, vo)
+        gb, = torch.autograd.grad(out_b, b, vo)
+        assert torch.equal(ga, gb)
+
+
+def test_fused_activations_match_eager_trainer():
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    sc = make_scene(3000, 60000, seed=2)
+    v = sphere_view(1, 96, 128).to(DEV)
+    gt = torch.rand(96, 128, 3, generator=torch.Generator().manual_seed(0)).to(DEV)
+    tf = GStexTrainer(sc, DEV, fused_activations=True)
+    te = GStexTrainer(sc, DEV, fused_activations=False)
+    of, oe = tf.forward_backward(v, gt), te.forward_backward(v, gt)
+    assert abs(float(of.loss) - float(oe.loss)) <= 1e-5 * abs(float(oe.loss))
+    assert float((of.rgb - oe.rgb).abs().max()) < 1e-4
+    for pf, pe, name in zip(tf.parameters(), te.parameters(), ["means", "features_dc", "features_rest", "opacities",
+                                                                "scales", "quats", "texture_dc"]):
+        if pe.grad is None:
+            assert pf.grad is None or float(pf.grad.abs().max()) == 0.0, name
+            continue
+        err = float((pf.grad - pe.grad).norm() / pe.grad.norm().clamp(min=1e-30))
+        assert err < 1e-4, f"{name}: rel err {err:.2e}"
