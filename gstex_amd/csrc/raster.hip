@@ -620,14 +620,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         const size_t pix = (size_t)pyi * cam.W + pxi;
         const float4 st = state[pix];
         T = st.x; M1f = st.y; M2f = st.z; last = __float_as_int(st.w);
-        Gimg[0] = v_img[3 * pix]; Gimg[1] = v_img[3 * pix + 1]; Gimg[2] = v_img[3 * pix + 2];
+        // a NULL upstream gradient (an output the loss does not use) counts as zero
+        if (v_img) { Gimg[0] = v_img[3 * pix]; Gimg[1] = v_img[3 * pix + 1]; Gimg[2] = v_img[3 * pix + 2]; }
 #pragma unroll
         for (int c = 0; c < CM; ++c)
-            if (c < Cn) Gtex[c] = v_tex[(size_t)Cn * pix + c];
-        Gd = v_depth[pix];
-        Greg = dreg ? v_reg[pix] : 0.f;
-        Ga = v_alpha[pix];
-        Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2];
+            if (c < Cn && v_tex) Gtex[c] = v_tex[(size_t)Cn * pix + c];
+        Gd = v_depth ? v_depth[pix] : 0.f;
+        Greg = (dreg && v_reg) ? v_reg[pix] : 0.f;
+        Ga = v_alpha ? v_alpha[pix] : 0.f;
+        if (v_normal) { Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2]; }
     }
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
@@ -1201,7 +1202,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
     int rc = check_settings(settings);
     if (rc) return rc;
-    GSTEX_REQUIRE(tile_ranges && state && v_img && v_depth && v_reg && v_alpha && v_tex && v_normal,
+    GSTEX_REQUIRE(tile_ranges && state,
                   "gstex_raster_bwd: null pointer");
     GSTEX_REQUIRE(n_texels == 0 || (texture && v_texture), "gstex_raster_bwd: null texture");
     const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;

@@ -116,6 +116,7 @@ class _ProjectPoints(torch.autograd.Function):
         call("gstex_project_points", n, ptr(means), cam, ptr(xys), ptr(depths), _stream(means))
         ctx.save_for_backward(means, vm)
         ctx.intr = (fx, fy, cx, cy)
+        ctx.set_materialize_grads(False)  # the kernel reads a NULL v_xys / v_depths as zero
         return xys, depths
 
     @staticmethod
@@ -289,6 +290,7 @@ class _TextureGaussians(torch.autograd.Function):
         ctx.has_bg = bg is not None
         ctx.args = (float(glob_scale), float(fx), float(fy), float(cx), float(cy), H, W, C, int(settings))
         ctx.tex_affine = (ctx_scale, ctx_bias)
+        ctx.set_materialize_grads(False)  # unused outputs' gradients stay None (no zero tensors)
         return img, depth, reg, alpha, tex, normal
 
     @staticmethod
@@ -303,8 +305,8 @@ class _TextureGaussians(torch.autograd.Function):
         st = _stream(means)
         cam = _lib.make_camera(vm, cw, fx, fy, cx, cy, H, W, BLOCK_WIDTH)
 
-        def g(t, shape):
-            return torch.zeros(shape, device=dev, dtype=torch.float32) if t is None else t.contiguous()
+        def g(t, shape):  # unused outputs arrive as None (no zero fill): the kernel reads NULL as zero
+            return None if t is None else t.contiguous()
 
         v_img = g(v_img, (H, W, 3))
         v_depth = g(v_depth, (H, W))
@@ -331,7 +333,7 @@ class _TextureGaussians(torch.autograd.Function):
              ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
         v_bg = None
         if ctx.needs_input_grad[26]:
-            v_bg = (v_img * state[..., 0:1]).sum((0, 1))
+            v_bg = (v_img * state[..., 0:1]).sum((0, 1)) if v_img is not None else torch.zeros_like(bg)
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None)
 

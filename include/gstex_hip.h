@@ -132,7 +132,8 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      int64_t n_texels, float tex_scale, float tex_bias,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                      float* out_tex, float* out_normal, float* state, void* stream);
-/* Backward composite. Needs the forward state and the same tile_order. Writes
+/* Backward composite. Needs the forward state and the same tile_order. Any of v_img ... v_normal may be
+ * NULL (that output's gradient is zero). Writes
  * partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of every (tile, splat) pair and
  * accumulates (+=) texel gradients into v_texture[n_texels][C]. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
