@@ -294,12 +294,14 @@ struct Hit {
 
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
 __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool aa, Hit& h) {
+    // branch-free: a skipped pair's values are computed anyway (possibly inf/NaN) and never used, so
+    // the callers see one predicate instead of three divergent exits (fewer exec-mask joins)
     h.dx = px - r.xa;
     h.dy = py - r.ya;
     h.k = f3{h.dx * r.Tw.x - r.Tu.x, h.dx * r.Tw.y - r.Tu.y, h.dx * r.Tw.z};
     h.l = f3{h.dy * r.Tw.x - r.Tv.x, h.dy * r.Tw.y - r.Tv.y, h.dy * r.Tw.z};
     h.p = cross3(h.k, h.l);
-    if (h.p.z == 0.0f) return false;
+    const bool ok = h.p.z != 0.0f;
 #if GSTEX_FAST_EVAL
     h.ipz = __builtin_amdgcn_rcpf(h.p.z);
 #else
@@ -313,7 +315,6 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     h.use3 = !aa || (h.rho3 <= h.rho2);
     float rho = h.use3 ? h.rho3 : h.rho2;
     h.z = h.use3 ? (h.u * r.Tw.x + h.v * r.Tw.y) + r.Tw.z : r.Tw.z;
-    if (h.z < kNear) return false;
 #if GSTEX_FAST_EVAL
     h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);  // exp(-rho/2) = 2^(-rho/(2 ln 2))
 #else
@@ -321,7 +322,7 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
 #endif
     h.a_raw = r.opac * h.G;
     h.alpha = fminf(kAlphaMax, h.a_raw);
-    return h.alpha >= kAlphaMin;
+    return ok && h.z >= kNear && h.alpha >= kAlphaMin;  // oracle/raster.py: nz & (zz >= near) & (alpha >= amin)
 }
 
 // One texel's channels: with C == 3 a single 12-B global_load_dwordx3 (the three channels share a cache
@@ -718,19 +719,20 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             const int j = 31 - __builtin_clz(todo);
             todo &= ~(1u << j);
             const int rel = bb * kBwdBatch + j;
+            const Rec r = read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
+            // one predicate for the whole heavy path (a single exec-mask region: the zero rows below are
+            // materialised once, not at every divergent exit)
+            Hit h;
+            const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
             float P[kNP];
 #pragma unroll
             for (int i = 0; i < kNP; ++i) P[i] = 0.f;
-            bool contrib = false;
-            const Rec r = read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
             // texel-gradient inputs, expanded into the 4*C bilinear contributions after P is reduced:
             // tkey = top-left texel of the block | (i1 - i0) << 29 | (j1 - j0) << 30, -1 if none
             int tkey = -1;
             float tw = 0.f, tax = 0.f, tay = 0.f;
-            if (rel <= last) {
-                Hit h;
-                if (eval_hit(r, px, py, aa, h)) {
-                    contrib = true;
+            {
+                if (contrib) {
                     const float one_m = 1.0f - h.alpha;
                     T = T * grad_rcp(one_m);
                     const float w = h.alpha * T;
@@ -811,25 +813,26 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     P[P_TV0] = dtv; P[P_AVU] = dtv * h.u; P[P_AVV] = dtv * h.v;
                     float du = dtu * r.auu + dtv * r.avu;
                     float dv = dtu * r.auv + dtv * r.avv;
-                    f3 dTw = f3{0.f, 0.f, 0.f};
-                    if (h.use3) {
-                        du += drho * 2.0f * h.u + dz * r.Tw.x;
-                        dv += drho * 2.0f * h.v + dz * r.Tw.y;
-                        dTw = f3{dz * h.u, dz * h.v, dz};
-                    } else {
-                        P[P_XY + 0] = drho * (2.0f * kFilterInvSq) * (r.x - px);
-                        P[P_XY + 1] = drho * (2.0f * kFilterInvSq) * (r.y - py);
-                        dTw.z = dz;
-                    }
+                    // ray-splat (use3) vs screen-space low-pass branch, per lane, as selects (a divergent
+                    // if/else here cost ~30 register moves at the join)
+                    const float du3 = drho * 2.0f * h.u + dz * r.Tw.x;
+                    const float dv3 = drho * 2.0f * h.v + dz * r.Tw.y;
+                    du = h.use3 ? du + du3 : du;
+                    dv = h.use3 ? dv + dv3 : dv;
+                    const f3 dTw = f3{h.use3 ? dz * h.u : 0.f, h.use3 ? dz * h.v : 0.f, dz};
+                    P[P_XY + 0] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.x - px);
+                    P[P_XY + 1] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.y - py);
                     const float ipz = h.ipz;
                     const f3 dp = f3{du * ipz, dv * ipz, -(du * h.u + dv * h.v) * ipz};
-                    const f3 dk = cross3(h.l, dp);
-                    const f3 dl = cross3(dp, h.k);
-                    P[P_TU + 0] = -dk.x; P[P_TU + 1] = -dk.y; P[P_TU + 2] = -dk.z;
-                    P[P_TV + 0] = -dl.x; P[P_TV + 1] = -dl.y; P[P_TV + 2] = -dl.z;
-                    P[P_TW + 0] = dTw.x + h.dx * dk.x + h.dy * dl.x;
-                    P[P_TW + 1] = dTw.y + h.dx * dk.y + h.dy * dl.y;
-                    P[P_TW + 2] = dTw.z + h.dx * dk.z + h.dy * dl.z;
+                    // nk = -dL/dk and nl = -dL/dl exactly (operands of the cross products swapped), so
+                    // the Tu/Tv rows need no negation and Tw subtracts
+                    const f3 nk = cross3(dp, h.l);
+                    const f3 nl = cross3(h.k, dp);
+                    P[P_TU + 0] = nk.x; P[P_TU + 1] = nk.y; P[P_TU + 2] = nk.z;
+                    P[P_TV + 0] = nl.x; P[P_TV + 1] = nl.y; P[P_TV + 2] = nl.z;
+                    P[P_TW + 0] = (dTw.x - h.dx * nk.x) - h.dy * nl.x;
+                    P[P_TW + 1] = (dTw.y - h.dx * nk.y) - h.dy * nl.y;
+                    P[P_TW + 2] = (dTw.z - h.dx * nk.z) - h.dy * nl.z;
                 }
             }
             const bool any = __any(contrib);
