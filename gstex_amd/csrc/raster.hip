@@ -292,6 +292,29 @@ struct Hit {
     bool use3;
 };
 
+// reciprocal for values that feed no threshold decision (gradients and the distortion term only)
+__device__ __forceinline__ float grad_rcp(float x) {
+#if GSTEX_FAST_RCP
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
+// expf for x <= 0: the device library's expf sequence (two-part x*log2(e), rint, v_exp_f32, ldexp) without its
+// overflow/underflow selects, so the same bits wherever expf is finite and non-zero.  The argument is
+// clamped at -104 (expf's own flush-to-zero point; a NaN argument also lands there), so a degenerate
+// pair gets G ~ 0 and fails the alpha test instead of propagating NaN.
+__device__ __forceinline__ float exp_nonpos(float x) {
+    x = fmaxf(x, -104.0f);
+    const float ph = x * 1.44269502e+00f;                        // 0x3fb8aa3b
+    float pl = __builtin_fmaf(x, 1.44269502e+00f, -ph);
+    pl = __builtin_fmaf(x, 1.92596286e-08f, pl);                  // 0x32a5705f
+    const float e = __builtin_rintf(ph);
+    const float a = (ph - e) + pl;
+    return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
+}
+
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
 __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool aa, Hit& h) {
     // branch-free: a skipped pair's values are computed anyway (possibly inf/NaN) and never used, so
@@ -318,7 +341,7 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
 #if GSTEX_FAST_EVAL
     h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);  // exp(-rho/2) = 2^(-rho/(2 ln 2))
 #else
-    h.G = expf(-0.5f * rho);
+    h.G = exp_nonpos(-0.5f * rho);
 #endif
     h.a_raw = r.opac * h.G;
     h.alpha = fminf(kAlphaMax, h.a_raw);
@@ -338,6 +361,29 @@ __device__ __forceinline__ void load_texel(const float* __restrict__ p, int Cn, 
     } else {
 #pragma unroll
         for (int c = 0; c < CM; ++c) out[c] = (c < Cn) ? p[c] : 0.0f;
+    }
+}
+
+// A splat's texel block as a buffer resource: the wave-uniform block base and size live in SGPRs and
+// each lane supplies a 32-bit byte offset, so a gather costs one buffer_load and no 64-bit address
+// arithmetic; the hardware range check (size = the block's h*w*C floats) returns 0 outside the block.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t texel_rsrc(const float* texture, int off, int n_texels, int Cn) {
+    off = __builtin_amdgcn_readfirstlane(off);
+    n_texels = __builtin_amdgcn_readfirstlane(n_texels);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(texture) + (size_t)off * Cn, 0, n_texels * Cn * 4,
+                                             0x00020000);
+}
+template <int CM>
+__device__ __forceinline__ void load_texel_rs(__amdgpu_buffer_rsrc_t rs, int idx, int Cn, float (&out)[CM]) {
+    if constexpr (CM == 3) {
+        const auto t = __builtin_amdgcn_raw_buffer_load_b96(rs, idx * 12, 0, 0);
+        out[0] = __int_as_float(t[0]);
+        out[1] = __int_as_float(t[1]);
+        out[2] = __int_as_float(t[2]);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            out[c] = (c < Cn) ? __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (idx * Cn + c) * 4, 0, 0)) : 0.0f;
     }
 }
 
@@ -418,14 +464,12 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
                 const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
-                const float* tblk = texture + (size_t)r.off * Cn;  // wave-uniform block base
-                const int o00 = (b.i0 * r.w + b.j0) * Cn, o01 = (b.i0 * r.w + b.j1) * Cn;
-                const int o10 = (b.i1 * r.w + b.j0) * Cn, o11 = (b.i1 * r.w + b.j1) * Cn;
+                const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
                 float t00[CM], t01[CM], t10[CM], t11[CM];
-                load_texel<CM>(tblk + o00, Cn, t00);
-                load_texel<CM>(tblk + o01, Cn, t01);
-                load_texel<CM>(tblk + o10, Cn, t10);
-                load_texel<CM>(tblk + o11, Cn, t11);
+                load_texel_rs<CM>(rs, b.i0 * r.w + b.j0, Cn, t00);
+                load_texel_rs<CM>(rs, b.i0 * r.w + b.j1, Cn, t01);
+                load_texel_rs<CM>(rs, b.i1 * r.w + b.j0, Cn, t10);
+                load_texel_rs<CM>(rs, b.i1 * r.w + b.j1, Cn, t11);
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < Cn) {
@@ -444,7 +488,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             nrm[2] = nrm[2] + r.nrm[2] * w;
             if (dreg) {
                 const float A = 1.0f - T;
-                const float m = kFarRatio * (1.0f - kNear / h.z);
+                const float m = kFarRatio * (1.0f - kNear * grad_rcp(h.z));
                 reg = reg + ((m * m * A + M2) - 2.0f * m * M1) * w;
                 M1 = M1 + m * w;
                 M2 = M2 + m * m * w;
@@ -561,15 +605,6 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     if (SW > 8) seg_step<NV, 8>(seg, v);
     const int ns = __builtin_amdgcn_update_dpp(-1, seg, 0x101, 0xF, 0xF, false);  // row_shl:1
     return key >= 0 && (ns != seg || pos == SW - 1);
-}
-
-// reciprocal for values that feed no threshold decision (gradients only)
-__device__ __forceinline__ float grad_rcp(float x) {
-#if GSTEX_FAST_RCP
-    return __builtin_amdgcn_rcpf(x);
-#else
-    return 1.0f / x;
-#endif
 }
 
 template <int C>
@@ -740,8 +775,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     // latency overlaps that work
                     const bool has_tex = r.h * r.w > 0;
                     Bilerp b;
-                    // wave-uniform block base (scalar) + 32-bit per-lane offsets
-                    const float* tblk = texture + (size_t)r.off * Cn;
+                    // wave-uniform block base and size (scalar) + 32-bit per-lane offsets
+                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
                     float t00[CM], t01[CM], t10[CM], t11[CM];
 #pragma unroll
                     for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
@@ -750,10 +785,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                         tex_coords(r, h.u, h.v, tu, tv);
                         b = bilerp_coords(tu, tv, r.h, r.w);
                         if (!(GSTEX_ABLATE & 8)) {
-                            load_texel<CM>(tblk + (b.i0 * r.w + b.j0) * Cn, Cn, t00);
-                            load_texel<CM>(tblk + (b.i0 * r.w + b.j1) * Cn, Cn, t01);
-                            load_texel<CM>(tblk + (b.i1 * r.w + b.j0) * Cn, Cn, t10);
-                            load_texel<CM>(tblk + (b.i1 * r.w + b.j1) * Cn, Cn, t11);
+                            load_texel_rs<CM>(rs, b.i0 * r.w + b.j0, Cn, t00);
+                            load_texel_rs<CM>(rs, b.i0 * r.w + b.j1, Cn, t01);
+                            load_texel_rs<CM>(rs, b.i1 * r.w + b.j0, Cn, t10);
+                            load_texel_rs<CM>(rs, b.i1 * r.w + b.j1, Cn, t11);
                         }
                     }
                     const float iz = grad_rcp(h.z);
