@@ -47,6 +47,7 @@ class _Activate(torch.autograd.Function):
              _lib.stream_of(means.device))
         ctx.save_for_backward(quats, log_scales, op)
         ctx.mark_non_differentiable(uv0, umap, vmap, vd)
+        ctx.set_materialize_grads(False)  # no zero tensors for the detached outputs; the kernel reads NULL as 0
         return qn, sc, op, uv0, umap, vmap, vd
 
     @staticmethod

@@ -96,12 +96,22 @@ __global__ __launch_bounds__(kBlock) void aabb_bwd_kernel(int n, const float* __
     int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     float gcx = v_centers[2 * i], gcy = v_centers[2 * i + 1];
-    if (gcx == 0.0f && gcy == 0.0f) return;
     Frame fr;
     float su, sv;
-    Homog h = load_homog(i, means, scales, glob, quats, cam, fr, su, sv);
     float cx, cy, ex, ey;
-    if (!aabb_from_homog(h, cx, cy, ex, ey)) return;
+    Homog h;
+    bool live = !(gcx == 0.0f && gcy == 0.0f);
+    if (live) {
+        h = load_homog(i, means, scales, glob, quats, cam, fr, su, sv);
+        live = aabb_from_homog(h, cx, cy, ex, ey);
+    }
+    if (!live) {
+        // no centre gradient (or a culled splat): the outputs are written, not accumulated
+        v_means[3 * i + 0] = v_means[3 * i + 1] = v_means[3 * i + 2] = 0.0f;
+        v_scales[3 * i + 0] = v_scales[3 * i + 1] = v_scales[3 * i + 2] = 0.0f;
+        v_quats[4 * i + 0] = v_quats[4 * i + 1] = v_quats[4 * i + 2] = v_quats[4 * i + 3] = 0.0f;
+        return;
+    }
     const f3 Tu = h.Tu, Tv = h.Tv, Tw = h.Tw;
     float d = (kCutoff2 * (Tw.x * Tw.x) + kCutoff2 * (Tw.y * Tw.y)) - Tw.z * Tw.z;
     float invd = 1.0f / d;
@@ -114,15 +124,16 @@ __global__ __launch_bounds__(kBlock) void aabb_bwd_kernel(int n, const float* __
     HomogGrad g = splat_homography_vjp(cam, su, sv, fr, dTu, dTv, dTw);
     float dq[4];
     frame_vjp(fr, g.dtu, g.dtv, f3{0.0f, 0.0f, 0.0f}, dq);
-    v_means[3 * i + 0] += g.dmu.x;
-    v_means[3 * i + 1] += g.dmu.y;
-    v_means[3 * i + 2] += g.dmu.z;
-    v_scales[3 * i + 0] += g.dsu * glob;
-    v_scales[3 * i + 1] += g.dsv * glob;
-    v_quats[4 * i + 0] += dq[0];
-    v_quats[4 * i + 1] += dq[1];
-    v_quats[4 * i + 2] += dq[2];
-    v_quats[4 * i + 3] += dq[3];
+    v_means[3 * i + 0] = g.dmu.x;
+    v_means[3 * i + 1] = g.dmu.y;
+    v_means[3 * i + 2] = g.dmu.z;
+    v_scales[3 * i + 0] = g.dsu * glob;
+    v_scales[3 * i + 1] = g.dsv * glob;
+    v_scales[3 * i + 2] = 0.0f;
+    v_quats[4 * i + 0] = dq[0];
+    v_quats[4 * i + 1] = dq[1];
+    v_quats[4 * i + 2] = dq[2];
+    v_quats[4 * i + 3] = dq[3];
 }
 
 __global__ __launch_bounds__(kBlock) void num_tiles_kernel(int n, const float* __restrict__ centers,

@@ -607,7 +607,10 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     return key >= 0 && (ns != seg || pos == SW - 1);
 }
 
-template <int C>
+// GEO = false: no depth / distortion / normal upstream gradient (all NULL, the training default:
+// gstex.py:198-201 sets both weights to 0), so every term they scale is dropped at compile time.  The
+// remaining arithmetic is unchanged (x + 0 * y = x), so both variants give the same values.
+template <int C, bool GEO>
 __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
@@ -661,10 +664,12 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 #pragma unroll
         for (int c = 0; c < CM; ++c)
             if (c < Cn && v_tex) Gtex[c] = v_tex[(size_t)Cn * pix + c];
-        Gd = v_depth ? v_depth[pix] : 0.f;
-        Greg = (dreg && v_reg) ? v_reg[pix] : 0.f;
         Ga = v_alpha ? v_alpha[pix] : 0.f;
-        if (v_normal) { Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2]; }
+        if (GEO) {
+            Gd = v_depth ? v_depth[pix] : 0.f;
+            Greg = (dreg && v_reg) ? v_reg[pix] : 0.f;
+            if (v_normal) { Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2]; }
+        }
     }
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
@@ -791,19 +796,22 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                             load_texel_rs<CM>(rs, b.i1 * r.w + b.j1, Cn, t11);
                         }
                     }
-                    const float iz = grad_rcp(h.z);
-                    const float m = kFarRatio * (1.0f - kNear * iz);
-                    const float E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
                     float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
                     P[P_RGB + 0] = w * Gimg[0];
                     P[P_RGB + 1] = w * Gimg[1];
                     P[P_RGB + 2] = w * Gimg[2];
-                    P[P_NRM + 0] = w * Gn[0];
-                    P[P_NRM + 1] = w * Gn[1];
-                    P[P_NRM + 2] = w * Gn[2];
                     // depth: direct + distortion (m depends on z)
-                    float dz = w * Gd;
-                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
+                    float dz = 0.f, E = 0.f;
+                    if (GEO) {
+                        P[P_NRM + 0] = w * Gn[0];
+                        P[P_NRM + 1] = w * Gn[1];
+                        P[P_NRM + 2] = w * Gn[2];
+                        const float iz = grad_rcp(h.z);
+                        const float m = kFarRatio * (1.0f - kNear * iz);
+                        E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
+                        dz = w * Gd;
+                        if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
+                    }
                     // texel gradients: per-lane bilinear contributions, scattered after the P reduction
                     if (has_tex && !(GSTEX_ABLATE & 1)) {
                         tkey = (b.i0 * r.w + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
@@ -829,10 +837,12 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                             }
                         }
                     }
-                    g += Gd * h.z;
-                    g += (Gn[0] * r.nrm[0] + Gn[1] * r.nrm[1]) + Gn[2] * r.nrm[2];
+                    if (GEO) {
+                        g += Gd * h.z;
+                        g += (Gn[0] * r.nrm[0] + Gn[1] * r.nrm[1]) + Gn[2] * r.nrm[2];
+                    }
                     g += Ga;
-                    g += Greg * E;
+                    if (GEO) g += Greg * E;
                     const float dL_dalpha = T * (g - R);
                     R = h.alpha * g + one_m * R;
 
@@ -850,11 +860,11 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     float dv = dtu * r.auv + dtv * r.avv;
                     // ray-splat (use3) vs screen-space low-pass branch, per lane, as selects (a divergent
                     // if/else here cost ~30 register moves at the join)
-                    const float du3 = drho * 2.0f * h.u + dz * r.Tw.x;
-                    const float dv3 = drho * 2.0f * h.v + dz * r.Tw.y;
+                    const float du3 = GEO ? drho * 2.0f * h.u + dz * r.Tw.x : drho * 2.0f * h.u;
+                    const float dv3 = GEO ? drho * 2.0f * h.v + dz * r.Tw.y : drho * 2.0f * h.v;
                     du = h.use3 ? du + du3 : du;
                     dv = h.use3 ? dv + dv3 : dv;
-                    const f3 dTw = f3{h.use3 ? dz * h.u : 0.f, h.use3 ? dz * h.v : 0.f, dz};
+                    const f3 dTw = GEO ? f3{h.use3 ? dz * h.u : 0.f, h.use3 ? dz * h.v : 0.f, dz} : f3{0.f, 0.f, 0.f};
                     P[P_XY + 0] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.x - px);
                     P[P_XY + 1] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.y - py);
                     const float ipz = h.ipz;
@@ -1024,6 +1034,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 // setup backward: sum partials per splat, chain to parameters
 // ------------------------------------------------------------------------------------------
+constexpr int kSetupBwdSplats = 256 / kNP;  // 10 splats x 24 partial columns per 256-thread workgroup
 __global__ __launch_bounds__(256) void setup_bwd_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
@@ -1031,21 +1042,30 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
     float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers,
     float* __restrict__ v_uv0) {
+    // phase 1: kNP lanes per splat, lane c sums column c of the splat's partial rows in slot order (the
+    // rows of one splat are contiguous, so each step reads one 96-B row per splat instead of one
+    // 96-B row per thread); phase 2: one thread per splat chains the sums to the parameters
+    __shared__ float s_sum[kSetupBwdSplats][kNP];
+    const int t = threadIdx.x;
+    const int g0 = blockIdx.x * kSetupBwdSplats;
+    if (t < kSetupBwdSplats * kNP) {
+        const int j = t / kNP, c = t - j * kNP;
+        float acc = 0.f;
+        if (g0 + j < n) {
+            const int cnt = nth[g0 + j];
+            const float* src = partials + (size_t)offsets[g0 + j] * kNP + c;
+            for (int e = 0; e < cnt; ++e) acc += src[(size_t)e * kNP];
+        }
+        s_sum[j][c] = acc;
+    }
+    __syncthreads();
+    const int g = g0 + t;
+    if (t >= kSetupBwdSplats || g >= n) return;
     const Camera cam = load_camera(cam_args);
-    int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
     float S[kNP];
 #pragma unroll
-    for (int i = 0; i < kNP; ++i) S[i] = 0.f;
+    for (int i = 0; i < kNP; ++i) S[i] = s_sum[t][i];
     const int cnt = nth[g];
-    const float4* src = reinterpret_cast<const float4*>(partials) + (size_t)offsets[g] * (kNP / 4);
-    for (int e = 0; e < cnt; ++e) {
-#pragma unroll
-        for (int k = 0; k < kNP / 4; ++k) {
-            float4 v = src[(size_t)e * (kNP / 4) + k];
-            S[4 * k] += v.x; S[4 * k + 1] += v.y; S[4 * k + 2] += v.z; S[4 * k + 3] += v.w;
-        }
-    }
     v_rgbs[3 * g + 0] = S[P_RGB + 0];
     v_rgbs[3 * g + 1] = S[P_RGB + 1];
     v_rgbs[3 * g + 2] = S[P_RGB + 2];
@@ -1247,15 +1267,20 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     CamArgs dc = to_device_camera(*cam);
     hipStream_t st = as_stream(stream);
     const int nblk = tiles_x * tiles_y;
-#define GSTEX_BWD(CC)                                                                                          \
-    raster_bwd_kernel<CC><<<nblk, kThreads, 0, st>>>(                                                          \
+    // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
+    const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
+#define GSTEX_BWD(CC, GG)                                                                                      \
+    raster_bwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(                                                      \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         tile_order, sorted_ids, sorted_slots, texture, tex_scale, tex_bias, (const float4*)state, v_img, v_depth,      \
         v_reg, v_alpha, v_tex,                                                                                  \
         v_normal, partials, v_texture)
-    if (channels == 3) GSTEX_BWD(3);
-    else if (channels == 6) GSTEX_BWD(6);
-    else GSTEX_BWD(0);
+    if (channels == 3 && !geo) GSTEX_BWD(3, false);
+    else if (channels == 3) GSTEX_BWD(3, true);
+    else if (channels == 6 && !geo) GSTEX_BWD(6, false);
+    else if (channels == 6) GSTEX_BWD(6, true);
+    else if (!geo) GSTEX_BWD(0, false);
+    else GSTEX_BWD(0, true);
 #undef GSTEX_BWD
     return launch_status("gstex_raster_bwd");
 }
@@ -1272,7 +1297,7 @@ extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float
     GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd: null pointer");
-    setup_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(
+    setup_bwd_kernel<<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
         n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
         v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     return launch_status("gstex_raster_setup_bwd");

@@ -101,6 +101,72 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int k0, 
     }
 }
 
+// The same two kernels with the coefficient rows staged through LDS: a workgroup's 128 splats own one
+// contiguous span of coefficients, read (forward) or written (backward) with consecutive lanes on
+// consecutive words; the per-thread strided rows (180 B apart at K = 15) made every load instruction
+// touch 64 cache lines.  Same arithmetic and order as above.  Used for K <= kShStagedMaxK.
+constexpr int kShBlock = 128;
+constexpr int kShStagedMaxK = 25;
+__global__ __launch_bounds__(kShBlock) void sh_fwd_staged_kernel(int n, int degree, int k0, int K,
+                                                                const float* __restrict__ dirs,
+                                                                const float* __restrict__ coeffs,
+                                                                float* __restrict__ out) {
+    extern __shared__ float s_c[];
+    const int t = threadIdx.x;
+    const int i0 = blockIdx.x * kShBlock;
+    const int cnt = min(kShBlock, n - i0);
+    const int nb = (degree + 1) * (degree + 1);
+    const int kn = (nb - k0) * 3;  // coefficient words used per splat (<= 3K)
+    const float* src = coeffs + (size_t)i0 * K * 3;
+    for (int q = t; q < cnt * kn; q += kShBlock) {
+        const int sp = q / kn, col = q - sp * kn;
+        s_c[sp * kn + col] = src[(size_t)sp * K * 3 + col];
+    }
+    __syncthreads();
+    if (t >= cnt) return;
+    const int i = i0 + t;
+    float b[25];
+    sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
+    const float* c = s_c + t * kn - 3 * k0;
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+    for (int k = k0; k < nb; ++k) {
+        r0 = r0 + b[k] * c[3 * k];
+        r1 = r1 + b[k] * c[3 * k + 1];
+        r2 = r2 + b[k] * c[3 * k + 2];
+    }
+    out[3 * i] = r0;
+    out[3 * i + 1] = r1;
+    out[3 * i + 2] = r2;
+}
+
+__global__ __launch_bounds__(kShBlock) void sh_bwd_staged_kernel(int n, int degree, int k0, int K,
+                                                                const float* __restrict__ dirs,
+                                                                const float* __restrict__ v_out,
+                                                                float* __restrict__ v_coeffs) {
+    extern __shared__ float s_c[];
+    const int t = threadIdx.x;
+    const int i0 = blockIdx.x * kShBlock;
+    const int cnt = min(kShBlock, n - i0);
+    const int kw = K * 3;
+    if (t < cnt) {
+        const int i = i0 + t;
+        float b[25];
+        sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
+        const int nb = (degree + 1) * (degree + 1);
+        const float g0 = v_out[3 * i], g1 = v_out[3 * i + 1], g2 = v_out[3 * i + 2];
+        float* vc = s_c + t * kw;
+        for (int k = 0; k < K; ++k) {
+            const float bk = (k + k0 < nb) ? b[k + k0] : 0.0f;
+            vc[3 * k] = bk * g0;
+            vc[3 * k + 1] = bk * g1;
+            vc[3 * k + 2] = bk * g2;
+        }
+    }
+    __syncthreads();
+    float* dst = v_coeffs + (size_t)i0 * kw;
+    for (int q = t; q < cnt * kw; q += kShBlock) dst[q] = s_c[q];
+}
+
 // One thread per (query, channel-group): query q reads its 4 corner texels.
 __global__ __launch_bounds__(256) void texture_sample_kernel(long long nq, int C, const int32_t* __restrict__ qd,
                                                              const float* __restrict__ tex,
@@ -150,7 +216,11 @@ extern "C" int gstex_sh_fwd(int32_t n, int32_t degree, int32_t n_coeffs, const f
                   n_coeffs, (degree + 1) * (degree + 1));
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(viewdirs && coeffs && colors, "gstex_sh_fwd: null pointer");
-    sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, coeffs, colors);
+    if (n_coeffs <= kShStagedMaxK)
+        sh_fwd_staged_kernel<<<div_up(n, kShBlock), kShBlock, (size_t)kShBlock * n_coeffs * 3 * sizeof(float),
+                               as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, coeffs, colors);
+    else
+        sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, coeffs, colors);
     return launch_status("gstex_sh_fwd");
 }
 
@@ -160,7 +230,11 @@ extern "C" int gstex_sh_bwd(int32_t n, int32_t degree, int32_t n_coeffs, const f
     GSTEX_REQUIRE(n_coeffs >= (degree + 1) * (degree + 1), "gstex_sh_bwd: too few coefficients");
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(viewdirs && v_colors && v_coeffs, "gstex_sh_bwd: null pointer");
-    sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, v_colors, v_coeffs);
+    if (n_coeffs <= kShStagedMaxK)
+        sh_bwd_staged_kernel<<<div_up(n, kShBlock), kShBlock, (size_t)kShBlock * n_coeffs * 3 * sizeof(float),
+                               as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, v_colors, v_coeffs);
+    else
+        sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 0, n_coeffs, viewdirs, v_colors, v_coeffs);
     return launch_status("gstex_sh_bwd");
 }
 
@@ -171,7 +245,11 @@ extern "C" int gstex_sh_rest_fwd(int32_t n, int32_t degree, int32_t n_rest, cons
                   n_rest);
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(viewdirs && colors && (coeffs_rest || n_rest == 0), "gstex_sh_rest_fwd: null pointer");
-    sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, coeffs_rest, colors);
+    if (n_rest <= kShStagedMaxK)
+        sh_fwd_staged_kernel<<<div_up(n, kShBlock), kShBlock, (size_t)kShBlock * n_rest * 3 * sizeof(float),
+                               as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, coeffs_rest, colors);
+    else
+        sh_fwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, coeffs_rest, colors);
     return launch_status("gstex_sh_rest_fwd");
 }
 
@@ -181,8 +259,11 @@ extern "C" int gstex_sh_rest_bwd(int32_t n, int32_t degree, int32_t n_rest, cons
     GSTEX_REQUIRE(n_rest >= 0, "gstex_sh_rest_bwd: n_rest < 0");
     if (n == 0 || n_rest == 0) return GSTEX_OK;
     GSTEX_REQUIRE(viewdirs && v_colors && v_coeffs_rest, "gstex_sh_rest_bwd: null pointer");
-    sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, v_colors,
-                                                                  v_coeffs_rest);
+    if (n_rest <= kShStagedMaxK)
+        sh_bwd_staged_kernel<<<div_up(n, kShBlock), kShBlock, (size_t)kShBlock * n_rest * 3 * sizeof(float),
+                               as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, v_colors, v_coeffs_rest);
+    else
+        sh_bwd_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, degree, 1, n_rest, viewdirs, v_colors, v_coeffs_rest);
     return launch_status("gstex_sh_rest_bwd");
 }
 

@@ -60,10 +60,13 @@ class _PhotometricLoss(torch.autograd.Function):
         ctx.save_for_backward(img, tex, alpha, background, gt, ws)
         ctx.ssim_lambda = float(ssim_lambda)
         ctx.mark_non_differentiable(rgb)
+        ctx.set_materialize_grads(False)  # rgb's (always unused) gradient stays None, no zero image
         return out[0], rgb  # out[1:] = (L1, SSIM) stay readable through the base tensor
 
     @staticmethod
     def backward(ctx, g_loss, g_rgb):
+        if g_loss is None:
+            return None, None, None, None, None, None
         img, tex, alpha, background, gt, ws = ctx.saved_tensors
         H, W = alpha.shape
         C = tex.shape[2]

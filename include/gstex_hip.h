@@ -82,7 +82,8 @@ int gstex_project_points_bwd(int32_t n, const float* means, const gstex_camera* 
 int gstex_aabb_2d(int32_t n, const float* means, const float* scales, float glob_scale,
                   const float* quats, const gstex_camera* cam, float* centers, float* extents,
                   void* stream);
-/* Accumulates (+=) the gradient of the AABB centre into v_means / v_scales / v_quats. */
+/* Writes the gradient of the AABB centre to v_means / v_scales / v_quats (every element; zero for
+   splats with no centre gradient or culled). */
 int gstex_aabb_2d_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                       const float* quats, const gstex_camera* cam, const float* v_centers,
                       float* v_means, float* v_scales, float* v_quats, void* stream);

@@ -50,7 +50,7 @@ def upstream(H, W, C, seed=5):
                 tex=torch.randn(H, W, C, generator=g), normal=torch.randn(H, W, 3, generator=g))
 
 
-def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64):
+def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64, outputs=None):
     inp = case.inp
     leaves = {}
     if grads:
@@ -62,7 +62,7 @@ def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64):
     out = {}
     if grads:
         up = upstream(inp.cam.H, inp.cam.W, case.C, seed)
-        loss = sum((o64[k] * up[k].to(grad_dtype)).sum() for k in up)
+        loss = sum((o64[k] * up[k].to(grad_dtype)).sum() for k in up if outputs is None or k in outputs)
         loss.backward()
         out = {k: (v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v).detach()).float()
                if v.grad is None else v.grad.detach().clone() for k, v in leaves.items()}
@@ -71,7 +71,9 @@ def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64):
     return o32, o64, aux, out
 
 
-def gpu_run(case: Case, grads=True, seed=5, device="cuda"):
+def gpu_run(case: Case, grads=True, seed=5, device="cuda", outputs=None):
+    """outputs: names of the outputs that receive an upstream gradient (default all six; the others
+    reach the kernel as NULL, as for outputs the loss does not use)."""
     import gstex_cuda
 
     inp = case.inp
@@ -92,7 +94,8 @@ def gpu_run(case: Case, grads=True, seed=5, device="cuda"):
     gr = {}
     if grads:
         up = upstream(inp.cam.H, inp.cam.W, case.C, seed)
-        torch.autograd.backward(list(outs), [up[k].to(device) for k in names])
+        sel = [i for i, k in enumerate(names) if outputs is None or k in outputs]
+        torch.autograd.backward([outs[i] for i in sel], [up[names[i]].to(device) for i in sel])
         gr = {k: (t[k].grad.detach().cpu() if t[k].grad is not None else torch.zeros_like(t[k]).cpu()) for k in t}
     return res, gr
 

@@ -145,13 +145,24 @@ CASES = {
 
 @pytest.mark.parametrize("name", list(CASES))
 def test_raster_forward_backward(name):
+    _check_raster(name, None)
+
+
+# img / alpha / tex gradients only (depth, distortion and normal gradients None, the training default):
+# the backward runs its specialisation without those terms
+@pytest.mark.parametrize("name", ["tex3_default", "tex6_eval", "no_aa", "ragged_17x33", "big_texel_blocks"])
+def test_raster_backward_photometric_only(name):
+    _check_raster(name, ("img", "alpha", "tex"))
+
+
+def _check_raster(name, outputs):
     case = make_case(**CASES[name])
-    o32, o64, aux, og = oracle_run(case, grads=True)
-    gout, gg = gpu_run(case, grads=True)
+    o32, o64, aux, og = oracle_run(case, grads=True, outputs=outputs)
+    gout, gg = gpu_run(case, grads=True, outputs=outputs)
     fwd = {k: (gout[k].double() - o64[k]).abs().max().item() for k in gout}
     _report(f"{name} fwd", fwd)
     assert_close_fwd(gout, o64)
-    _, _, _, og32 = oracle_run(case, grads=True, grad_dtype=torch.float32)
+    _, _, _, og32 = oracle_run(case, grads=True, grad_dtype=torch.float32, outputs=outputs)
     errs, norm_errs, inherent, inherent_n = {}, {}, {}, {}
     for k in DIFF:
         errs[k], _ = grad_rel_err(gg[k], og[k])
@@ -225,12 +236,13 @@ def test_outputs_independent_of_launch_order(monkeypatch):
 
 
 # ---------------------------------------------------------------- SH / texture_sample
+@pytest.mark.parametrize("K", [25, 30])  # LDS-staged kernels up to K = 25, direct kernels above
 @pytest.mark.parametrize("degree", [0, 1, 2, 3, 4])
-def test_sh_parity(degree):
+def test_sh_parity(degree, K):
     import gstex_cuda
 
     g = torch.Generator().manual_seed(degree)
-    n, K = 1000, 25
+    n = 1000
     dirs = torch.randn(n, 3, generator=g)
     coeffs = torch.randn(n, K, 3, generator=g)
     c = coeffs.to(DEV).requires_grad_(True)
