@@ -85,7 +85,8 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #ifndef GSTEX_ABLATE
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
-                        // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch
+                        // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
+                        // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion
 #endif
 #ifndef GSTEX_TEX_FIXED
 #define GSTEX_TEX_FIXED 1  // stage texel gradients as int64 fixed point (ds_add_u64) instead of ds_add_f32
@@ -573,14 +574,45 @@ __device__ __forceinline__ float dpp_shr_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x110 + OFF, 0xF, 0xF, false));
 }
 
+#ifndef GSTEX_SEG_FMA
+#define GSTEX_SEG_FMA 1
+#endif
+#ifndef GSTEX_FLUSH_WAVE
+#define GSTEX_FLUSH_WAVE 1  // flush staged texel gradients splat-major, one wave per splat block
+#endif
+// v += row_shr:OFF(v) * mf, mf = 1 where the lane OFF to the left is in the same segment, else 0: one
+// v_fmac_f32 with a DPP source per value (the compiler does not fold a DPP move into the tied-accumulator
+// fmac, so it is written out).  fma(t, 1, v) rounds as t + v and fma(t, 0, v) = v, so the result equals the
+// add-and-select form bit for bit.  The leading s_nop covers the VALU-write -> DPP-read hazard for the
+// values' last writers (the asm is opaque to the compiler's hazard recognizer); within the block each value is
+// read by DPP only after the other NV - 1 writes, and the trailing s_nop covers the compiler's next DPP read.
+template <int OFF>
+__device__ __forceinline__ void fmac_dpp_shr(float& v, float mf) {
+    if constexpr (OFF == 1)
+        asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(v) : "v"(mf));
+    else if constexpr (OFF == 2)
+        asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(v) : "v"(mf));
+    else if constexpr (OFF == 4)
+        asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(v) : "v"(mf));
+    else
+        asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(v) : "v"(mf));
+}
 template <int NV, int OFF>
 __device__ __forceinline__ void seg_step(int seg, float (&v)[NV]) {
     const int ss = dpp_shr_i<OFF>(-1, seg);
     const bool m = (ss == seg);
+    if (GSTEX_SEG_FMA) {
+        const float mf = m ? 1.0f : 0.0f;
+        asm volatile("s_nop 1" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const float t = dpp_shr_f<OFF>(v[i]);
-        v[i] = m ? v[i] + t : v[i];
+        for (int i = 0; i < NV; ++i) fmac_dpp_shr<OFF>(v[i], mf);
+        asm volatile("s_nop 1" ::: "memory");
+    } else {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const float t = dpp_shr_f<OFF>(v[i]);
+            v[i] = m ? v[i] + t : v[i];
+        }
     }
 }
 
@@ -627,7 +659,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     __shared__ float s_part[kBwdBatch][4][kNP];
     __shared__ int s_slot[kBwdBatch];
     __shared__ int s_toff[kBwdBatch];  // LDS offset of each splat's texel-gradient block (-1: global)
-    __shared__ int s_nfit, s_used, s_gexp;
+    __shared__ int s_gexp;
     __shared__ unsigned long long s_texq[kTexLds / 2];
     float* s_tex = reinterpret_cast<float*>(s_texq);  // float staging (GSTEX_TEX_FIXED = 0)
     __shared__ int s_maxlast;
@@ -718,9 +750,11 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         }
         if (tid < nb) s_slot[tid] = sorted_slots[b0 + tid];
         __syncthreads();
-        // place the batch's texel blocks in LDS: prefix of h*w*C over the batch (wave 0); splats past
-        // the capacity accumulate straight into global memory
-        if (wave == 0) {
+        // place the batch's texel blocks in LDS: prefix of h*w*C over the batch, computed by every wave for
+        // itself (lane j <-> splat j; no extra barrier); splats past the capacity accumulate straight into
+        // global memory
+        int my_toff, nfit, used;
+        {
             int sz = 0;
             if (lane < nb) {
                 const float4 q = s_rec[6 * kBwdBatch + lane];
@@ -728,22 +762,17 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             }
             int incl = sz;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
+            for (int o = 1; o < kBwdBatch; o <<= 1) {
                 const int t = __shfl_up(incl, o, 64);
                 if (lane >= o) incl += t;
             }
             const bool fits = incl <= kTexCap;
-            if (lane < kBwdBatch) s_toff[lane] = (lane < nb && fits) ? incl - sz : -1;
+            my_toff = (lane < nb && fits) ? incl - sz : -1;
             const unsigned long long fm = __ballot(fits && lane < nb);
-            if (lane == 0) {
-                const int nfit = __popcll(fm);
-                s_nfit = nfit;
-                s_used = 0;
-            }
-            const int nfit = __popcll(fm);
-            if (nfit > 0 && lane == nfit - 1) s_used = incl;
+            nfit = __popcll(fm);
+            used = nfit > 0 ? __builtin_amdgcn_readlane(incl, nfit - 1) : 0;
+            if (!GSTEX_FLUSH_WAVE && wave == 0 && lane < kBwdBatch) s_toff[lane] = my_toff;
         }
-        __syncthreads();
 
         // the batch splats this wave must visit, tested all at once (lane j <-> splat j): some lane
         // of the wave reaches it (rel <= last) and its contribution box meets the wave's 16x4 block
@@ -884,7 +913,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             GSTEX_STAT(1, 1);
             GSTEX_STAT(2, any ? 1 : 0);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
-            GSTEX_STAT(4, (__popcll(__ballot(tkey >= 0)) && s_toff[j] < 0) ? 1 : 0);  // texel grads via global
+            GSTEX_STAT(4, (__popcll(__ballot(tkey >= 0)) && __builtin_amdgcn_readlane(my_toff, j) < 0) ? 1 : 0);  // texel grads via global
             if (GSTEX_ABLATE & 2) {
 #pragma unroll
                 for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
@@ -936,7 +965,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 } else if (tail) {
                     // keep the LDS and global paths apart: a pointer that may be either compiles to
                     // flat atomics, several times slower than ds_add_f32 on LDS
-                    const int toff = s_toff[j];
+                    const int toff = __builtin_amdgcn_readlane(my_toff, j);
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
                     const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
                     const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
@@ -944,10 +973,12 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-                                atomicAdd(&s_texq[toff + c00 + c], (unsigned long long)fixed_from(tg[c], tex_S));
-                                atomicAdd(&s_texq[toff + c01 + c], (unsigned long long)fixed_from(tg[CM + c], tex_S));
-                                atomicAdd(&s_texq[toff + c10 + c], (unsigned long long)fixed_from(tg[2 * CM + c], tex_S));
-                                atomicAdd(&s_texq[toff + c11 + c], (unsigned long long)fixed_from(tg[3 * CM + c], tex_S));
+#define GSTEX_FX(v) ((GSTEX_ABLATE & 64) ? (unsigned long long)__float_as_uint(v) : (unsigned long long)fixed_from(v, tex_S))
+                                atomicAdd(&s_texq[toff + c00 + c], GSTEX_FX(tg[c]));
+                                atomicAdd(&s_texq[toff + c01 + c], GSTEX_FX(tg[CM + c]));
+                                atomicAdd(&s_texq[toff + c10 + c], GSTEX_FX(tg[2 * CM + c]));
+                                atomicAdd(&s_texq[toff + c11 + c], GSTEX_FX(tg[3 * CM + c]));
+#undef GSTEX_FX
                             }
                         }
                     } else if (toff >= 0) {
@@ -995,8 +1026,23 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             }
         }
         // flush the staged texel gradients (only touched entries) and re-zero the staging area
-        {
-            const int used = s_used, nfit = s_nfit;
+        if (GSTEX_TEX_FIXED && GSTEX_FLUSH_WAVE) {
+            // splat-major: wave k flushes the staged blocks of batch splats k, k+4, ... (the block base and
+            // size are wave-uniform, so no per-slot owner search), lanes striding over the block
+            for (int j = wave; j < nfit; j += 4) {
+                const int t0 = __builtin_amdgcn_readlane(my_toff, j);
+                const float4 q = s_rec[6 * kBwdBatch + j];
+                const int size = __float_as_int(q.x) * __float_as_int(q.y) * Cn;
+                float* dst = v_texture + (size_t)__float_as_int(q.z) * Cn;
+                for (int e = lane; e < size; e += 64) {
+                    const long long v = (long long)s_texq[t0 + e];
+                    if (v != 0) {
+                        s_texq[t0 + e] = 0ull;
+                        if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e, fixed_to(v, tex_S));
+                    }
+                }
+            }
+        } else {
             for (int idx = tid; idx < used; idx += kThreads) {
                 float val;
                 if (GSTEX_TEX_FIXED) {
@@ -1014,7 +1060,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                         else hi = mid - 1;
                     }
                     const int off = __float_as_int(s_rec[6 * kBwdBatch + lo].z);
-                    atomicAdd(v_texture + (size_t)off * Cn + (idx - s_toff[lo]), val);
+                    if (!(GSTEX_ABLATE & 32)) atomicAdd(v_texture + (size_t)off * Cn + (idx - s_toff[lo]), val);
                     if (!GSTEX_TEX_FIXED) s_tex[idx] = 0.0f;
                 }
             }

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--n-texels", type=float, default=1e7)
     ap.add_argument("--size", type=int, default=800)
     ap.add_argument("--opacity", type=float, default=0.1)
+    ap.add_argument("--photometric", action="store_true",
+                    help="upstream gradients on img/alpha/tex only (the training step's case)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = make_scene(args.n_splats, args.n_texels, seed=42, opacity=args.opacity if args.opacity > 0 else None)
@@ -45,7 +47,10 @@ def main():
         outs = ops.texture_gaussians((sc.n, 1, 3), dims, c, e, depths, nth, rgbs, opac, means, scales, 1, quats,
                                      uv0, umap, vmap, tex, v.viewmat, v.c2w, v.fx, v.fy, v.cx, v.cy, args.size,
                                      args.size, 16, (1 << 9) | (1 << 10), background=None)
-        torch.autograd.backward(list(outs), ups)
+        if args.photometric:
+            torch.autograd.backward([outs[0], outs[3], outs[4]], [ups[0], ups[3], ups[4]])
+        else:
+            torch.autograd.backward(list(outs), ups)
         return nth
 
     nth = run()
