@@ -388,6 +388,36 @@ __device__ __forceinline__ void load_texel_rs(__amdgpu_buffer_rsrc_t rs, int idx
     }
 }
 
+// The 4 bilinear texels of a splat block: byte offsets from one 24-bit multiply-add (v_mul_u32_u24 is
+// full rate; the block index i*w + j < 2^24) plus wave-uniform row/column steps.
+template <int CM>
+__device__ __forceinline__ void load_texel_quad(__amdgpu_buffer_rsrc_t rs, const Bilerp& b, int w, int Cn,
+                                                float (&t00)[CM], float (&t01)[CM], float (&t10)[CM],
+                                                float (&t11)[CM]) {
+    if constexpr (CM == 3) {
+        const int o00 = (int)__umul24(__umul24(b.i0, w) + b.j0, 12u);
+        const int o01 = b.j1 > b.j0 ? o00 + 12 : o00;
+        const int o10 = b.i1 > b.i0 ? o00 + w * 12 : o00;
+        const int o11 = b.j1 > b.j0 ? o10 + 12 : o10;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b96(rs, o00, 0, 0);
+        const auto c = __builtin_amdgcn_raw_buffer_load_b96(rs, o01, 0, 0);
+        const auto d = __builtin_amdgcn_raw_buffer_load_b96(rs, o10, 0, 0);
+        const auto e = __builtin_amdgcn_raw_buffer_load_b96(rs, o11, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            t00[k] = __int_as_float(a[k]);
+            t01[k] = __int_as_float(c[k]);
+            t10[k] = __int_as_float(d[k]);
+            t11[k] = __int_as_float(e[k]);
+        }
+    } else {
+        load_texel_rs<CM>(rs, b.i0 * w + b.j0, Cn, t00);
+        load_texel_rs<CM>(rs, b.i0 * w + b.j1, Cn, t01);
+        load_texel_rs<CM>(rs, b.i1 * w + b.j0, Cn, t10);
+        load_texel_rs<CM>(rs, b.i1 * w + b.j1, Cn, t11);
+    }
+}
+
 __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float& tu, float& tv) {
     tu = r.tu0 + (u * r.auu + v * r.auv);
     tv = r.tv0 + (u * r.avu + v * r.avv);
@@ -467,10 +497,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
                 const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
                 const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
                 float t00[CM], t01[CM], t10[CM], t11[CM];
-                load_texel_rs<CM>(rs, b.i0 * r.w + b.j0, Cn, t00);
-                load_texel_rs<CM>(rs, b.i0 * r.w + b.j1, Cn, t01);
-                load_texel_rs<CM>(rs, b.i1 * r.w + b.j0, Cn, t10);
-                load_texel_rs<CM>(rs, b.i1 * r.w + b.j1, Cn, t11);
+                load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < Cn) {
@@ -525,7 +552,9 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
 // (l & 7) == 0 holds the wave sums of values [12*b5 + 6*b4 + 3*b3 + 0..2] (b5,b4,b3 = bits of l).
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    // every pattern used here reads a lane inside the same row, so the old value never shows: mov_dpp
+    // (undefined old) needs no zero materialised and folds into the consuming add
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ void wave_reduce24(float (&v)[kNP]) {
@@ -569,6 +598,11 @@ template <int OFF>
 __device__ __forceinline__ int dpp_shr_i(int old, int v) {
     return __builtin_amdgcn_update_dpp(old, v, 0x110 + OFF, 0xF, 0xF, false);
 }
+// row_shr:OFF with out-of-row lanes reading 0 (bound_ctrl)
+template <int CTRL>
+__device__ __forceinline__ int dpp_bc_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
 template <int OFF>
 __device__ __forceinline__ float dpp_shr_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x110 + OFF, 0xF, 0xF, false));
@@ -599,7 +633,7 @@ __device__ __forceinline__ void fmac_dpp_shr(float& v, float mf) {
 }
 template <int NV, int OFF>
 __device__ __forceinline__ void seg_step(int seg, float (&v)[NV]) {
-    const int ss = dpp_shr_i<OFF>(-1, seg);
+    const int ss = dpp_bc_i<0x110 + OFF>(seg);  // segment ids are >= 1: an out-of-row 0 never matches
     const bool m = (ss == seg);
     if (GSTEX_SEG_FMA) {
         const float mf = m ? 1.0f : 0.0f;
@@ -623,7 +657,7 @@ template <int NV>
 __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     constexpr int SW = GSTEX_SEG_W;
     const int pos = threadIdx.x & (SW - 1);
-    const int left = dpp_shr_i<1>(-7, key);
+    const int left = dpp_bc_i<0x111>(key);  // unused at pos 0 (a forced head)
     int seg = (pos == 0 || left != key) ? 1 : 0;  // head flag: group start or key change
     // segment id = inclusive prefix count of heads over the whole 16-lane DPP row (a shorter window would
     // give two lanes of one segment different counts); the forced head at pos 0 separates groups
@@ -635,7 +669,7 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     seg_step<NV, 2>(seg, v);
     if (SW > 4) seg_step<NV, 4>(seg, v);
     if (SW > 8) seg_step<NV, 8>(seg, v);
-    const int ns = __builtin_amdgcn_update_dpp(-1, seg, 0x101, 0xF, 0xF, false);  // row_shl:1
+    const int ns = dpp_bc_i<0x101>(seg);  // row_shl:1; 0 past the row end (ids are >= 1)
     return key >= 0 && (ns != seg || pos == SW - 1);
 }
 
@@ -705,6 +739,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     }
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
+    float Gtex_bias = 0.f;  // tex_bias * sum_c dL/dtex[c]: the bias part of sum_c dL/dtex[c] * texel value
+#pragma unroll
+    for (int c = 0; c < CM; ++c) Gtex_bias += Gtex[c];
+    Gtex_bias *= tex_bias;
 
     if (tid == 0) {
         s_maxlast = -1;
@@ -818,12 +856,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                         float tu, tv;
                         tex_coords(r, h.u, h.v, tu, tv);
                         b = bilerp_coords(tu, tv, r.h, r.w);
-                        if (!(GSTEX_ABLATE & 8)) {
-                            load_texel_rs<CM>(rs, b.i0 * r.w + b.j0, Cn, t00);
-                            load_texel_rs<CM>(rs, b.i0 * r.w + b.j1, Cn, t01);
-                            load_texel_rs<CM>(rs, b.i1 * r.w + b.j0, Cn, t10);
-                            load_texel_rs<CM>(rs, b.i1 * r.w + b.j1, Cn, t11);
-                        }
+                        if (!(GSTEX_ABLATE & 8)) load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
                     }
                     float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
                     P[P_RGB + 0] = w * Gimg[0];
@@ -843,28 +876,32 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     }
                     // texel gradients: per-lane bilinear contributions, scattered after the P reduction
                     if (has_tex && !(GSTEX_ABLATE & 1)) {
-                        tkey = (b.i0 * r.w + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
+                        tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
                         tw = w * tex_scale;  // d value / d stored texel
                         tax = b.ax;
                         tay = b.ay;
                     }
-                    // texture value (tex_scale * stored + tex_bias) and its uv-gradient
+                    // texture value (tex_scale * stored + tex_bias) and its uv-gradient.  Both are linear in the
+                    // texels, so the channels are folded first: D_k = sum_c Gtex[c] * t_k[c] per bilinear corner,
+                    // then one bilinear mix and one pair of differences serve all channels
                     float dtu = 0.f, dtv = 0.f;
                     if (has_tex) {
                         const float hf = (float)r.h, wf = (float)r.w;
+                        float D00 = 0.f, D01 = 0.f, D10 = 0.f, D11 = 0.f;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-                                const float v00 = t00[c], v01 = t01[c], v10 = t10[c], v11 = t11[c];
-                                const float tau = bilerp_mix(v00, v01, v10, v11, b.ax, b.ay) * tex_scale + tex_bias;
-                                g += Gtex[c] * tau;
-                                const float gt = w * Gtex[c];
-                                const float eu = gt * (hf * ((1.0f - b.ay) * (v10 - v00) + b.ay * (v11 - v01)));
-                                const float ev = gt * (wf * ((1.0f - b.ax) * (v01 - v00) + b.ax * (v11 - v10)));
-                                dtu += b.in_u ? eu : 0.0f;
-                                dtv += b.in_v ? ev : 0.0f;
+                                D00 = D00 + Gtex[c] * t00[c];
+                                D01 = D01 + Gtex[c] * t01[c];
+                                D10 = D10 + Gtex[c] * t10[c];
+                                D11 = D11 + Gtex[c] * t11[c];
                             }
                         }
+                        g += bilerp_mix(D00, D01, D10, D11, b.ax, b.ay) * tex_scale + Gtex_bias;
+                        const float su = (1.0f - b.ay) * (D10 - D00) + b.ay * (D11 - D01);
+                        const float sv = (1.0f - b.ax) * (D01 - D00) + b.ax * (D11 - D10);
+                        dtu = b.in_u ? w * (hf * su) : 0.0f;
+                        dtv = b.in_v ? w * (wf * sv) : 0.0f;
                     }
                     if (GEO) {
                         g += Gd * h.z;
