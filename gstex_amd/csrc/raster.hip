@@ -113,6 +113,11 @@ __device__ __forceinline__ long long fixed_from(float v, int S) {
     return __double_as_longlong(d + 0x1.8p52) - __double_as_longlong(0x1.8p52);
 }
 __device__ __forceinline__ float fixed_to(long long q, int S) { return __builtin_ldexpf((float)q, -S); }
+// fixed_from for a value already scaled by 2^S (exact: a power-of-two factor commutes with every rounding of
+// the products that formed it): one f32 -> f64 conversion and the magic-number add, no f64 ldexp
+__device__ __forceinline__ long long fixed_from_scaled(float y) {
+    return __double_as_longlong((double)y + 0x1.8p52) - __double_as_longlong(0x1.8p52);
+}
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -767,6 +772,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         if (gmax > 0.f) (void)frexpf(gmax, &e);  // gmax < 2^e
         tex_S = 41 - e;
     }
+    // texel-gradient contributions are formed directly in the fixed-point scale
+    const float tex_scale_q = GSTEX_TEX_FIXED ? __builtin_ldexpf(tex_scale, tex_S) : tex_scale;
     int wave_last = last;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wave_last = max(wave_last, __shfl_xor(wave_last, o, 64));
@@ -877,7 +884,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     // texel gradients: per-lane bilinear contributions, scattered after the P reduction
                     if (has_tex && !(GSTEX_ABLATE & 1)) {
                         tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
-                        tw = w * tex_scale;  // d value / d stored texel
+                        tw = w * tex_scale_q;  // d value / d stored texel (x 2^tex_S with fixed-point staging)
                         tax = b.ax;
                         tay = b.ay;
                     }
@@ -1010,7 +1017,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-#define GSTEX_FX(v) ((GSTEX_ABLATE & 64) ? (unsigned long long)__float_as_uint(v) : (unsigned long long)fixed_from(v, tex_S))
+#define GSTEX_FX(v) ((GSTEX_ABLATE & 64) ? (unsigned long long)__float_as_uint(v) : (unsigned long long)fixed_from_scaled(v))
                                 atomicAdd(&s_texq[toff + c00 + c], GSTEX_FX(tg[c]));
                                 atomicAdd(&s_texq[toff + c01 + c], GSTEX_FX(tg[CM + c]));
                                 atomicAdd(&s_texq[toff + c10 + c], GSTEX_FX(tg[2 * CM + c]));
@@ -1029,14 +1036,16 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                             }
                         }
                     } else {
+                        // staging overflow: straight to global, back in value units
                         float* base = v_texture + (size_t)r.off * Cn;
+                        const int uS = GSTEX_TEX_FIXED ? -tex_S : 0;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-                                atomicAdd(base + c00 + c, tg[c]);
-                                atomicAdd(base + c01 + c, tg[CM + c]);
-                                atomicAdd(base + c10 + c, tg[2 * CM + c]);
-                                atomicAdd(base + c11 + c, tg[3 * CM + c]);
+                                atomicAdd(base + c00 + c, __builtin_ldexpf(tg[c], uS));
+                                atomicAdd(base + c01 + c, __builtin_ldexpf(tg[CM + c], uS));
+                                atomicAdd(base + c10 + c, __builtin_ldexpf(tg[2 * CM + c], uS));
+                                atomicAdd(base + c11 + c, __builtin_ldexpf(tg[3 * CM + c], uS));
                             }
                         }
                     }

@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/ablate; mkdir -p $OUT
 for v in "$@"; do
   GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 120 python3 tools/raster_loop.py --photometric --iters 20 > $OUT/$v.log 2>&1 || { echo "FAIL $v"; exit 1; }
-  echo "$v: $(tail -1 $OUT/$v.log)"
+  echo "$v: $(tail -2 $OUT/$v.log | tr '\n' ' ')"
 done
 if [ -n "$PMC" ]; then
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --output-format csv -d $OUT/pmc1 -o run -- python3 tools/raster_loop.py --photometric --iters 3 > $OUT/pmc1.log 2>&1 || { echo "pmc1 failed"; exit 1; }

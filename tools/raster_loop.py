@@ -63,6 +63,15 @@ def main():
     dt = (time.perf_counter() - t0) / args.iters
     kt = {k.replace("gstex_", ""): round(sum(v) / len(v), 3) for k, v in ops.kernel_times().items()}
     ops.set_kernel_timing(False)
+    from gstex_amd import _lib
+    lib = _lib.load()
+    if hasattr(lib, "gstex_debug_stats"):  # GSTEX_STATS=1 builds: backward work counters over all launches
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        lib.gstex_debug_stats(buf)
+        n = args.iters + 1
+        names = ["batch_splats", "visits", "visits_any", "contrib_lanes", "global_tex", "tails", "distinct", "tail_visits"]
+        print("stats/launch:", {k: round(v / n) for k, v in zip(names, buf)})
     print(f"fwd+bwd+preprocess {dt * 1e3:.3f} ms/iter  visible={int((nth > 0).sum())} isect={int(nth.sum())} "
           f"kernel_ms={kt}")
 
