@@ -86,7 +86,8 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #ifndef GSTEX_ABLATE
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
-                        // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion
+                        // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
+                        // 128 = no barrier before the combine (timing experiments only: racy)
 #endif
 #ifndef GSTEX_TEX_FIXED
 #define GSTEX_TEX_FIXED 1  // stage texel gradients as int64 fixed point (ds_add_u64) instead of ds_add_f32
@@ -707,6 +708,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 #if GSTEX_STATS
     const unsigned long long t_start = wall_clock64();
 #endif
+#if GSTEX_STATS == 2
+    // phase clock per wave: 0 record load + barrier, 1 placement + cull, 2 visits, 3 barrier before the
+    // combine, 4 combine + flush, 5 closing barrier, 6 prologue
+    unsigned long long ph_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = __builtin_amdgcn_s_memtime();
+#define GSTEX_PHASE(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[k] += t_ - ph_t; ph_t = t_; } while (0)
+#else
+#define GSTEX_PHASE(k) do { } while (0)
+#endif
     const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -786,6 +796,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         for (int k = 0; k < kNP / 4; ++k) dst[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
+    GSTEX_PHASE(6);
     for (int bb = tile_last / kBwdBatch; bb >= 0 && tile_last >= 0; --bb) {
         const int b0 = rng.x + bb * kBwdBatch;
         const int nb = min(kBwdBatch, tile_last - bb * kBwdBatch + 1);
@@ -795,6 +806,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         }
         if (tid < nb) s_slot[tid] = sorted_slots[b0 + tid];
         __syncthreads();
+        GSTEX_PHASE(0);
         // place the batch's texel blocks in LDS: prefix of h*w*C over the batch, computed by every wave for
         // itself (lane j <-> splat j; no extra barrier); splats past the capacity accumulate straight into
         // global memory
@@ -829,6 +841,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         }
         unsigned live = 0u;
         GSTEX_STAT(0, nb);
+        GSTEX_PHASE(1);
         while (todo) {
             const int j = 31 - __builtin_clz(todo);
             todo &= ~(1u << j);
@@ -1052,8 +1065,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 }
             }
         }
+        GSTEX_PHASE(2);
         if (lane == 0) s_live[wave] = live;
-        __syncthreads();
+        if (!(GSTEX_ABLATE & 128)) __syncthreads();  // (ablation 128: timing only, races)
+        GSTEX_PHASE(3);
         // combine the 4 waves in a fixed order (a wave that skipped the splat adds +0) and store the
         // (tile, splat) partial
         {
@@ -1111,8 +1126,14 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 }
             }
         }
+        GSTEX_PHASE(4);
         __syncthreads();
+        GSTEX_PHASE(5);
     }
+#if GSTEX_STATS == 2
+    if (lane == 0)
+        for (int k = 0; k < 7; ++k) atomicAdd(&g_stats[k], ph_acc[k]);
+#endif
 #if GSTEX_STATS
     if (tid == 0 && tile < 4096) {
         g_wg[4 * tile + 0] = t_start;

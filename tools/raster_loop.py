@@ -71,6 +71,9 @@ def main():
         lib.gstex_debug_stats(buf)
         n = args.iters + 1
         names = ["batch_splats", "visits", "visits_any", "contrib_lanes", "global_tex", "tails", "distinct", "tail_visits"]
+        if os.environ.get("GSTEX_STATS_PHASES"):  # GSTEX_STATS=2: wave-clock sums per backward phase
+            names = ["load+barrier", "place+cull", "visits", "barrier_pre_combine", "combine+flush", "barrier_end",
+                     "prologue", "-"]
         print("stats/launch:", {k: round(v / n) for k, v in zip(names, buf)})
     print(f"fwd+bwd+preprocess {dt * 1e3:.3f} ms/iter  visible={int((nth > 0).sum())} isect={int(nth.sum())} "
           f"kernel_ms={kt}")
