@@ -44,21 +44,32 @@ __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
     const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
                        reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
     if (vec) {
+        // all 16 loads of the thread issued before any store (stores could alias later loads, so the
+        // compiler would otherwise keep only one iteration's 4 loads in flight)
+        float4 p[4], g[4], m[4], v[4];
+        bool full[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t i = base + 4 * ((int64_t)r * kAdamThreads + threadIdx.x);
-            if (i + 3 < t.numel) {
-                float4 p = *reinterpret_cast<const float4*>(t.param + i);
-                const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
-                float4 m = *reinterpret_cast<const float4*>(t.exp_avg + i);
-                float4 v = *reinterpret_cast<const float4*>(t.exp_avg_sq + i);
-                adam_elem(p.x, g.x, m.x, v.x, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                adam_elem(p.y, g.y, m.y, v.y, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                adam_elem(p.z, g.z, m.z, v.z, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                adam_elem(p.w, g.w, m.w, v.w, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                *reinterpret_cast<float4*>(t.param + i) = p;
-                *reinterpret_cast<float4*>(t.exp_avg + i) = m;
-                *reinterpret_cast<float4*>(t.exp_avg_sq + i) = v;
+            full[r] = i + 3 < t.numel;
+            if (full[r]) {
+                p[r] = *reinterpret_cast<const float4*>(t.param + i);
+                g[r] = *reinterpret_cast<const float4*>(t.grad + i);
+                m[r] = *reinterpret_cast<const float4*>(t.exp_avg + i);
+                v[r] = *reinterpret_cast<const float4*>(t.exp_avg_sq + i);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t i = base + 4 * ((int64_t)r * kAdamThreads + threadIdx.x);
+            if (full[r]) {
+                adam_elem(p[r].x, g[r].x, m[r].x, v[r].x, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem(p[r].y, g[r].y, m[r].y, v[r].y, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem(p[r].z, g[r].z, m[r].z, v[r].z, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem(p[r].w, g[r].w, m[r].w, v[r].w, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                *reinterpret_cast<float4*>(t.param + i) = p[r];
+                *reinterpret_cast<float4*>(t.exp_avg + i) = m[r];
+                *reinterpret_cast<float4*>(t.exp_avg_sq + i) = v[r];
             } else {
                 for (int64_t e = i; e < t.numel; ++e)
                     adam_elem(t.param[e], t.grad[e], t.exp_avg[e], t.exp_avg_sq[e], a.one_m_beta1, a.beta2,

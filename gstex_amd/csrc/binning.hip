@@ -305,44 +305,54 @@ __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
 // 5. largest-first tile order (LPT list scheduling).  The hardware hands out workgroups in
 // blockIdx order, round-robin over the 8 XCDs; launching the heaviest tiles first keeps every XCD
 // busy until the end instead of leaving a long tail behind the image centre's deep tiles.
-constexpr int kOrderCap = 16384;  // tiles sorted in one LDS pass (64 KiB of 32-bit keys)
-constexpr int kOrderThreads = 1024;
+constexpr int kOrderCap = 16384;  // tiles ranked by the quadratic kernel (beyond: row-major order)
 constexpr unsigned kOrderTileBits = 14;
 constexpr unsigned kOrderMaxCount = (1u << (32 - kOrderTileBits)) - 1;
 
-__global__ __launch_bounds__(kOrderThreads) void tile_order_kernel(int n_tiles, const int32_t* __restrict__ tile_ranges,
-                                                                   int32_t* __restrict__ tile_order) {
-    __shared__ unsigned s_key[kOrderCap];
-    if (n_tiles > kOrderCap) {  // too many tiles for one LDS sort: plain row-major order
-        for (int t = threadIdx.x; t < n_tiles; t += kOrderThreads) tile_order[t] = t;
-        return;
-    }
-    int P = 1;
-    while (P < n_tiles) P <<= 1;
-    for (int t = threadIdx.x; t < P; t += kOrderThreads) {
-        unsigned key = ~0u;
-        if (t < n_tiles) {
-            const unsigned cnt = (unsigned)min((int)kOrderMaxCount, tile_ranges[2 * t + 1] - tile_ranges[2 * t]);
-            key = ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
+// Tile order by ranking: tile t goes to position #{tiles u : key_u < key_t} (keys are unique: the tile index is
+// in the low bits).  Each 256-thread workgroup ranks 256 tiles against all keys, staged through LDS in chunks
+// and read as broadcast 16-B vectors: O(n^2) compares spread over the whole chip instead of a bitonic sort
+// in one workgroup (78 barrier-separated stages for 2 500 tiles).
+constexpr int kRankThreads = 256;
+constexpr int kRankTiles = 64;  // tiles per workgroup; the 4 waves each compare against a quarter of the keys
+constexpr int kRankChunk = 4096;
+
+__device__ __forceinline__ unsigned order_key(const int32_t* tile_ranges, int t) {
+    const unsigned cnt = (unsigned)min((int)kOrderMaxCount, tile_ranges[2 * t + 1] - tile_ranges[2 * t]);
+    return ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
+}
+
+__global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, const int32_t* __restrict__ tile_ranges,
+                                                                 int32_t* __restrict__ tile_order) {
+    __shared__ uint4 s_key[kRankChunk / 4];
+    __shared__ int s_rank[4][kRankTiles];
+    unsigned* s_k = reinterpret_cast<unsigned*>(s_key);
+    const int part = threadIdx.x >> 6;
+    const int t = blockIdx.x * kRankTiles + (threadIdx.x & 63);
+    const unsigned mine = t < n_tiles ? order_key(tile_ranges, t) : 0u;
+    int rank = 0;
+    for (int c0 = 0; c0 < n_tiles; c0 += kRankChunk) {
+        const int cn = min(kRankChunk, n_tiles - c0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < kRankChunk; i += kRankThreads)
+            s_k[i] = i < cn ? order_key(tile_ranges, c0 + i) : ~0u;  // padding never ranks below a key
+        __syncthreads();
+        const int nv = (cn + 3) >> 2;
+        const int q0 = (nv * part) >> 2, q1 = (nv * (part + 1)) >> 2;
+        for (int i = q0; i < q1; ++i) {
+            const uint4 k = s_key[i];
+            rank += (int)(k.x < mine) + (int)(k.y < mine) + (int)(k.z < mine) + (int)(k.w < mine);
         }
-        s_key[t] = key;
     }
+    s_rank[part][threadIdx.x & 63] = rank;
     __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int p = threadIdx.x; p < (P >> 1); p += kOrderThreads) {
-                const int i = 2 * p - (p & (j - 1)), ixj = i + j;
-                const unsigned a = s_key[i], b = s_key[ixj];
-                if ((a > b) == ((i & k) == 0)) {
-                    s_key[i] = b;
-                    s_key[ixj] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int t = threadIdx.x; t < n_tiles; t += kOrderThreads)
-        tile_order[t] = (int32_t)(s_key[t] & ((1u << kOrderTileBits) - 1));
+    if (part == 0 && t < n_tiles)
+        tile_order[s_rank[0][threadIdx.x] + s_rank[1][threadIdx.x] + s_rank[2][threadIdx.x] + s_rank[3][threadIdx.x]] = t;
+}
+
+__global__ void iota_kernel(int n, int32_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = i;
 }
 
 struct BinWorkspace {
@@ -442,6 +452,11 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
     GSTEX_REQUIRE(n_tiles >= 0, "gstex_tile_order: invalid n_tiles %d", n_tiles);
     if (n_tiles == 0) return GSTEX_OK;
     GSTEX_REQUIRE(tile_ranges && tile_order, "gstex_tile_order: null pointer");
-    tile_order_kernel<<<1, kOrderThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges, tile_order);
+    if (n_tiles > kOrderCap) {  // beyond the quadratic ranking's budget: row-major order
+        iota_kernel<<<div_up(n_tiles, 256), 256, 0, as_stream(stream)>>>(n_tiles, tile_order);
+        return launch_status("gstex_tile_order");
+    }
+    tile_rank_kernel<<<div_up(n_tiles, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges,
+                                                                                         tile_order);
     return launch_status("gstex_tile_order");
 }

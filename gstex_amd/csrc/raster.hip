@@ -66,6 +66,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #else
 #define GSTEX_FWD_ATTR
 #endif
+#ifndef GSTEX_FWD_SLOAD
+#define GSTEX_FWD_SLOAD 0  // 1: forward reads each visited record through scalar loads (SGPRs) instead of LDS
+#endif
 #ifndef GSTEX_CONIC_CULL
 #define GSTEX_CONIC_CULL 1  // per-wave ellipse-vs-rectangle cull on top of the contribution box
 #endif
@@ -222,6 +225,24 @@ __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
     const float4 c = uni4<SGPR>(s[2 * NB + j]), d = uni4<SGPR>(s[3 * NB + j]);
     const float4 e = uni4<SGPR>(s[4 * NB + j]), f = uni4<SGPR>(s[5 * NB + j]);
     const float4 g = uni4<SGPR>(s[6 * NB + j]), q = uni4<SGPR>(s[7 * NB + j]);
+    Rec r;
+    r.Tu = f3{a.x, a.y, a.z};
+    r.Tv = f3{a.w, b.x, b.y};
+    r.Tw = f3{b.z, b.w, c.x};
+    r.x = c.y; r.y = c.z; r.opac = c.w;
+    r.rgb[0] = d.x; r.rgb[1] = d.y; r.rgb[2] = d.z;
+    r.nrm[0] = d.w; r.nrm[1] = e.x; r.nrm[2] = e.y;
+    r.tu0 = e.z; r.auu = e.w; r.auv = f.x; r.tv0 = f.y; r.avu = f.z; r.avv = f.w;
+    r.h = __float_as_int(g.x); r.w = __float_as_int(g.y); r.off = __float_as_int(g.z);
+    r.xa = q.x; r.ya = q.y;
+    return r;
+}
+
+// The same record read from global memory at a wave-uniform address: scalar loads straight into SGPRs
+// (no LDS read, no v_readfirstlane per value).
+__device__ __forceinline__ Rec read_rec_global(const float4* __restrict__ rec) {
+    const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
+    const float4 e = rec[4], f = rec[5], g = rec[6], q = rec[7];
     Rec r;
     r.Tu = f3{a.x, a.y, a.z};
     r.Tv = f3{a.w, b.x, b.y};
@@ -444,6 +465,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
+    __shared__ int s_gid[kFwdBatch];
     const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x;
@@ -472,6 +494,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             const int j = q / kRecF4, k = q % kRecF4;
             if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
         }
+        if (GSTEX_FWD_SLOAD && tid < kFwdBatch && b0 + tid < rng.y) s_gid[tid] = sorted_ids[b0 + tid];
         __syncthreads();
         const int nb = min(kFwdBatch, rng.y - b0);
         // the batch splats whose contribution box meets this wave's 16x4 block, tested all at once
@@ -488,7 +511,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             if (done) break;
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
-            const Rec r = read_rec<kFwdBatch>(s_rec, j);
+            const Rec r = GSTEX_FWD_SLOAD ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
+                                         : read_rec<kFwdBatch>(s_rec, j);
             Hit h;
             if (!eval_hit(r, px, py, aa, h)) continue;
             const float test_T = T * (1.0f - h.alpha);
@@ -698,6 +722,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     __shared__ float4 s_rec[kRecF4 * kBwdBatch];
     __shared__ float s_part[kBwdBatch][4][kNP];
     __shared__ int s_slot[kBwdBatch];
+    __shared__ int s_gid[kBwdBatch];
     __shared__ int s_toff[kBwdBatch];  // LDS offset of each splat's texel-gradient block (-1: global)
     __shared__ int s_gexp;
     __shared__ unsigned long long s_texq[kTexLds / 2];
@@ -804,7 +829,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             const int j = q >> 3, k = q & 7;
             if (j < nb) s_rec[k * kBwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
         }
-        if (tid < nb) s_slot[tid] = sorted_slots[b0 + tid];
+        if (tid < nb) {
+            s_slot[tid] = sorted_slots[b0 + tid];
+            s_gid[tid] = sorted_ids[b0 + tid];
+        }
         __syncthreads();
         GSTEX_PHASE(0);
         // place the batch's texel blocks in LDS: prefix of h*w*C over the batch, computed by every wave for
@@ -846,7 +874,12 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             const int j = 31 - __builtin_clz(todo);
             todo &= ~(1u << j);
             const int rel = bb * kBwdBatch + j;
-            const Rec r = read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
+#ifndef GSTEX_REC_SLOAD
+#define GSTEX_REC_SLOAD 1
+#endif
+            const Rec r = GSTEX_REC_SLOAD
+                              ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
+                              : read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
             // one predicate for the whole heavy path (a single exec-mask region: the zero rows below are
             // materialised once, not at every divergent exit)
             Hit h;
@@ -1167,7 +1200,16 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
         if (g0 + j < n) {
             const int cnt = nth[g0 + j];
             const float* src = partials + (size_t)offsets[g0 + j] * kNP + c;
-            for (int e = 0; e < cnt; ++e) acc += src[(size_t)e * kNP];
+            // same summation order as a plain loop; 8 row loads in flight per lane
+            int e = 0;
+            for (; e + 8 <= cnt; e += 8) {
+                float r[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) r[u] = src[(size_t)(e + u) * kNP];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += r[u];
+            }
+            for (; e < cnt; ++e) acc += src[(size_t)e * kNP];
         }
         s_sum[j][c] = acc;
     }
