@@ -184,18 +184,23 @@ __global__ __launch_bounds__(256) void place_kernel(int n, const float* __restri
                                                     int tiles_y, int block,
                                                     const int32_t* __restrict__ tile_start,
                                                     const int32_t* __restrict__ rank,
-                                                    unsigned long long* __restrict__ keys) {
+                                                    unsigned long long* __restrict__ keys,
+                                                    int32_t* __restrict__ slot_gid) {
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
                        tiles_y, block);
-    const unsigned long long key =
-        ((unsigned long long)__float_as_uint(depths[g]) << 32) | (unsigned long long)(unsigned)g;
+    // key = depth bits << 32 | emission slot: a splat's slots lie in [offsets[g], offsets[g + 1]) and each
+    // splat has at most one slot per tile, so inside a tile the slot orders exactly as the splat id does
+    // and the sorted key hands over the slot directly (the id comes from slot_gid)
+    const unsigned long long dk = (unsigned long long)__float_as_uint(depths[g]) << 32;
     int e = offsets[g];
     for (int ty = r.y0; ty < r.y1; ++ty)
         for (int tx = r.x0; tx < r.x1; ++tx) {
             int t = ty * tiles_x + tx;
-            keys[tile_start[t] + rank[e++]] = key;
+            keys[tile_start[t] + rank[e]] = dk | (unsigned long long)(unsigned)e;
+            slot_gid[e] = g;
+            ++e;
         }
 }
 
@@ -217,27 +222,23 @@ __device__ __forceinline__ void bitonic_lds(unsigned long long* s, int P) {
     }
 }
 
-__device__ __forceinline__ void write_sorted(int t, int tiles_x, int block, int pos, unsigned long long key,
-                                             const float* centers, const float* extents,
-                                             const int32_t* offsets, int tiles_y, int32_t* sorted_ids,
-                                             int32_t* sorted_slots) {
-    int g = (int)(unsigned)(key & 0xffffffffull);
-    sorted_ids[pos] = g;
-    Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
-                       tiles_y, block);
-    int tx = t % tiles_x, ty = t / tiles_x;
-    sorted_slots[pos] = offsets[g] + (ty - r.y0) * (r.x1 - r.x0) + (tx - r.x0);
+__device__ __forceinline__ void write_sorted(int pos, unsigned long long key, const int32_t* slot_gid,
+                                             int32_t* sorted_ids, int32_t* sorted_slots) {
+    const int slot = (int)(unsigned)(key & 0xffffffffull);
+    sorted_slots[pos] = slot;
+    sorted_ids[pos] = slot_gid[slot];
 }
 
 // 4. one workgroup per tile
+// 4. one workgroup per tile, launched largest bucket first (order[]): the big image-centre buckets no
+//    longer start last and set the kernel's tail
 __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
-    int n_tiles, int tiles_x, int tiles_y, int block, const int32_t* __restrict__ tile_start,
+    int n_tiles, const int32_t* __restrict__ order, const int32_t* __restrict__ tile_start,
     unsigned long long* __restrict__ keys, unsigned long long* __restrict__ scratch,
-    const float* __restrict__ centers, const float* __restrict__ extents,
-    const int32_t* __restrict__ offsets, int32_t* __restrict__ tile_ranges, int32_t* __restrict__ sorted_ids,
+    const int32_t* __restrict__ slot_gid, int32_t* __restrict__ tile_ranges, int32_t* __restrict__ sorted_ids,
     int32_t* __restrict__ sorted_slots) {
     __shared__ unsigned long long s_keys[kSortCap];
-    const int t = blockIdx.x;
+    const int t = order ? order[blockIdx.x] : (int)blockIdx.x;
     const int start = tile_start[t], end = tile_start[t + 1];
     const int K = end - start;
     if (threadIdx.x == 0) {
@@ -253,8 +254,7 @@ __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
         __syncthreads();
         bitonic_lds(s_keys, P);
         for (int i = threadIdx.x; i < K; i += kSortThreads)
-            write_sorted(t, tiles_x, block, start + i, s_keys[i], centers, extents, offsets, tiles_y, sorted_ids,
-                         sorted_slots);
+            write_sorted(start + i, s_keys[i], slot_gid, sorted_ids, sorted_slots);
         return;
     }
     // Large bucket: sort kSortCap-sized chunks in LDS, then merge-path passes in global memory.
@@ -298,8 +298,7 @@ __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
         b_buf = tmp;
     }
     for (int i = threadIdx.x; i < K; i += kSortThreads)
-        write_sorted(t, tiles_x, block, start + i, a_buf[i], centers, extents, offsets, tiles_y, sorted_ids,
-                     sorted_slots);
+        write_sorted(start + i, a_buf[i], slot_gid, sorted_ids, sorted_slots);
 }
 
 // 5. largest-first tile order (LPT list scheduling).  The hardware hands out workgroups in
@@ -317,11 +316,15 @@ constexpr int kRankThreads = 256;
 constexpr int kRankTiles = 64;  // tiles per workgroup; the 4 waves each compare against a quarter of the keys
 constexpr int kRankChunk = 4096;
 
-__device__ __forceinline__ unsigned order_key(const int32_t* tile_ranges, int t) {
-    const unsigned cnt = (unsigned)min((int)kOrderMaxCount, tile_ranges[2 * t + 1] - tile_ranges[2 * t]);
+// bucket size of tile t from tile_ranges (pairs [start, end)) or, STARTS, from the n+1 exclusive-scan starts
+template <bool STARTS>
+__device__ __forceinline__ unsigned order_key(const int32_t* r, int t) {
+    const int c = STARTS ? r[t + 1] - r[t] : r[2 * t + 1] - r[2 * t];
+    const unsigned cnt = (unsigned)min((int)kOrderMaxCount, c);
     return ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
 }
 
+template <bool STARTS>
 __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, const int32_t* __restrict__ tile_ranges,
                                                                  int32_t* __restrict__ tile_order) {
     __shared__ uint4 s_key[kRankChunk / 4];
@@ -329,13 +332,13 @@ __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, co
     unsigned* s_k = reinterpret_cast<unsigned*>(s_key);
     const int part = threadIdx.x >> 6;
     const int t = blockIdx.x * kRankTiles + (threadIdx.x & 63);
-    const unsigned mine = t < n_tiles ? order_key(tile_ranges, t) : 0u;
+    const unsigned mine = t < n_tiles ? order_key<STARTS>(tile_ranges, t) : 0u;
     int rank = 0;
     for (int c0 = 0; c0 < n_tiles; c0 += kRankChunk) {
         const int cn = min(kRankChunk, n_tiles - c0);
         __syncthreads();
         for (int i = threadIdx.x; i < kRankChunk; i += kRankThreads)
-            s_k[i] = i < cn ? order_key(tile_ranges, c0 + i) : ~0u;  // padding never ranks below a key
+            s_k[i] = i < cn ? order_key<STARTS>(tile_ranges, c0 + i) : ~0u;  // padding never ranks below a key
         __syncthreads();
         const int nv = (cn + 3) >> 2;
         const int q0 = (nv * part) >> 2, q1 = (nv * (part + 1)) >> 2;
@@ -362,6 +365,8 @@ struct BinWorkspace {
     int32_t* rank;         // n_isect
     unsigned long long* keys;     // n_isect
     unsigned long long* scratch;  // n_isect
+    int32_t* slot_gid;            // n_isect: splat id of each emission slot
+    int32_t* order;               // n_tiles: tile_sort launch order (largest bucket first)
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -379,6 +384,8 @@ size_t bin_layout(int n_tiles, int64_t n_isect, char* base, BinWorkspace* ws) {
     char* p3 = take((size_t)n_isect * 4);
     char* p4 = take((size_t)n_isect * 8);
     char* p5 = take((size_t)n_isect * 8);
+    char* p6 = take((size_t)n_isect * 4);
+    char* p7 = take((size_t)n_tiles * 4);
     if (ws) {
         ws->tile_count = (int32_t*)p0;
         ws->tile_start = (int32_t*)p1;
@@ -386,6 +393,8 @@ size_t bin_layout(int n_tiles, int64_t n_isect, char* base, BinWorkspace* ws) {
         ws->rank = (int32_t*)p3;
         ws->keys = (unsigned long long*)p4;
         ws->scratch = (unsigned long long*)p5;
+        ws->slot_gid = (int32_t*)p6;
+        ws->order = (int32_t*)p7;
     }
     return off;
 }
@@ -441,10 +450,13 @@ extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, 
     int rc = run_scan(n_tiles, ws.tile_count, ws.tile_start, ws.scan_ws, st);
     if (rc) return rc;
     place_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, depths, offsets, tiles_x, tiles_y, block,
-                                                  ws.tile_start, ws.rank, ws.keys);
-    tile_sort_kernel<<<n_tiles, kSortThreads, 0, st>>>(n_tiles, tiles_x, tiles_y, block, ws.tile_start, ws.keys,
-                                                       ws.scratch, centers, extents, offsets, tile_ranges,
-                                                       sorted_ids, sorted_slots);
+                                                  ws.tile_start, ws.rank, ws.keys, ws.slot_gid);
+    const bool ranked = n_tiles <= kOrderCap;
+    if (ranked)
+        tile_rank_kernel<true><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, st>>>(n_tiles, ws.tile_start, ws.order);
+    tile_sort_kernel<<<n_tiles, kSortThreads, 0, st>>>(n_tiles, ranked ? ws.order : nullptr, ws.tile_start, ws.keys,
+                                                       ws.scratch, ws.slot_gid, tile_ranges, sorted_ids,
+                                                       sorted_slots);
     return launch_status("gstex_bin_sort");
 }
 
@@ -456,7 +468,7 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
         iota_kernel<<<div_up(n_tiles, 256), 256, 0, as_stream(stream)>>>(n_tiles, tile_order);
         return launch_status("gstex_tile_order");
     }
-    tile_rank_kernel<<<div_up(n_tiles, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges,
-                                                                                         tile_order);
+    tile_rank_kernel<false><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges,
+                                                                                                tile_order);
     return launch_status("gstex_tile_order");
 }
