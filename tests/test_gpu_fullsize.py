@@ -1,5 +1,6 @@
-"""Full-size (BASELINE cfg3: 200k splats, 1e7 texels, 800x800) checks through size-independent
-properties, plus the GStex train-step harness.  Needs an MI355X."""
+"""Full-size checks through size-independent properties (BASELINE cfg3: 200k splats, 1e7 texels,
+800x800; cfg5 stand-in: 200k splats, 1e7 texels, 1600x1200 with depth/normal/distortion gradients; cfg2:
+50k splats, 1e6 texels), plus the GStex train-step harness.  Needs an MI355X."""
 import numpy as np
 import pytest
 import torch
@@ -12,10 +13,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(scope="module")
-def cfg3():
-    sc = make_scene(200_000, 1e7, seed=42)
-    v = sphere_view(0, 800, 800).to(DEV)
+def _scene(n, n_texels, H, W, seed):
+    sc = make_scene(n, n_texels, seed=seed)
+    v = sphere_view(0, H, W).to(DEV)
     means, scales, quats, opac = [t.to(DEV) for t in sc.activated()]
     uv0, umap, vmap = [t.to(DEV) for t in sc.uv_mapping()]
     g = torch.Generator().manual_seed(3)
@@ -24,17 +24,47 @@ def cfg3():
                 rgbs=rgbs, tex=sc.texture.to(DEV), dims=sc.texture_dims.to(DEV))
 
 
+@pytest.fixture(scope="module")
+def cfg3():
+    return _scene(200_000, 1e7, 800, 800, 42)
+
+
+@pytest.fixture(scope="module")
+def cfg5():
+    # DTU-like stand-in (the COLMAP init is not available): 1600x1200, 7 500 tiles, geometric outputs used
+    return _scene(200_000, 1e7, 1200, 1600, 24)
+
+
+@pytest.fixture(scope="module")
+def cfg2():
+    return _scene(50_000, 1e6, 800, 800, 7)
+
+
+def _grads(d, ups):
+    """Leaf gradients for upstream gradients `ups` (None = that output unused)."""
+    leaves, _, outs = _render(d)
+    used = [(o, u) for o, u in zip(outs, ups) if u is not None]
+    torch.autograd.backward([o for o, _ in used], [u for _, u in used])
+    return {k: t.grad.detach().double() for k, t in leaves.items()}
+
+
+def _upstream(outs_shapes, which, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(s, generator=g).to(DEV) * 1e-3 if i in which else None for i, s in enumerate(outs_shapes)]
+
+
 def _render(d, requires_grad=True):
     v = d["v"]
+    H, W = v.H, v.W
     leaves = {k: d[k].detach().clone().requires_grad_(requires_grad) for k in ("means", "scales", "quats", "opac",
                                                                               "rgbs", "tex")}
     intr = (v.fx, v.fy, v.cx, v.cy)
     _, depths = ops.project_points(leaves["means"], v.viewmat, intr)
     c, e = ops.get_aabb_2d(leaves["means"], leaves["scales"], 1, leaves["quats"], v.viewmat, intr)
-    nth = ops.get_num_tiles_hit_2d(c, e, 800, 800, 16)
+    nth = ops.get_num_tiles_hit_2d(c, e, H, W, 16)
     outs = ops.texture_gaussians((d["sc"].n, 1, 3), d["dims"], c, e, depths, nth, leaves["rgbs"], leaves["opac"],
                                  leaves["means"], leaves["scales"], 1, leaves["quats"], d["uv0"], d["umap"], d["vmap"],
-                                 leaves["tex"], v.viewmat, v.c2w, v.fx, v.fy, v.cx, v.cy, 800, 800, 16,
+                                 leaves["tex"], v.viewmat, v.c2w, v.fx, v.fy, v.cx, v.cy, H, W, 16,
                                  (1 << 9) | (1 << 10), background=None)
     return leaves, (c, e, depths, nth), outs
 
@@ -103,3 +133,27 @@ def test_train_steps_reduce_loss_and_rechart():
             assert tr.texture_dims.shape == (3000, 3)
             assert abs(tr.texture_dc.shape[0] - old_T) <= 0.01 * old_T
     assert losses[-1] < 0.8 * losses[0], losses
+
+
+PHOTO, GEO = (0, 3, 4), (1, 2, 5)  # (img, alpha, tex) and (depth, reg, normal) output indices
+
+
+@pytest.mark.parametrize("cfg", ["cfg5", "cfg2"])
+def test_fullsize_backward_linear_in_upstream(cfg, request):
+    """The backward is linear in the upstream gradients: grads(photometric + geometric) equal
+    grads(photometric) + grads(geometric) (norm-wise, fp32 summation-order tolerance), and geometric-only
+    upstream gradients give exactly zero colour and texel gradients (GEO kernel variant at full size)."""
+    d = request.getfixturevalue(cfg)
+    _, _, outs = _render(d, requires_grad=False)
+    shapes = [o.shape for o in outs]
+    up_p = _upstream(shapes, PHOTO, 1)
+    up_g = _upstream(shapes, GEO, 2)
+    up_pg = [a if a is not None else b for a, b in zip(up_p, up_g)]
+    gp, gg, gpg = _grads(d, up_p), _grads(d, up_g), _grads(d, up_pg)
+    assert float(gg["rgbs"].abs().max()) == 0.0 and float(gg["tex"].abs().max()) == 0.0
+    assert float(gg["means"].abs().max()) > 0.0 and float(gg["opac"].abs().max()) > 0.0
+    for k in gpg:
+        assert torch.isfinite(gpg[k]).all(), k
+        ref = gp[k] + gg[k]
+        err = float((gpg[k] - ref).norm() / max(float(ref.norm()), 1e-30))
+        assert err < 1e-4, f"{cfg}: {k} not linear in the upstream gradients (rel err {err:.2e})"
