@@ -886,7 +886,14 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
             float P[kNP];
 #pragma unroll
-            for (int i = 0; i < kNP; ++i) P[i] = 0.f;
+            for (int i = 0; i < kNP; i += 2) {
+                // zero rows in 64-bit moves (one v_mov_b64 per register pair; the compiler emits one
+                // v_mov_b32 per register)
+                unsigned long long zz;
+                asm volatile("v_mov_b64 %0, 0" : "=v"(zz));
+                P[i] = __uint_as_float((unsigned)zz);
+                P[i + 1] = __uint_as_float((unsigned)(zz >> 32));
+            }
             // texel-gradient inputs, expanded into the 4*C bilinear contributions after P is reduced:
             // tkey = top-left texel of the block | (i1 - i0) << 29 | (j1 - j0) << 30, -1 if none
             int tkey = -1;
