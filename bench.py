@@ -51,8 +51,8 @@ def pmc_row(kernel):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--n-splats", type=int, default=200_000)
     p.add_argument("--n-texels", type=float, default=1e7)
     p.add_argument("--height", type=int, default=800)
@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-kernel-timing", action="store_true",
+                   help="diagnostics only: no HIP events around the raster launches (no roofline figures)")
     return p.parse_args()
 
 
@@ -161,7 +163,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ops.set_kernel_timing(True)
+    ops.set_kernel_timing(not args.no_kernel_timing)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()

@@ -89,6 +89,10 @@ SIGNATURES = {
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
+    "gstex_raster_setup_bwd_aabb": (
+        c_int32,
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
     "gstex_sh_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_texture_sample": (c_int32, [c_int64, c_int32, _P, _P, c_int64, _P, _P, _P]),

@@ -258,6 +258,20 @@ __device__ __forceinline__ bool aabb_from_homog(const Homog& h, float& cxo, floa
     return true;
 }
 
+// dL/d(AABB centre) -> dL/d(homography rows) through aabb_from_homog's centre (the extents carry no gradient:
+// they only bound the tile lists).  c = (9 (T.x Tw.x + T.y Tw.y) - T.z Tw.z) / d for T = Tu (x) and Tv (y).
+__device__ __forceinline__ void aabb_centre_vjp(const Homog& h, float cx, float cy, float gcx, float gcy, f3& dTu,
+                                                f3& dTv, f3& dTw) {
+    const f3 Tu = h.Tu, Tv = h.Tv, Tw = h.Tw;
+    float d = (kCutoff2 * (Tw.x * Tw.x) + kCutoff2 * (Tw.y * Tw.y)) - Tw.z * Tw.z;
+    float invd = 1.0f / d;
+    dTu = scale3(f3{kCutoff2 * Tw.x, kCutoff2 * Tw.y, -Tw.z}, gcx * invd);
+    dTv = scale3(f3{kCutoff2 * Tw.x, kCutoff2 * Tw.y, -Tw.z}, gcy * invd);
+    f3 dd = f3{2.0f * kCutoff2 * Tw.x, 2.0f * kCutoff2 * Tw.y, -2.0f * Tw.z};
+    dTw = add3(scale3(add3(f3{kCutoff2 * Tu.x, kCutoff2 * Tu.y, -Tu.z}, scale3(dd, -cx)), gcx * invd),
+               scale3(add3(f3{kCutoff2 * Tv.x, kCutoff2 * Tv.y, -Tv.z}, scale3(dd, -cy)), gcy * invd));
+}
+
 // Tile rectangle [x0,x1) x [y0,y1) in tile units (gsplat-0.1 get_tile_bbox convention).
 struct Rect { int x0, x1, y0, y1; };
 

@@ -112,15 +112,8 @@ __global__ __launch_bounds__(kBlock) void aabb_bwd_kernel(int n, const float* __
         v_quats[4 * i + 0] = v_quats[4 * i + 1] = v_quats[4 * i + 2] = v_quats[4 * i + 3] = 0.0f;
         return;
     }
-    const f3 Tu = h.Tu, Tv = h.Tv, Tw = h.Tw;
-    float d = (kCutoff2 * (Tw.x * Tw.x) + kCutoff2 * (Tw.y * Tw.y)) - Tw.z * Tw.z;
-    float invd = 1.0f / d;
-    // c = S/d with S = 9(T.x Tw.x + T.y Tw.y) - T.z Tw.z
-    f3 dTu = scale3(f3{kCutoff2 * Tw.x, kCutoff2 * Tw.y, -Tw.z}, gcx * invd);
-    f3 dTv = scale3(f3{kCutoff2 * Tw.x, kCutoff2 * Tw.y, -Tw.z}, gcy * invd);
-    f3 dd = f3{2.0f * kCutoff2 * Tw.x, 2.0f * kCutoff2 * Tw.y, -2.0f * Tw.z};
-    f3 dTw = add3(scale3(add3(f3{kCutoff2 * Tu.x, kCutoff2 * Tu.y, -Tu.z}, scale3(dd, -cx)), gcx * invd),
-                  scale3(add3(f3{kCutoff2 * Tv.x, kCutoff2 * Tv.y, -Tv.z}, scale3(dd, -cy)), gcy * invd));
+    f3 dTu, dTv, dTw;
+    aabb_centre_vjp(h, cx, cy, gcx, gcy, dTu, dTv, dTw);
     HomogGrad g = splat_homography_vjp(cam, su, sv, fr, dTu, dTv, dTw);
     float dq[4];
     frame_vjp(fr, g.dtu, g.dtv, f3{0.0f, 0.0f, 0.0f}, dq);

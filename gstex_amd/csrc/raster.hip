@@ -1188,6 +1188,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 // setup backward: sum partials per splat, chain to parameters
 // ------------------------------------------------------------------------------------------
 constexpr int kSetupBwdSplats = 256 / kNP;  // 10 splats x 24 partial columns per 256-thread workgroup
+// FOLD_AABB: the centres were produced by get_aabb_2d from these same means / scales / quats (training
+// path), so the AABB-centre chain (aabb_bwd_kernel's arithmetic) is applied here and added in, instead of
+// a separate launch plus autograd's accumulation kernels; the sums are the same two terms added once.
+template <bool FOLD_AABB>
 __global__ __launch_bounds__(256) void setup_bwd_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
@@ -1261,11 +1265,35 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     f3 dtw = f3{sgn * S[P_NRM], sgn * S[P_NRM + 1], sgn * S[P_NRM + 2]};
     float dq[4];
     frame_vjp(fr, dtu, dtv, dtw, dq);
-    v_means[3 * g + 0] = hg.dmu.x;
-    v_means[3 * g + 1] = hg.dmu.y;
-    v_means[3 * g + 2] = hg.dmu.z;
-    v_scales[3 * g + 0] = dsu * glob;
-    v_scales[3 * g + 1] = dsv * glob;
+    f3 vmu = hg.dmu;
+    float vsu = dsu * glob, vsv = dsv * glob;
+    if (FOLD_AABB) {
+        // aabb_bwd_kernel for this splat (zero when there is no centre gradient or the splat is culled)
+        f3 amu = f3{0.f, 0.f, 0.f};
+        float asu = 0.f, asv = 0.f, aq[4] = {0.f, 0.f, 0.f, 0.f};
+        const float gcx = S[P_XY + 0], gcy = S[P_XY + 1];
+        float acx, acy, aex, aey;
+        const Homog ah = splat_homography(cam, mu, su, sv, fr);
+        if (!(gcx == 0.0f && gcy == 0.0f) && aabb_from_homog(ah, acx, acy, aex, aey)) {
+            f3 dTu, dTv, dTw;
+            aabb_centre_vjp(ah, acx, acy, gcx, gcy, dTu, dTv, dTw);
+            const HomogGrad ag = splat_homography_vjp(cam, su, sv, fr, dTu, dTv, dTw);
+            frame_vjp(fr, ag.dtu, ag.dtv, f3{0.0f, 0.0f, 0.0f}, aq);
+            amu = ag.dmu;
+            asu = ag.dsu * glob;
+            asv = ag.dsv * glob;
+        }
+        vmu = add3(vmu, amu);
+        vsu = vsu + asu;
+        vsv = vsv + asv;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dq[k] = dq[k] + aq[k];
+    }
+    v_means[3 * g + 0] = vmu.x;
+    v_means[3 * g + 1] = vmu.y;
+    v_means[3 * g + 2] = vmu.z;
+    v_scales[3 * g + 0] = vsu;
+    v_scales[3 * g + 1] = vsv;
     v_scales[3 * g + 2] = 0.f;
     v_quats[4 * g + 0] = dq[0];
     v_quats[4 * g + 1] = dq[1];
@@ -1459,10 +1487,28 @@ extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float
     GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd: null pointer");
-    setup_bwd_kernel<<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
+    setup_bwd_kernel<false><<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
         n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
         v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     return launch_status("gstex_raster_setup_bwd");
+}
+
+extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
+                                           const float* quats, const float* opacities, const float* umap,
+                                           const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
+                                           const float* partials, const gstex_camera* cam, float* v_means,
+                                           float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities,
+                                           float* v_centers, float* v_uv0, void* stream) {
+    (void)opacities;
+    GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup_bwd_aabb: invalid arguments");
+    if (n == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
+                      v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
+                  "gstex_raster_setup_bwd_aabb: null pointer");
+    setup_bwd_kernel<true><<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
+        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
+        v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+    return launch_status("gstex_raster_setup_bwd_aabb");
 }
 
 extern "C" int gstex_texture_edit(const gstex_camera* cam, int32_t settings, const float* records,

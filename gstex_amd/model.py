@@ -185,7 +185,7 @@ class GStexTrainer:
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
             ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
-            texture_transform=(SH_C0, 0.5))
+            texture_transform=(SH_C0, 0.5), fold_aabb=True)  # centers come from get_aabb_2d just above
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],

@@ -23,10 +23,16 @@ BLOCK_WIDTH = 16
 _TIMING: dict | None = None
 
 
-def set_kernel_timing(enabled: bool) -> None:
-    """Record a HIP event pair around every timed C-ABI launch (bench.py / profiling only)."""
-    global _TIMING
+_TIMED = {"gstex_raster_fwd", "gstex_raster_bwd"}  # the roofline kernels; each event pair costs ~3 us of stream time
+
+
+def set_kernel_timing(enabled: bool, names=None) -> None:
+    """Record a HIP event pair around the raster forward / backward launches (or the C-ABI entry points in
+    `names`) on the stream they run on (bench.py / profiling only)."""
+    global _TIMING, _TIMED
     _TIMING = {} if enabled else None
+    if names is not None:
+        _TIMED = set(names)
 
 
 def kernel_times() -> dict:
@@ -38,7 +44,7 @@ def kernel_times() -> dict:
 
 
 def _launch(name: str, *args) -> None:
-    if _TIMING is None:
+    if _TIMING is None or name not in _TIMED:
         call(name, *args)
         return
     a = torch.cuda.Event(enable_timing=True)
@@ -122,6 +128,10 @@ class _ProjectPoints(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, v_xys, v_depths):
+        if v_xys is None and v_depths is None:
+            # reached with no upstream gradient (texture_gaussians uses depths only as sort keys): the
+            # gradient is exactly zero, so none is returned (no kernel, no accumulation into means.grad)
+            return None, None, None, None, None, None
         means, vm = ctx.saved_tensors
         n = means.shape[0]
         v_means = torch.empty_like(means)
@@ -198,38 +208,57 @@ def get_num_tiles_hit_2d(centers, extents, H: int, W: int, block_width: int) -> 
 _PINNED = {}
 
 
-def _read_count(x: torch.Tensor) -> int:
-    """Host value of a non-negative int32 device scalar, stream-ordered.  The value is copied into a pinned
-    host word preset to -1 and the host polls that word, which returns as soon as the copy lands instead of
-    after a blocking stream synchronisation's wake-up (~50 us of idle GPU per step, measured).  After 50 ms
-    without the copy it falls back to a real synchronisation (which raises any pending device error)."""
+def _start_count(x: torch.Tensor):
+    """Queue the copy of a non-negative int32 device scalar into a pinned host word preset to -1 (stream-ordered);
+    _finish_count polls that word.  Work queued between the two calls runs on the device while the host waits
+    and then sizes buffers from the value, instead of the device idling through that host time."""
     buf = _PINNED.get(x.device)
     if buf is None:
         buf = _PINNED[x.device] = torch.empty((1,), dtype=torch.int32, pin_memory=True)
     host = buf.numpy()
     host[0] = -1
     buf.copy_(x.reshape(1), non_blocking=True)
+    return host, x.device
+
+
+def _finish_count(pending) -> int:
+    """Host value of a _start_count copy: polls the pinned word, which returns as soon as the copy lands instead
+    of after a blocking stream synchronisation's wake-up (~50 us of idle GPU per step, measured).  After 50 ms
+    without the copy it falls back to a real synchronisation (which raises any pending device error)."""
+    host, dev = pending
     deadline = None
     while host[0] < 0:
         if deadline is None:
             deadline = time.perf_counter() + 0.05
         elif time.perf_counter() > deadline:
-            torch.cuda.current_stream(x.device).synchronize()
+            torch.cuda.current_stream(dev).synchronize()
             break
     return int(host[0])
 
 
-def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_width: int = BLOCK_WIDTH):
-    """Tile binning + per-tile depth sort.  Returns (offsets (N+1,), tile_ranges (n_tiles,2),
-    sorted_ids (I,), sorted_slots (I,)), all int32.  One host sync to size the I-length buffers."""
-    n = centers.shape[0]
-    dev = centers.device
-    st = _stream(centers)
+def _read_count(x: torch.Tensor) -> int:
+    return _finish_count(_start_count(x))
+
+
+def bin_begin(num_tiles_hit):
+    """First half of bin_and_sort: the offsets scan and the asynchronous read of the pair count."""
+    n = num_tiles_hit.shape[0]
+    dev = num_tiles_hit.device
     nth = _i32(num_tiles_hit, "num_tiles_hit", (n,))
     offsets = torch.empty((n + 1,), device=dev, dtype=torch.int32)
     ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=dev, dtype=torch.uint8)
-    call("gstex_scan_offsets", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), st)
-    n_isect = _read_count(offsets[n]) if offsets.is_cuda else int(offsets[n].item())
+    call("gstex_scan_offsets", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), _stream(nth))
+    pending = _start_count(offsets[n]) if offsets.is_cuda else int(offsets[n].item())
+    return nth, offsets, pending
+
+
+def bin_finish(begun, centers, extents, depths, H: int, W: int, block_width: int = BLOCK_WIDTH):
+    """Second half of bin_and_sort: wait for the pair count, size the pair buffers, bin and sort."""
+    nth, offsets, pending = begun
+    n = nth.shape[0]
+    dev = nth.device
+    st = _stream(nth)
+    n_isect = pending if isinstance(pending, int) else _finish_count(pending)
     tiles_x = (W + block_width - 1) // block_width
     tiles_y = (H + block_width - 1) // block_width
     n_tiles = tiles_x * tiles_y
@@ -242,6 +271,14 @@ def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_
          ptr(depths.detach().contiguous()), ptr(nth), ptr(offsets), int(H), int(W), int(block_width),
          ptr(tile_ranges), ptr(sorted_ids), ptr(sorted_slots), ptr(bws), bws.numel(), st)
     return offsets, tile_ranges, sorted_ids, sorted_slots
+
+
+def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_width: int = BLOCK_WIDTH):
+    """Tile binning + per-tile depth sort.  Returns (offsets (N+1,), tile_ranges (n_tiles,2),
+    sorted_ids (I,), sorted_slots (I,)), all int32.  One host read of the pair count I to size the I-length
+    buffers."""
+    _i32(num_tiles_hit, "num_tiles_hit", (centers.shape[0],))
+    return bin_finish(bin_begin(num_tiles_hit), centers, extents, depths, H, W, block_width)
 
 
 def tile_order(tile_ranges: torch.Tensor) -> torch.Tensor:
@@ -259,7 +296,7 @@ class _TextureGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
-                block_width, settings, background, texture_transform=None):
+                block_width, settings, background, texture_transform=None, fold_aabb=False):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -288,13 +325,18 @@ class _TextureGaussians(torch.autograd.Function):
         st = _stream(means)
         cam = _lib.make_camera(vm, cw, fx, fy, cx, cy, H, W, BLOCK_WIDTH)
 
-        offsets, tile_ranges, sorted_ids, sorted_slots = bin_and_sort(
-            centers_c.detach(), extents_c, depths_c, nth, H, W, BLOCK_WIDTH)
-        order = tile_order(tile_ranges)
+        # the pair count is read to the host once; work that does not depend on the tile lists is queued
+        # between the copy and the wait, so the device runs it while the host waits and sizes the pair
+        # buffers: the splat records and the zeroed texel-gradient buffer of the backward
+        begun = bin_begin(nth)
         records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
              ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
              st)
+        ctx.v_texture = torch.zeros_like(texture) if ctx.needs_input_grad[15] else None
+        offsets, tile_ranges, sorted_ids, sorted_slots = bin_finish(begun, centers_c.detach(), extents_c, depths_c,
+                                                                    H, W, BLOCK_WIDTH)
+        order = tile_order(tile_ranges)
         ctx_scale, ctx_bias = (1.0, 0.0) if texture_transform is None else (float(texture_transform[0]),
                                                                              float(texture_transform[1]))
         f = dict(device=dev, dtype=torch.float32)
@@ -317,6 +359,7 @@ class _TextureGaussians(torch.autograd.Function):
         ctx.has_bg = bg is not None
         ctx.args = (float(glob_scale), float(fx), float(fy), float(cx), float(cy), H, W, C, int(settings))
         ctx.tex_affine = (ctx_scale, ctx_bias)
+        ctx.fold_aabb = bool(fold_aabb)
         ctx.set_materialize_grads(False)  # unused outputs' gradients stay None (no zero tensors)
         return img, depth, reg, alpha, tex, normal
 
@@ -343,7 +386,8 @@ class _TextureGaussians(torch.autograd.Function):
         v_normal = g(v_normal, (H, W, 3))
         n_isect = sorted_ids.shape[0]
         partials = torch.empty((n_isect, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
-        v_texture = torch.zeros_like(texture)
+        v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
+        ctx.v_texture = None
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0], ctx.tex_affine[1],
              ptr(state), ptr(v_img), ptr(v_depth),
@@ -355,24 +399,32 @@ class _TextureGaussians(torch.autograd.Function):
         v_opac = torch.empty((n, 1), device=dev, dtype=torch.float32)
         v_centers = torch.empty((n, 2), device=dev, dtype=torch.float32)
         v_uv0 = torch.empty((n, 1, 2), device=dev, dtype=torch.float32)
-        _launch("gstex_raster_setup_bwd", n, ptr(means), ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap),
+        _launch("gstex_raster_setup_bwd_aabb" if ctx.fold_aabb else "gstex_raster_setup_bwd", n, ptr(means), ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap),
              ptr(vmap), ptr(nth), ptr(offsets), ptr(partials), cam, ptr(v_means), ptr(v_scales), ptr(v_quats),
              ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
         v_bg = None
         if ctx.needs_input_grad[26]:
             v_bg = (v_img * state[..., 0:1]).sum((0, 1)) if v_img is not None else torch.zeros_like(bg)
+        if ctx.fold_aabb:
+            v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
-                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None)
+                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
-                      block_width, settings, background=None, use_torch_impl=False, texture_transform=None):
+                      block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
+                      fold_aabb=False):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
     texel values s * texture + b, so SH2RGB(texture_dc) (gstex.py:1119) need not be materialised: pass
     texture_dc with (0.28209479177387814, 0.5); the texture gradient is then w.r.t. the stored values.
+
+    fold_aabb=True (not in the reference API; training path only) declares that `centers` came from
+    get_aabb_2d(means, scales, glob_scale, quats, viewmat, (fx, fy, cx, cy)): the backward then chains the centre
+    gradient through the AABB itself (gstex_raster_setup_bwd_aabb) and returns none for `centers`, so neither
+    get_aabb_2d's backward nor autograd's accumulation kernels run.  Same gradients, bit for bit.
 
     Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
     Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
@@ -384,7 +436,8 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
             "the CPU restatement in oracle/ is test infrastructure only")
     return _TextureGaussians.apply(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs,
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
-                                   c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform)
+                                   c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
+                                   fold_aabb)
 
 
 rasterize_gaussians = texture_gaussians  # north_star name

@@ -153,6 +153,17 @@ int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, f
                            const gstex_camera* cam, float* v_means, float* v_scales,
                            float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                            float* v_uv0, void* stream);
+/* gstex_raster_setup_bwd with gstex_aabb_2d_bwd folded in: for callers whose centres came from
+ * gstex_aabb_2d on these same means / scales / quats (glob_scale, camera), the centre gradient is chained
+ * through the AABB centre here and added to v_means / v_scales / v_quats (bit-identical to running
+ * gstex_aabb_2d_bwd separately and adding the two results); v_centers is still written. */
+int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
+                                const float* quats, const float* opacities, const float* umap,
+                                const float* vmap, const int32_t* num_tiles_hit,
+                                const int32_t* offsets, const float* partials,
+                                const gstex_camera* cam, float* v_means, float* v_scales,
+                                float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
+                                float* v_uv0, void* stream);
 
 /* ---- spherical harmonics (degree <= 4) ------------------------------------------------- */
 int gstex_sh_fwd(int32_t n, int32_t degree, int32_t n_coeffs, const float* viewdirs,

@@ -480,3 +480,38 @@ def test_fused_activations_match_eager_trainer():
             continue
         err = float((pf.grad - pe.grad).norm() / pe.grad.norm().clamp(min=1e-30))
         assert err < 1e-4, f"{name}: rel err {err:.2e}"
+
+
+# ---------------------------------------------------------------- folded AABB-centre chain (training path)
+def test_fold_aabb_gradients_bit_identical():
+    """texture_gaussians(fold_aabb=True) chains the centre gradient through get_aabb_2d inside the raster's
+    setup backward: means / scales / quats gradients are bit-identical to the separate get_aabb_2d backward
+    plus autograd's accumulation."""
+    import gstex_cuda
+
+    case = make_case(n=600, n_texels=30000, H=72, W=88, seed=21)
+    v, inp = case.view, case.inp
+    intr = (v.fx, v.fy, v.cx, v.cy)
+    dv = lambda t: t.detach().to(DEV).contiguous()  # noqa: E731
+    up = upstream(inp.cam.H, inp.cam.W, case.C, 8)
+    res = []
+    for fold in (False, True):
+        leaves = {k: dv(getattr(inp, k)).requires_grad_(True) for k in ("means", "scales", "quats", "rgbs",
+                                                                          "opacities", "texture", "uv0")}
+        c, e = gstex_cuda.get_aabb_2d(leaves["means"], leaves["scales"], inp.glob_scale, leaves["quats"],
+                                      dv(v.viewmat), intr)
+        _, depths = gstex_cuda.project_points(leaves["means"], dv(v.viewmat), intr)
+        nth = gstex_cuda.get_num_tiles_hit_2d(c, e, inp.cam.H, inp.cam.W, 16)
+        outs = gstex_cuda.texture_gaussians(
+            (inp.means.shape[0], 1, case.C), dv(inp.texture_dims), c, e, depths, nth, leaves["rgbs"],
+            leaves["opacities"], leaves["means"], leaves["scales"], inp.glob_scale, leaves["quats"], leaves["uv0"],
+            dv(inp.umap), dv(inp.vmap), leaves["texture"], dv(v.viewmat), dv(v.c2w), v.fx, v.fy, v.cx, v.cy,
+            inp.cam.H, inp.cam.W, 16, inp.settings, fold_aabb=fold)
+        names = ["img", "depth", "reg", "alpha", "tex", "normal"]
+        torch.autograd.backward(list(outs), [up[k].to(DEV) for k in names])
+        res.append({k: t.grad.detach().cpu() for k, t in leaves.items()})
+    for k in ("means", "scales", "quats", "rgbs", "opacities", "uv0"):
+        assert torch.equal(res[0][k], res[1][k]), f"{k}: folded AABB chain differs"
+    # texel gradients combine tiles with float atomics (order-dependent rounding), unaffected by the fold
+    assert grad_norm_err(res[1]["texture"], res[0]["texture"]) < 1e-6
+    assert float(res[0]["means"].abs().max()) > 0

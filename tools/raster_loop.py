@@ -55,7 +55,8 @@ def main():
 
     nth = run()
     torch.cuda.synchronize()
-    ops.set_kernel_timing(True)
+    ops.set_kernel_timing(True, names={"gstex_bin_sort", "gstex_raster_setup", "gstex_raster_fwd", "gstex_raster_bwd",
+                                      "gstex_raster_setup_bwd", "gstex_raster_setup_bwd_aabb"})
     t0 = time.perf_counter()
     for _ in range(args.iters):
         run()
