@@ -238,6 +238,13 @@ __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
     return r;
 }
 
+// Visit-mask layout: tile t owns 64-bit words [ceil(start_t / 64) + t, + ceil(len_t / 64)) (disjoint across tiles);
+// word i holds, for each of the 4 waves (interleaved: word * 4 + wave), one bit per tile-list position
+// 64 i .. 64 i + 63: the forward's per-wave cull (the splat's contribution region meets the wave's block).
+__host__ __device__ __forceinline__ size_t visit_mask_base(int start, int tile) {
+    return (size_t)((start + 63) / 64) + (size_t)tile;
+}
+
 // The same record read from global memory at a wave-uniform address: scalar loads straight into SGPRs
 // (no LDS read, no v_readfirstlane per value).
 __device__ __forceinline__ Rec read_rec_global(const float4* __restrict__ rec) {
@@ -460,7 +467,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float tex_scale, float tex_bias,
     float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
-    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state) {
+    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state,
+    unsigned long long* __restrict__ visit_masks) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
@@ -487,6 +495,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     float D = 0.f, M1 = 0.f, M2 = 0.f, reg = 0.f;
     int last = -1;
     bool done = !inside;
+    const int lane = tid & 63, wave = tid >> 6;
+    const size_t vm_base = visit_mask_base(rng.x, tile);
 
     for (int b0 = rng.x; b0 < rng.y; b0 += kFwdBatch) {
         if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
@@ -498,12 +508,14 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
         __syncthreads();
         const int nb = min(kFwdBatch, rng.y - b0);
         // the batch splats whose contribution box meets this wave's 16x4 block, tested all at once
-        const int lane = tid & 63;
         unsigned long long todo[kFwdBatch / 64];
 #pragma unroll
         for (int hb = 0; hb < kFwdBatch / 64; ++hb) {
             const int jj = hb * 64 + lane;
             todo[hb] = __ballot(jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa));
+            // hand the cull to the backward, which visits these splats up to the wave's last contributor
+            if (visit_masks && lane == 0 && hb * 64 < nb)
+                visit_masks[(vm_base + ((b0 - rng.x) >> 6) + hb) * 4 + wave] = todo[hb];
         }
         for (int hb = 0; hb < kFwdBatch / 64 && !done; ++hb) {
           unsigned long long m = todo[hb];
@@ -514,9 +526,11 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             const Rec r = GSTEX_FWD_SLOAD ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
                                          : read_rec<kFwdBatch>(s_rec, j);
             Hit h;
-            if (!eval_hit(r, px, py, aa, h)) continue;
+            const bool ok = eval_hit(r, px, py, aa, h);
             const float test_T = T * (1.0f - h.alpha);
-            if (test_T < kTMin) {
+            const bool stop = ok && test_T < kTMin;
+            if (!ok) continue;
+            if (stop) {
                 done = true;
                 break;
             }
@@ -715,7 +729,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
-    float* __restrict__ v_texture) {
+    float* __restrict__ v_texture, const unsigned long long* __restrict__ visit_masks) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
@@ -809,6 +823,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     }
     // texel-gradient contributions are formed directly in the fixed-point scale
     const float tex_scale_q = GSTEX_TEX_FIXED ? __builtin_ldexpf(tex_scale, tex_S) : tex_scale;
+    const size_t vm_base = visit_mask_base(rng.x, tile);
     int wave_last = last;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wave_last = max(wave_last, __shfl_xor(wave_last, o, 64));
@@ -862,7 +877,14 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         // the batch splats this wave must visit, tested all at once (lane j <-> splat j): some lane
         // of the wave reaches it (rel <= last) and its contribution box meets the wave's 16x4 block
         unsigned todo;
-        {
+        if (visit_masks) {
+            // the forward's cull bits for this wave (one wave-uniform word), clipped to its last contributor
+            const int pos = bb * kBwdBatch;
+            const unsigned long long vw = visit_masks[(vm_base + (pos >> 6)) * 4 + wave];
+            const int lim = min(nb, wave_last - pos + 1);
+            const unsigned keep = lim <= 0 ? 0u : (lim >= 32 ? ~0u : (1u << lim) - 1u);
+            todo = (unsigned)(vw >> (pos & 63)) & ((1u << kBwdBatch) - 1u) & keep;
+        } else {
             const bool need = lane < nb && bb * kBwdBatch + lane <= wave_last &&
                               wave_may_hit<kBwdBatch>(s_rec, lane < nb ? lane : 0, wx0, wx1, wy0, wy1, aa);
             todo = (unsigned)__ballot(need);
@@ -1411,7 +1433,7 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
                                 const float* background, const float* records, const int32_t* tile_ranges,
                                 const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                                 int64_t n_texels, float tex_scale, float tex_bias, float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
-                                float* out_normal, float* state, void* stream) {
+                                float* out_normal, float* state, uint64_t* visit_masks, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_fwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_fwd: channels must be in [1, 8] (got %d)",
@@ -1430,7 +1452,8 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
                                                      (const float4*)records, (const int2*)tile_ranges,        \
                                                      tile_order, sorted_ids, texture, tex_scale, tex_bias, out_img,       \
                                                      out_depth, out_reg,                                                  \
-                                                     out_alpha, out_tex, out_normal, (float4*)state)
+                                                     out_alpha, out_tex, out_normal, (float4*)state,                  \
+                                                     (unsigned long long*)visit_masks)
     if (channels == 3) GSTEX_FWD(3);
     else if (channels == 6) GSTEX_FWD(6);
     else GSTEX_FWD(0);
@@ -1444,7 +1467,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
                                 const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
                                 const float* state, const float* v_img,
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
-                                const float* v_normal, float* partials, float* v_texture, void* stream) {
+                                const float* v_normal, float* partials, float* v_texture,
+                                const uint64_t* visit_masks, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
@@ -1464,7 +1488,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         tile_order, sorted_ids, sorted_slots, texture, tex_scale, tex_bias, (const float4*)state, v_img, v_depth,      \
         v_reg, v_alpha, v_tex,                                                                                  \
-        v_normal, partials, v_texture)
+        v_normal, partials, v_texture, (const unsigned long long*)visit_masks)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
     else if (channels == 3) GSTEX_BWD(3, true);
     else if (channels == 6 && !geo) GSTEX_BWD(6, false);
@@ -1473,6 +1497,11 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     else GSTEX_BWD(0, true);
 #undef GSTEX_BWD
     return launch_status("gstex_raster_bwd");
+}
+
+extern "C" size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles) {
+    if (n_isect < 0 || n_tiles < 0) return 0;
+    return ((size_t)((n_isect + 63) / 64) + (size_t)n_tiles + 1) * 4;
 }
 
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,

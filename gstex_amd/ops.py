@@ -347,11 +347,18 @@ class _TextureGaussians(torch.autograd.Function):
         tex = torch.empty((H, W, C), **f)
         normal = torch.empty((H, W, 3), **f)
         state = torch.empty((H, W, 4), **f)
+        # per (tile, wave, splat) "some pixel of the wave received a contribution" bits for the backward
+        needs_bwd = any(ctx.needs_input_grad)
+        vmask = None
+        if needs_bwd:
+            words = int(_lib.load().gstex_visit_mask_words(sorted_ids.shape[0], tile_ranges.shape[0]))
+            vmask = torch.empty((words,), device=dev, dtype=torch.int64)
         _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
              ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), ptr(depth), ptr(reg), ptr(alpha),
              ptr(tex), ptr(normal),
-             ptr(state), st)
+             ptr(state), ptr(vmask), st)
+        ctx.vmask = vmask
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
                               bg if bg is not None else vm)
@@ -391,7 +398,8 @@ class _TextureGaussians(torch.autograd.Function):
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0], ctx.tex_affine[1],
              ptr(state), ptr(v_img), ptr(v_depth),
-             ptr(v_reg), ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), st)
+             ptr(v_reg), ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), ptr(ctx.vmask), st)
+        ctx.vmask = None
         v_means = torch.empty_like(means)
         v_scales = torch.empty_like(scales)
         v_quats = torch.empty_like(quats)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 3
+#define GSTEX_ABI_VERSION 4
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -132,7 +132,12 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                      int64_t n_texels, float tex_scale, float tex_bias,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
-                     float* out_tex, float* out_normal, float* state, void* stream);
+                     float* out_tex, float* out_normal, float* state, uint64_t* visit_masks, void* stream);
+/* visit_masks (ABI 4; NULL = not recorded / not used): gstex_visit_mask_words(n_isect, n_tiles) 64-bit
+ * words in which the forward records its per-wave cull (per tile, wave of 64 pixels and tile-list
+ * position: can the splat reach alpha >= 1/255 in that wave's 8x8 block); the backward reads them instead
+ * of re-running the geometric test.  Pass the same buffer to both. */
+size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles);
 /* Backward composite. Needs the forward state and the same tile_order. Any of v_img ... v_normal may be
  * NULL (that output's gradient is zero). Writes
  * partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of every (tile, splat) pair and
@@ -144,7 +149,8 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      float tex_scale, float tex_bias, const float* state, const float* v_img,
                      const float* v_depth,
                      const float* v_reg, const float* v_alpha, const float* v_tex,
-                     const float* v_normal, float* partials, float* v_texture, void* stream);
+                     const float* v_normal, float* partials, float* v_texture,
+                     const uint64_t* visit_masks, void* stream);
 /* Sums each splat's partials and chains them to the splat parameters. Outputs are overwritten. */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                            const float* quats, const float* opacities, const float* umap,

@@ -37,7 +37,7 @@ def test_every_header_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.gstex_abi_version() == 3
+    assert lib.gstex_abi_version() == 4
 
 
 def test_workspace_size_queries(lib):
@@ -67,15 +67,21 @@ def test_bin_sort_rejects_non16_block(lib):
 def test_raster_rejects_bad_channels_and_settings(lib):
     cam = _cam()
     rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 9, 0, None, None, None, None, None, None, 0, 1.0,
-                      0.0, None, None, None, None, None, None, None, None)
+                      0.0, None, None, None, None, None, None, None, None, None)
     assert rc == 1 and "channels" in msg
     rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 3, 1 << 2, None, None, None, None, None, None, 0,
-                      1.0, 0.0, None, None, None, None, None, None, None, None)
+                      1.0, 0.0, None, None, None, None, None, None, None, None, None)
     assert rc == 3 and "unsupported settings" in msg
     bad = _cam(block=8)
     rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, None, 0,
-                      1.0, 0.0, None, None, None, None, None, None, None, None, None, None)
+                      1.0, 0.0, None, None, None, None, None, None, None, None, None, None, None)
     assert rc == 1 and "block_width" in msg
+
+
+def test_visit_mask_words(lib):
+    # per tile ceil-aligned runs of 64-bit words, 4 waves interleaved: (ceil(I / 64) + n_tiles + 1) * 4
+    assert lib.gstex_visit_mask_words(0, 1) == 8
+    assert lib.gstex_visit_mask_words(1_915_389, 2500) == ((1_915_389 + 63) // 64 + 2501) * 4
 
 
 def test_sh_rejects_degree(lib):
