@@ -655,9 +655,6 @@ __device__ __forceinline__ float dpp_shr_f(float v) {
 #ifndef GSTEX_SEG_FMA
 #define GSTEX_SEG_FMA 1
 #endif
-#ifndef GSTEX_FLUSH_WAVE
-#define GSTEX_FLUSH_WAVE 1  // flush staged texel gradients splat-major, one wave per splat block
-#endif
 // v += row_shr:OFF(v) * mf, mf = 1 where the lane OFF to the left is in the same segment, else 0: one
 // v_fmac_f32 with a DPP source per value (the compiler does not fold a DPP move into the tied-accumulator
 // fmac, so it is written out).  fma(t, 1, v) rounds as t + v and fma(t, 0, v) = v, so the result equals the
@@ -735,9 +732,6 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     const int Cn = (C > 0) ? C : Cdyn;
     __shared__ float4 s_rec[kRecF4 * kBwdBatch];
     __shared__ float s_part[kBwdBatch][4][kNP];
-    __shared__ int s_slot[kBwdBatch];
-    __shared__ int s_gid[kBwdBatch];
-    __shared__ int s_toff[kBwdBatch];  // LDS offset of each splat's texel-gradient block (-1: global)
     __shared__ int s_gexp;
     __shared__ unsigned long long s_texq[kTexLds / 2];
     float* s_tex = reinterpret_cast<float*>(s_texq);  // float staging (GSTEX_TEX_FIXED = 0)
@@ -836,30 +830,46 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         for (int k = 0; k < kNP / 4; ++k) dst[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
+    // Batch metadata lives in registers, lane j <-> splat j of the batch: splat id, emission slot and texel
+    // block (h, w, off: plane 6 of the record).  The next batch's ids and slots are loaded at the start of a
+    // batch and its block dims after the visits, so with the forward's cull bits (visit_masks) a batch needs
+    // no LDS staging and no barrier before its visits.
+    int cur_gid = 0, cur_slot = 0;
+    float4 cur_dims = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tile_last >= 0) {
+        const int bb0 = tile_last / kBwdBatch;
+        if (lane < min(kBwdBatch, tile_last - bb0 * kBwdBatch + 1)) {
+            cur_gid = sorted_ids[rng.x + bb0 * kBwdBatch + lane];
+            cur_slot = sorted_slots[rng.x + bb0 * kBwdBatch + lane];
+            cur_dims = records[(size_t)cur_gid * kRecF4 + 6];
+        }
+    }
+
     GSTEX_PHASE(6);
     for (int bb = tile_last / kBwdBatch; bb >= 0 && tile_last >= 0; --bb) {
         const int b0 = rng.x + bb * kBwdBatch;
         const int nb = min(kBwdBatch, tile_last - bb * kBwdBatch + 1);
-        for (int q = tid; q < kBwdBatch * kRecF4; q += kThreads) {
-            const int j = q >> 3, k = q & 7;
-            if (j < nb) s_rec[k * kBwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+        if (!visit_masks) {  // the backward's own cull reads the batch records from LDS
+            for (int q = tid; q < kBwdBatch * kRecF4; q += kThreads) {
+                const int j = q >> 3, k = q & 7;
+                if (j < nb) s_rec[k * kBwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+            }
+            __syncthreads();
         }
-        if (tid < nb) {
-            s_slot[tid] = sorted_slots[b0 + tid];
-            s_gid[tid] = sorted_ids[b0 + tid];
+        // next batch (always a full one below the top batch): ids and slots now, block dims after the visits
+        int nx_gid = 0, nx_slot = 0;
+        if (bb > 0 && lane < kBwdBatch) {
+            nx_gid = sorted_ids[b0 - kBwdBatch + lane];
+            nx_slot = sorted_slots[b0 - kBwdBatch + lane];
         }
-        __syncthreads();
         GSTEX_PHASE(0);
         // place the batch's texel blocks in LDS: prefix of h*w*C over the batch, computed by every wave for
         // itself (lane j <-> splat j; no extra barrier); splats past the capacity accumulate straight into
         // global memory
-        int my_toff, nfit, used;
+        int my_toff, nfit;
         {
             int sz = 0;
-            if (lane < nb) {
-                const float4 q = s_rec[6 * kBwdBatch + lane];
-                sz = __float_as_int(q.x) * __float_as_int(q.y) * Cn;
-            }
+            if (lane < nb) sz = __float_as_int(cur_dims.x) * __float_as_int(cur_dims.y) * Cn;
             int incl = sz;
 #pragma unroll
             for (int o = 1; o < kBwdBatch; o <<= 1) {
@@ -870,8 +880,6 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             my_toff = (lane < nb && fits) ? incl - sz : -1;
             const unsigned long long fm = __ballot(fits && lane < nb);
             nfit = __popcll(fm);
-            used = nfit > 0 ? __builtin_amdgcn_readlane(incl, nfit - 1) : 0;
-            if (!GSTEX_FLUSH_WAVE && wave == 0 && lane < kBwdBatch) s_toff[lane] = my_toff;
         }
 
         // the batch splats this wave must visit, tested all at once (lane j <-> splat j): some lane
@@ -896,12 +904,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             const int j = 31 - __builtin_clz(todo);
             todo &= ~(1u << j);
             const int rel = bb * kBwdBatch + j;
-#ifndef GSTEX_REC_SLOAD
-#define GSTEX_REC_SLOAD 1
-#endif
-            const Rec r = GSTEX_REC_SLOAD
-                              ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
-                              : read_rec<kBwdBatch, GSTEX_REC_SGPR != 0>(s_rec, j);
+            const Rec r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(cur_gid, j) * kRecF4);
             // one predicate for the whole heavy path (a single exec-mask region: the zero rows below are
             // materialised once, not at every divergent exit)
             Hit h;
@@ -1128,6 +1131,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             }
         }
         GSTEX_PHASE(2);
+        float4 nx_dims = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bb > 0 && lane < kBwdBatch) nx_dims = records[(size_t)nx_gid * kRecF4 + 6];
         if (lane == 0) s_live[wave] = live;
         if (!(GSTEX_ABLATE & 128)) __syncthreads();  // (ablation 128: timing only, races)
         GSTEX_PHASE(3);
@@ -1135,10 +1140,11 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         // (tile, splat) partial
         {
             const int j = tid >> 2, c0 = (tid & 3) * 6;
+            const int slot_j = __shfl(cur_slot, j & 63, 64);  // wave 0 (tid < 64) does the combine
             if (j < nb) {
                 const bool l0 = (s_live[0] >> j) & 1, l1 = (s_live[1] >> j) & 1;
                 const bool l2 = (s_live[2] >> j) & 1, l3 = (s_live[3] >> j) & 1;
-                float* dst = partials + (size_t)s_slot[j] * kNP + c0;
+                float* dst = partials + (size_t)slot_j * kNP + c0;
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
                     const int c = c0 + i;
@@ -1148,49 +1154,35 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 }
             }
         }
-        // flush the staged texel gradients (only touched entries) and re-zero the staging area
-        if (GSTEX_TEX_FIXED && GSTEX_FLUSH_WAVE) {
-            // splat-major: wave k flushes the staged blocks of batch splats k, k+4, ... (the block base and
-            // size are wave-uniform, so no per-slot owner search), lanes striding over the block
-            for (int j = wave; j < nfit; j += 4) {
-                const int t0 = __builtin_amdgcn_readlane(my_toff, j);
-                const float4 q = s_rec[6 * kBwdBatch + j];
-                const int size = __float_as_int(q.x) * __float_as_int(q.y) * Cn;
-                float* dst = v_texture + (size_t)__float_as_int(q.z) * Cn;
-                for (int e = lane; e < size; e += 64) {
-                    const long long v = (long long)s_texq[t0 + e];
-                    if (v != 0) {
-                        s_texq[t0 + e] = 0ull;
-                        if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e, fixed_to(v, tex_S));
-                    }
-                }
-            }
-        } else {
-            for (int idx = tid; idx < used; idx += kThreads) {
+        // flush the staged texel gradients (only touched entries) and re-zero the staging area, splat-major:
+        // wave k flushes the staged blocks of batch splats k, k+4, ... (block base and size are wave-uniform,
+        // so no per-slot owner search), lanes striding over the block
+        for (int j = wave; j < nfit; j += 4) {
+            const int t0 = __builtin_amdgcn_readlane(my_toff, j);
+            const int size = __builtin_amdgcn_readlane(__float_as_int(cur_dims.x), j) *
+                             __builtin_amdgcn_readlane(__float_as_int(cur_dims.y), j) * Cn;
+            float* dst = v_texture + (size_t)__builtin_amdgcn_readlane(__float_as_int(cur_dims.z), j) * Cn;
+            for (int e = lane; e < size; e += 64) {
                 float val;
                 if (GSTEX_TEX_FIXED) {
-                    const long long q = (long long)s_texq[idx];
-                    val = fixed_to(q, tex_S);
-                    if (q != 0) s_texq[idx] = 0ull;
+                    const long long v = (long long)s_texq[t0 + e];
+                    if (v == 0) continue;
+                    s_texq[t0 + e] = 0ull;
+                    val = fixed_to(v, tex_S);
                 } else {
-                    val = s_tex[idx];
+                    val = s_tex[t0 + e];
+                    if (val == 0.0f) continue;
+                    s_tex[t0 + e] = 0.0f;
                 }
-                if (val != 0.0f) {
-                    int lo = 0, hi = nfit - 1;  // last j with s_toff[j] <= idx
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (s_toff[mid] <= idx) lo = mid;
-                        else hi = mid - 1;
-                    }
-                    const int off = __float_as_int(s_rec[6 * kBwdBatch + lo].z);
-                    if (!(GSTEX_ABLATE & 32)) atomicAdd(v_texture + (size_t)off * Cn + (idx - s_toff[lo]), val);
-                    if (!GSTEX_TEX_FIXED) s_tex[idx] = 0.0f;
-                }
+                if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e, val);
             }
         }
         GSTEX_PHASE(4);
         __syncthreads();
         GSTEX_PHASE(5);
+        cur_gid = nx_gid;
+        cur_slot = nx_slot;
+        cur_dims = nx_dims;
     }
 #if GSTEX_STATS == 2
     if (lane == 0)
