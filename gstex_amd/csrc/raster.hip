@@ -460,7 +460,9 @@ __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int C>
+// GEOF = false: depth / distortion / normal not produced (their outputs are NULL: a caller whose loss does
+// not use them, e.g. the photometric training step); every other output is computed unchanged.
+template <int C, bool GEOF>
 __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
@@ -554,11 +556,13 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             img[0] = img[0] + r.rgb[0] * w;
             img[1] = img[1] + r.rgb[1] * w;
             img[2] = img[2] + r.rgb[2] * w;
-            D = D + h.z * w;
-            nrm[0] = nrm[0] + r.nrm[0] * w;
-            nrm[1] = nrm[1] + r.nrm[1] * w;
-            nrm[2] = nrm[2] + r.nrm[2] * w;
-            if (dreg) {
+            if (GEOF) {
+                D = D + h.z * w;
+                nrm[0] = nrm[0] + r.nrm[0] * w;
+                nrm[1] = nrm[1] + r.nrm[1] * w;
+                nrm[2] = nrm[2] + r.nrm[2] * w;
+            }
+            if (GEOF && dreg) {
                 const float A = 1.0f - T;
                 const float m = kFarRatio * (1.0f - kNear * grad_rcp(h.z));
                 reg = reg + ((m * m * A + M2) - 2.0f * m * M1) * w;
@@ -575,15 +579,19 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     out_img[3 * pix + 0] = img[0] + T * bg0;
     out_img[3 * pix + 1] = img[1] + T * bg1;
     out_img[3 * pix + 2] = img[2] + T * bg2;
-    out_depth[pix] = D;
-    out_reg[pix] = reg;
+    if (GEOF) {
+        out_depth[pix] = D;
+        out_reg[pix] = reg;
+    }
     out_alpha[pix] = 1.0f - T;
 #pragma unroll
     for (int c = 0; c < CM; ++c)
         if (c < Cn) out_tex[(size_t)Cn * pix + c] = tex[c];
-    out_normal[3 * pix + 0] = nrm[0];
-    out_normal[3 * pix + 1] = nrm[1];
-    out_normal[3 * pix + 2] = nrm[2];
+    if (GEOF) {
+        out_normal[3 * pix + 0] = nrm[0];
+        out_normal[3 * pix + 1] = nrm[1];
+        out_normal[3 * pix + 2] = nrm[2];
+    }
     state[pix] = make_float4(T, M1, M2, __int_as_float(last));
 }
 
@@ -1433,22 +1441,27 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
     GSTEX_REQUIRE(n_texels >= 0, "gstex_raster_fwd: n_texels < 0");
     int rc = check_settings(settings);
     if (rc) return rc;
-    GSTEX_REQUIRE(tile_ranges && out_img && out_depth && out_reg && out_alpha && out_tex && out_normal && state,
-                  "gstex_raster_fwd: null pointer");
+    GSTEX_REQUIRE(tile_ranges && out_img && out_alpha && out_tex && state, "gstex_raster_fwd: null pointer");
+    const bool geo = out_depth || out_reg || out_normal;
+    GSTEX_REQUIRE(!geo || (out_depth && out_reg && out_normal),
+                  "gstex_raster_fwd: out_depth, out_reg and out_normal must be all given or all NULL");
     const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
     CamArgs dc = to_device_camera(*cam);
     hipStream_t st = as_stream(stream);
     const int nblk = tiles_x * tiles_y;
-#define GSTEX_FWD(CC)                                                                                          \
-    raster_fwd_kernel<CC><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,          \
+#define GSTEX_FWD(CC, GG)                                                                                      \
+    raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,      \
                                                      (const float4*)records, (const int2*)tile_ranges,        \
                                                      tile_order, sorted_ids, texture, tex_scale, tex_bias, out_img,       \
                                                      out_depth, out_reg,                                                  \
                                                      out_alpha, out_tex, out_normal, (float4*)state,                  \
                                                      (unsigned long long*)visit_masks)
-    if (channels == 3) GSTEX_FWD(3);
-    else if (channels == 6) GSTEX_FWD(6);
-    else GSTEX_FWD(0);
+    if (channels == 3 && geo) GSTEX_FWD(3, true);
+    else if (channels == 3) GSTEX_FWD(3, false);
+    else if (channels == 6 && geo) GSTEX_FWD(6, true);
+    else if (channels == 6) GSTEX_FWD(6, false);
+    else if (geo) GSTEX_FWD(0, true);
+    else GSTEX_FWD(0, false);
 #undef GSTEX_FWD
     return launch_status("gstex_raster_fwd");
 }

@@ -103,7 +103,7 @@ class GStexTrainer:
 
     def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
-                 fused_loss: bool = True, fused_activations: bool = True):
+                 fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -126,6 +126,9 @@ class GStexTrainer:
         self.fused_adam = fused_adam
         self.fused_loss = fused_loss
         self.fused_activations = fused_activations
+        # depth / distortion / normal renders: only for losses or views that read them (the reference's normal
+        # and distortion weights default to 0, gstex.py:198-201, so its training loss uses none of them)
+        self.geometry_outputs = geometry_outputs
         self._build_optimizer()
 
     # ------------------------------------------------------------------ parameters
@@ -185,7 +188,8 @@ class GStexTrainer:
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
             ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
-            texture_transform=(SH_C0, 0.5), fold_aabb=True)  # centers come from get_aabb_2d just above
+            texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
+            geometry_outputs=self.geometry_outputs)
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],

@@ -296,7 +296,8 @@ class _TextureGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
-                block_width, settings, background, texture_transform=None, fold_aabb=False):
+                block_width, settings, background, texture_transform=None, fold_aabb=False,
+                geometry_outputs=True):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -341,12 +342,19 @@ class _TextureGaussians(torch.autograd.Function):
                                                                              float(texture_transform[1]))
         f = dict(device=dev, dtype=torch.float32)
         img = torch.empty((H, W, 3), **f)
-        depth = torch.empty((H, W), **f)
-        reg = torch.empty((H, W), **f)
         alpha = torch.empty((H, W), **f)
         tex = torch.empty((H, W, C), **f)
-        normal = torch.empty((H, W, 3), **f)
         state = torch.empty((H, W, 4), **f)
+        if geometry_outputs:
+            depth = torch.empty((H, W), **f)
+            reg = torch.empty((H, W), **f)
+            normal = torch.empty((H, W, 3), **f)
+            geo_ptrs = (ptr(depth), ptr(reg), ptr(normal))
+        else:  # not produced by the kernel: zeros, no gradient
+            z = torch.zeros((5, H, W), **f)
+            depth, reg, normal = z[0], z[1], z[2:5].permute(1, 2, 0)
+            geo_ptrs = (None, None, None)
+            ctx.mark_non_differentiable(depth, reg, normal)
         # per (tile, wave, splat) "some pixel of the wave received a contribution" bits for the backward
         needs_bwd = any(ctx.needs_input_grad)
         vmask = None
@@ -355,8 +363,8 @@ class _TextureGaussians(torch.autograd.Function):
             vmask = torch.empty((words,), device=dev, dtype=torch.int64)
         _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
-             ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), ptr(depth), ptr(reg), ptr(alpha),
-             ptr(tex), ptr(normal),
+             ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), geo_ptrs[0], geo_ptrs[1], ptr(alpha),
+             ptr(tex), geo_ptrs[2],
              ptr(state), ptr(vmask), st)
         ctx.vmask = vmask
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
@@ -416,13 +424,14 @@ class _TextureGaussians(torch.autograd.Function):
         if ctx.fold_aabb:
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
-                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None)
+                None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
+                None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
-                      fold_aabb=False):
+                      fold_aabb=False, geometry_outputs=True):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -433,6 +442,10 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     get_aabb_2d(means, scales, glob_scale, quats, viewmat, (fx, fy, cx, cy)): the backward then chains the centre
     gradient through the AABB itself (gstex_raster_setup_bwd_aabb) and returns none for `centers`, so neither
     get_aabb_2d's backward nor autograd's accumulation kernels run.  Same gradients, bit for bit.
+
+    geometry_outputs=False (not in the reference API): depth, reg and normal are not produced (returned as
+    zeros without gradient) -- the photometric training step, whose loss does not read them (gstex.py:1313-1317
+    with the default zero normal / distortion weights); the other outputs are unchanged.
 
     Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
     Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
@@ -445,7 +458,7 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     return _TextureGaussians.apply(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs,
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
-                                   fold_aabb)
+                                   fold_aabb, geometry_outputs)
 
 
 rasterize_gaussians = texture_gaussians  # north_star name

@@ -126,7 +126,8 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
  * store itself; the backward's v_texture is then the gradient w.r.t. the stored values. */
 /* Forward composite. Outputs are [H][W][k] row-major. state[H*W][4] = {T_final, M1, M2,
  * last_contributor (as int bits)} is saved for the backward pass. background is a device
- * float[3] (or NULL = black) added as T_final * background. */
+ * float[3] (or NULL = black) added as T_final * background.  out_depth, out_reg and out_normal may be
+ * NULL together (geometric outputs not produced; the backward then takes no gradient for them). */
 int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,

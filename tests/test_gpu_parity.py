@@ -515,3 +515,33 @@ def test_fold_aabb_gradients_bit_identical():
     # texel gradients combine tiles with float atomics (order-dependent rounding), unaffected by the fold
     assert grad_norm_err(res[1]["texture"], res[0]["texture"]) < 1e-6
     assert float(res[0]["means"].abs().max()) > 0
+
+
+def test_geometry_outputs_off_matches():
+    """geometry_outputs=False (photometric training path): img / alpha / tex and every gradient of a
+    photometric upstream are bit-identical to the full render; depth / reg / normal come back as zeros."""
+    case = make_case(n=500, n_texels=25000, H=64, W=80, seed=23)
+    import gstex_cuda
+
+    v, inp = case.view, case.inp
+    dv = lambda t: t.detach().to(DEV).contiguous()  # noqa: E731
+    up = upstream(inp.cam.H, inp.cam.W, case.C, 4)
+    res = []
+    for geo in (True, False):
+        t = {k: dv(getattr(inp, k)).requires_grad_(True) for k in DIFF}
+        outs = gstex_cuda.texture_gaussians(
+            (inp.means.shape[0], 1, case.C), dv(inp.texture_dims), t["centers"], dv(inp.extents), dv(inp.depths),
+            dv(case.nth), t["rgbs"], t["opacities"], t["means"], t["scales"], inp.glob_scale, t["quats"], t["uv0"],
+            dv(inp.umap), dv(inp.vmap), t["texture"], dv(v.viewmat), dv(v.c2w), v.fx, v.fy, v.cx, v.cy, inp.cam.H,
+            inp.cam.W, 16, inp.settings, geometry_outputs=geo)
+        img, depth, reg, alpha, tex, normal = outs
+        torch.autograd.backward([img, alpha, tex], [up["img"].to(DEV), up["alpha"].to(DEV), up["tex"].to(DEV)])
+        res.append((img.detach().cpu(), alpha.detach().cpu(), tex.detach().cpu(),
+                    {k: t[k].grad.detach().cpu() for k in t}, depth, reg, normal))
+    for a, b in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(a, b)
+    for k in ("rgbs", "opacities", "means", "scales", "quats", "centers", "uv0"):
+        assert torch.equal(res[0][3][k], res[1][3][k]), k
+    assert grad_norm_err(res[1][3]["texture"], res[0][3]["texture"]) < 1e-6
+    assert float(res[0][4].detach().abs().max()) > 0 and float(res[1][4].abs().max()) == 0.0
+    assert float(res[1][5].abs().max()) == 0.0 and float(res[1][6].abs().max()) == 0.0

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--n-texels", type=float, default=1e7)
     ap.add_argument("--size", type=int, default=800)
     ap.add_argument("--opacity", type=float, default=0.1)
+    ap.add_argument("--no-geometry", action="store_true", help="geometry_outputs=False (training path)")
     ap.add_argument("--photometric", action="store_true",
                     help="upstream gradients on img/alpha/tex only (the training step's case)")
     args = ap.parse_args()
@@ -46,7 +47,8 @@ def main():
         nth = ops.get_num_tiles_hit_2d(c, e, args.size, args.size, 16)
         outs = ops.texture_gaussians((sc.n, 1, 3), dims, c, e, depths, nth, rgbs, opac, means, scales, 1, quats,
                                      uv0, umap, vmap, tex, v.viewmat, v.c2w, v.fx, v.fy, v.cx, v.cy, args.size,
-                                     args.size, 16, (1 << 9) | (1 << 10), background=None)
+                                     args.size, 16, (1 << 9) | (1 << 10), background=None,
+                                     geometry_outputs=not args.no_geometry)
         if args.photometric:
             torch.autograd.backward([outs[0], outs[3], outs[4]], [ups[0], ups[3], ups[4]])
         else:
