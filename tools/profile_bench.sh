@@ -9,7 +9,8 @@ TAG=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-BENCH="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline"
+# same step/warmup counts as the default bench line, so the steady-state averages agree
+BENCH="python3 bench.py --no-cpu-baseline"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- $BENCH > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- $BENCH > "$OUT/bench_write.log" 2>&1
