@@ -1209,7 +1209,17 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 // setup backward: sum partials per splat, chain to parameters
 // ------------------------------------------------------------------------------------------
-constexpr int kSetupBwdSplats = 256 / kNP;  // 10 splats x 24 partial columns per 256-thread workgroup
+constexpr int kSetupBwdRows = 256 / kNP;  // 10 splats x 24 partial columns summed at once per 256-thread workgroup
+#ifndef GSTEX_SETUP_SPW
+#define GSTEX_SETUP_SPW 40
+#endif
+// splats per workgroup: phase 1 sums them kSetupBwdRows at a time, phase 2 chains them one per thread
+constexpr int kSetupBwdSplats = GSTEX_SETUP_SPW;
+#ifndef GSTEX_SETUP_INFLIGHT
+#define GSTEX_SETUP_INFLIGHT 16
+#endif
+constexpr int kSetupBwdInflight = GSTEX_SETUP_INFLIGHT;
+static_assert(kSetupBwdSplats % kSetupBwdRows == 0 && kSetupBwdSplats <= 256, "setup_bwd splats per workgroup");
 // FOLD_AABB: the centres were produced by get_aabb_2d from these same means / scales / quats (training
 // path), so the AABB-centre chain (aabb_bwd_kernel's arithmetic) is applied here and added in, instead of
 // a separate launch plus autograd's accumulation kernels; the sums are the same two terms added once.
@@ -1223,28 +1233,30 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     float* __restrict__ v_uv0) {
     // phase 1: kNP lanes per splat, lane c sums column c of the splat's partial rows in slot order (the
     // rows of one splat are contiguous, so each step reads one 96-B row per splat instead of one
-    // 96-B row per thread); phase 2: one thread per splat chains the sums to the parameters
+    // 96-B row per thread; same summation order as a plain loop); phase 2: one thread per splat chains the sums to the parameters
     __shared__ float s_sum[kSetupBwdSplats][kNP];
     const int t = threadIdx.x;
     const int g0 = blockIdx.x * kSetupBwdSplats;
-    if (t < kSetupBwdSplats * kNP) {
-        const int j = t / kNP, c = t - j * kNP;
-        float acc = 0.f;
-        if (g0 + j < n) {
-            const int cnt = nth[g0 + j];
-            const float* src = partials + (size_t)offsets[g0 + j] * kNP + c;
-            // same summation order as a plain loop; 8 row loads in flight per lane
-            int e = 0;
-            for (; e + 8 <= cnt; e += 8) {
-                float r[8];
+    if (t < kSetupBwdRows * kNP) {
+        const int c = t % kNP;
+        for (int j = t / kNP; j < kSetupBwdSplats; j += kSetupBwdRows) {
+            float acc = 0.f;
+            if (g0 + j < n) {
+                const int cnt = nth[g0 + j];
+                const float* src = partials + (size_t)offsets[g0 + j] * kNP + c;
+                // groups of kSetupBwdInflight rows, the last one predicated: every row load of a group is in
+                // flight at once, also for the remainder (most splats hit fewer tiles than one group)
+                for (int e = 0; e < cnt; e += kSetupBwdInflight) {
+                    float r[kSetupBwdInflight];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) r[u] = src[(size_t)(e + u) * kNP];
+                    for (int u = 0; u < kSetupBwdInflight; ++u) r[u] = e + u < cnt ? src[(size_t)(e + u) * kNP] : 0.f;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) acc += r[u];
+                    for (int u = 0; u < kSetupBwdInflight; ++u)
+                        if (e + u < cnt) acc += r[u];
+                }
             }
-            for (; e < cnt; ++e) acc += src[(size_t)e * kNP];
+            s_sum[j][c] = acc;
         }
-        s_sum[j][c] = acc;
     }
     __syncthreads();
     const int g = g0 + t;
