@@ -139,6 +139,40 @@ __global__ __launch_bounds__(256) void count_kernel(int n, const float* __restri
 constexpr int kCountSplatsPerThread = 4;
 constexpr int kCountLdsTiles = 16384;  // 64 KiB histogram
 
+#ifndef GSTEX_WAVE_PAIRS
+#define GSTEX_WAVE_PAIRS 1
+#endif
+// place_kernel: wave-cooperative walk over the (splat, tile) pairs of 64 consecutive splats (lane l <-> splat l): the
+// pairs occupy the contiguous emission range [e0 of lane 0, e0 + count of lane 63) and lane l of the
+// wave takes pairs l, l + 64, ... of it, so a large splat's tiles are spread over the whole wave (no
+// lane runs its splat's loop alone while the others idle) and the rank / slot writes are coalesced.
+// The owner of pair e is the last lane whose first slot is <= e (lanes without a splat carry INT_MAX).
+// Must be called with every lane of the wave active (the shuffles read all lanes).  Not used by the
+// count: there one LDS atomic per pair is cheaper than the owner search's ten lane shuffles (measured
+// 46 -> 60 us at cfg3), while the place kernel's scattered global stores hide them (47 -> 32 us).
+struct WavePairs {
+    int e0, x0, y0, w, g;
+};
+__device__ __forceinline__ void wave_pairs_range(const WavePairs& wp, int cnt, int& e_begin, int& e_end) {
+    e_begin = __shfl(wp.e0, 0, 64);
+    int last = wp.e0 == INT_MAX ? -1 : wp.e0 + cnt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o, 64));
+    e_end = last;
+}
+// tile of pair e and its splat (g_out); e must lie in the wave's range for the result to mean anything
+__device__ __forceinline__ int wave_pair_tile(const WavePairs& wp, int e, int tiles_x, int& g_out) {
+    int lo = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+        if (__shfl(wp.e0, lo + st, 64) <= e) lo += st;
+    const int k = e - __shfl(wp.e0, lo, 64);
+    const int w = max(__shfl(wp.w, lo, 64), 1);
+    const int q = k / w;
+    g_out = __shfl(wp.g, lo, 64);
+    return (__shfl(wp.y0, lo, 64) + q) * tiles_x + __shfl(wp.x0, lo, 64) + (k - q * w);
+}
+
 __global__ __launch_bounds__(256) void count_lds_kernel(int n, const float* __restrict__ centers,
                                                         const float* __restrict__ extents,
                                                         const int32_t* __restrict__ offsets, int tiles_x,
@@ -186,13 +220,34 @@ __global__ __launch_bounds__(256) void place_kernel(int n, const float* __restri
                                                     const int32_t* __restrict__ rank,
                                                     unsigned long long* __restrict__ keys,
                                                     int32_t* __restrict__ slot_gid) {
-    int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
-    Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
-                       tiles_y, block);
     // key = depth bits << 32 | emission slot: a splat's slots lie in [offsets[g], offsets[g + 1]) and each
     // splat has at most one slot per tile, so inside a tile the slot orders exactly as the splat id does
     // and the sorted key hands over the slot directly (the id comes from slot_gid)
+    const int g = blockIdx.x * 256 + threadIdx.x;
+#if GSTEX_WAVE_PAIRS
+    // every lane stays active for the wave-wide shuffles; lanes past n own no pairs
+    Rect r{0, 0, 0, 0};
+    if (g < n)
+        r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x, tiles_y,
+                      block);
+    const unsigned dbits = g < n ? __float_as_uint(depths[g]) : 0u;
+    const WavePairs wp{g < n ? offsets[g] : INT_MAX, r.x0, r.y0, r.x1 - r.x0, g};
+    int eb, ee;
+    wave_pairs_range(wp, (r.x1 - r.x0) * (r.y1 - r.y0), eb, ee);
+    for (int base = eb; base < ee; base += 64) {
+        int gg;
+        const int e = base + (threadIdx.x & 63);
+        const int t = wave_pair_tile(wp, e, tiles_x, gg);
+        const unsigned long long dk = (unsigned long long)__shfl(dbits, gg & 63, 64) << 32;
+        if (e < ee) {
+            keys[tile_start[t] + rank[e]] = dk | (unsigned long long)(unsigned)e;
+            slot_gid[e] = gg;
+        }
+    }
+#else
+    if (g >= n) return;
+    Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
+                       tiles_y, block);
     const unsigned long long dk = (unsigned long long)__float_as_uint(depths[g]) << 32;
     int e = offsets[g];
     for (int ty = r.y0; ty < r.y1; ++ty)
@@ -202,6 +257,7 @@ __global__ __launch_bounds__(256) void place_kernel(int n, const float* __restri
             slot_gid[e] = g;
             ++e;
         }
+#endif
 }
 
 __device__ __forceinline__ void bitonic_lds(unsigned long long* s, int P) {
