@@ -9,15 +9,37 @@
 //   p = p - step_size * m / (sqrt(v) / sqrt(bc2) + eps),  step_size = lr / bc1
 // with bc1 = 1 - beta1^t, bc2 = 1 - beta2^t computed on the host per tensor (each tensor keeps its
 // own step count: the texel store restarts at t = 1 after every rechart, gstex.py:812-815).
-// HBM-bound: 16 B read + 12 B written per element, float4 vectorised, one launch for all tensors.
+// HBM-bound: 16 B read + 12 B written per element, float4 vectorised, one launch for all tensors; one
+// float4 per thread with nontemporal loads/stores (measured at cfg3: 205 us with 4 cached float4 per
+// thread, 178 us like this = 6.5 TB/s).
 #include "gstex_common.h"
 #include "gstex_error.h"
 
 namespace {
 
 constexpr int kAdamThreads = 256;
-constexpr int kAdamPerBlock = kAdamThreads * 4 * 4;  // 4 float4 per thread
+#ifndef GSTEX_ADAM_VEC
+#define GSTEX_ADAM_VEC 1
+#endif
+#ifndef GSTEX_ADAM_NT
+#define GSTEX_ADAM_NT 1
+#endif
+constexpr int kAdamVec = GSTEX_ADAM_VEC;  // float4 per thread
+constexpr int kAdamPerBlock = kAdamThreads * 4 * kAdamVec;
 constexpr int kAdamMaxTensors = GSTEX_ADAM_MAX_TENSORS;
+
+// streaming accesses: every byte is touched once per step, so nothing is worth keeping in the caches
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_stream(const float4* p) {
+    if (!GSTEX_ADAM_NT) return *p;
+    const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void st_stream(float4* p, const float4& x) {
+    if (!GSTEX_ADAM_NT) { *p = x; return; }
+    const f4v y = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(y, reinterpret_cast<f4v*>(p));
+}
 
 struct AdamArgs {
     gstex_adam_tensor t[kAdamMaxTensors];
@@ -44,32 +66,32 @@ __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
     const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
                        reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
     if (vec) {
-        // all 16 loads of the thread issued before any store (stores could alias later loads, so the
+        // all 4 * kAdamVec loads of the thread issued before any store (stores could alias later loads, so the
         // compiler would otherwise keep only one iteration's 4 loads in flight)
-        float4 p[4], g[4], m[4], v[4];
-        bool full[4];
+        float4 p[kAdamVec], g[kAdamVec], m[kAdamVec], v[kAdamVec];
+        bool full[kAdamVec];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < kAdamVec; ++r) {
             const int64_t i = base + 4 * ((int64_t)r * kAdamThreads + threadIdx.x);
             full[r] = i + 3 < t.numel;
             if (full[r]) {
-                p[r] = *reinterpret_cast<const float4*>(t.param + i);
-                g[r] = *reinterpret_cast<const float4*>(t.grad + i);
-                m[r] = *reinterpret_cast<const float4*>(t.exp_avg + i);
-                v[r] = *reinterpret_cast<const float4*>(t.exp_avg_sq + i);
+                p[r] = ld_stream(reinterpret_cast<const float4*>(t.param + i));
+                g[r] = ld_stream(reinterpret_cast<const float4*>(t.grad + i));
+                m[r] = ld_stream(reinterpret_cast<const float4*>(t.exp_avg + i));
+                v[r] = ld_stream(reinterpret_cast<const float4*>(t.exp_avg_sq + i));
             }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < kAdamVec; ++r) {
             const int64_t i = base + 4 * ((int64_t)r * kAdamThreads + threadIdx.x);
             if (full[r]) {
                 adam_elem(p[r].x, g[r].x, m[r].x, v[r].x, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
                 adam_elem(p[r].y, g[r].y, m[r].y, v[r].y, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
                 adam_elem(p[r].z, g[r].z, m[r].z, v[r].z, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
                 adam_elem(p[r].w, g[r].w, m[r].w, v[r].w, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                *reinterpret_cast<float4*>(t.param + i) = p[r];
-                *reinterpret_cast<float4*>(t.exp_avg + i) = m[r];
-                *reinterpret_cast<float4*>(t.exp_avg_sq + i) = v[r];
+                st_stream(reinterpret_cast<float4*>(t.param + i), p[r]);
+                st_stream(reinterpret_cast<float4*>(t.exp_avg + i), m[r]);
+                st_stream(reinterpret_cast<float4*>(t.exp_avg_sq + i), v[r]);
             } else {
                 for (int64_t e = i; e < t.numel; ++e)
                     adam_elem(t.param[e], t.grad[e], t.exp_avg[e], t.exp_avg_sq[e], a.one_m_beta1, a.beta2,
