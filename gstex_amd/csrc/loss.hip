@@ -39,6 +39,26 @@ __device__ __forceinline__ float composite(const float* img, const float* tex, c
     return fminf(fmaxf(v, 0.0f), 1.0f);
 }
 
+#ifndef GSTEX_LOSS_XCD
+#define GSTEX_LOSS_XCD 1
+#endif
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs, each with its own L2, so
+// in launch order neighbouring tiles (which share their 10-pixel halos) land on different XCDs and the
+// halos come from HBM again.  Launch slot L goes to XCD L % 8; giving XCD x the contiguous run of tiles
+// [x * n/8, ...) in (bx, by, c) order keeps neighbours on one L2.  A bijection of the launch slots.
+struct LossTile {
+    int bx, by, c;
+};
+__device__ __forceinline__ LossTile loss_tile() {
+    if (!GSTEX_LOSS_XCD) return LossTile{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * gridDim.z;
+    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int per = n / 8, rem = n % 8, xcd = L % 8;
+    const int t = xcd * per + min(xcd, rem) + L / 8;
+    return LossTile{t % gx, (t / gx) % gy, t / (gx * gy)};
+}
+
 __global__ __launch_bounds__(256) void loss_fwd_kernel(int H, int W, int C, const float* __restrict__ img,
                                                        const float* __restrict__ tex,
                                                        const float* __restrict__ alpha,
@@ -48,8 +68,9 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int H, int W, int C, cons
     __shared__ float s_x[kReg][kReg + 1], s_y[kReg][kReg + 1];
     __shared__ float s_h[5][kReg][kLT + 1];
     __shared__ float s_red[2][8];
-    const int c = blockIdx.z;
-    const int x0 = blockIdx.x * kLT, y0 = blockIdx.y * kLT;
+    const LossTile lt = loss_tile();
+    const int c = lt.c;
+    const int x0 = lt.bx * kLT, y0 = lt.by * kLT;
     const int tid = threadIdx.x;
     const int Hv = H - kHalo, Wv = W - kHalo;
     float l1 = 0.f;
@@ -131,7 +152,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int H, int W, int C, cons
     }
     __syncthreads();
     if (tid == 0) {
-        const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int b = (lt.c * gridDim.y + lt.by) * gridDim.x + lt.bx;  // tile index: fixed reduction order
         part[b] = make_float2(((s_red[0][0] + s_red[0][1]) + s_red[0][2]) + s_red[0][3],
                               ((s_red[1][0] + s_red[1][1]) + s_red[1][2]) + s_red[1][3]);
     }
@@ -174,8 +195,9 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int H, int W, int C, cons
                                                        float k_ssim, float* __restrict__ d_rgb) {
     __shared__ float s_g[3][kReg][kReg + 1];
     __shared__ float s_h[3][kReg][kLT + 1];
-    const int c = blockIdx.z;
-    const int x0 = blockIdx.x * kLT, y0 = blockIdx.y * kLT;  // output pixels [x0, x0+16)
+    const LossTile lt = loss_tile();
+    const int c = lt.c;
+    const int x0 = lt.bx * kLT, y0 = lt.by * kLT;  // output pixels [x0, x0+16)
     const int tid = threadIdx.x;
     const int Hv = H - kHalo, Wv = W - kHalo;
     const size_t plane = (size_t)3 * Hv * Wv;
