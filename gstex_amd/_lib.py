@@ -16,6 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
+ABI_VERSION = 5
 REC_FLOATS = 32
 PARTIAL_FLOATS = 24
 SETTING_AA_BLUR = 1 << 9

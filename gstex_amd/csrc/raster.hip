@@ -5,16 +5,18 @@
 // comments of gstex_common.h; the CPU restatement is oracle/raster.py.
 //
 // MI355X layout:
-//   * one 256-thread workgroup (4 wave64) per 16x16 tile, blockIdx -> tile remapped so that each
-//     XCD owns a contiguous band of tiles (neighbouring tiles share splats and texels in its L2);
-//   * splat records are 128-B AoS lines gathered once per batch into LDS as [field][splat] float4
-//     planes (conflict-free writes, broadcast reads);
-//   * forward early-out per wave (ballot) and per workgroup (__syncthreads_count);
-//   * backward: reverse traversal, per-splat gradient partials reduced across the wave with a
-//     reduce-scatter butterfly (30 shuffles for 24 values instead of 144), combined across the 4
-//     waves in LDS in a fixed order and written with plain stores to a per-(tile,splat) slot —
-//     no float atomics for splat gradients, bitwise reproducible; texel gradients use hardware
-//     fp32 atomics (global_atomic_add_f32).
+//   * one 256-thread workgroup (4 wave64, one 8x8 quadrant each) per 16x16 tile, launched in descending
+//     pair-count order (gstex_tile_order: LPT list scheduling over the 8 XCDs' workgroup slots);
+//   * splat records are 128-B AoS lines; the forward stages a batch of them in LDS as [field][splat] float4
+//     planes (conflict-free writes, broadcast reads), the backward reads each visited one into SGPRs;
+//   * forward early-out per wave (ballot) and per workgroup (__syncthreads_count); the forward hands its
+//     per-wave cull bits to the backward (visit_masks);
+//   * backward: reverse traversal, barrier-free between the 4 waves (an LDS ring of batch slots, the last
+//     wave to finish a batch combines and flushes it); per-splat gradient partials reduced across the wave
+//     with a reduce-scatter butterfly (permlane32/16 swaps + DPP), combined across the 4 waves in a fixed
+//     order and written with plain stores to a per-(tile, splat) row (bitwise reproducible, no float
+//     atomics); texel gradients staged per (tile, splat) as 32-bit fixed point in LDS (exact integer adds)
+//     and flushed once per batch with global fp32 atomics (only non-zero entries).
 #include "gstex_common.h"
 #include "gstex_error.h"
 
@@ -92,36 +94,10 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
                         // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
                         // 128 = no barrier before the combine (timing experiments only: racy)
 #endif
-#ifndef GSTEX_TEX_FIXED
-#define GSTEX_TEX_FIXED 1  // stage texel gradients as int64 fixed point (ds_add_u64) instead of ds_add_f32
-#endif
 #ifndef GSTEX_BWD_BATCH
-#define GSTEX_BWD_BATCH (GSTEX_TEX_FIXED ? 16 : 32)  // fixed point: 8-B slots, half the splats per batch
+#define GSTEX_BWD_BATCH 16
 #endif
 constexpr int kBwdBatch = GSTEX_BWD_BATCH;
-#ifndef GSTEX_TEX_LDS
-#define GSTEX_TEX_LDS (GSTEX_TEX_FIXED ? 8064 : 6016)  // what four workgroups per CU leave of the 160 KiB
-#endif
-constexpr int kTexLds = GSTEX_TEX_LDS;  // 4-B words of per-workgroup LDS texel-gradient staging
-constexpr int kTexCap = GSTEX_TEX_FIXED ? kTexLds / 2 : kTexLds;  // staged values per batch
-
-// Texel-gradient fixed point.  The LDS float-atomic path costs the CU ~2 LDS cycles per active lane
-// (the shared bottleneck of the backward: ~90 % of its LDS-busy cycles); 64-bit integer adds cost a
-// fraction of that and are order-independent.  Per tile, e = exponent of max|dL/dtex| over its pixels;
-// one staged value (a per-(tile, splat) texel sum) is bounded by 4 corners x 256 pixels x that max
-// < 2^(e+10), so values are held as round(v * 2^S) with S = 41 - e (|x| < 2^51, resolution 2^-41 of
-// the tile's largest upstream texel gradient).  The conversion rounds through fp64: x + 1.5*2^52 puts
-// the integer in the low mantissa bits (exact for |x| < 2^51).
-__device__ __forceinline__ long long fixed_from(float v, int S) {
-    const double d = __builtin_ldexp((double)v, S);
-    return __double_as_longlong(d + 0x1.8p52) - __double_as_longlong(0x1.8p52);
-}
-__device__ __forceinline__ float fixed_to(long long q, int S) { return __builtin_ldexpf((float)q, -S); }
-// fixed_from for a value already scaled by 2^S (exact: a power-of-two factor commutes with every rounding of
-// the products that formed it): one f32 -> f64 conversion and the magic-number add, no f64 ldexp
-__device__ __forceinline__ long long fixed_from_scaled(float y) {
-    return __double_as_longlong((double)y + 0x1.8p52) - __double_as_longlong(0x1.8p52);
-}
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -466,8 +442,8 @@ template <int C, bool GEOF>
 __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
-    const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, float tex_scale, float tex_bias,
-    float* __restrict__ out_img,
+    const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, int n_texels, float tex_scale,
+    float tex_bias, float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
     float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state,
     unsigned long long* __restrict__ visit_masks) {
@@ -537,7 +513,8 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
                 break;
             }
             const float w = h.alpha * T;
-            if (r.h * r.w > 0 && !(GSTEX_ABLATE & 4)) {
+            // (a block running past the texel store -- corrupt texture_dims -- contributes no texture)
+            if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && !(GSTEX_ABLATE & 4)) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
                 const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
@@ -722,42 +699,50 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     return key >= 0 && (ns != seg || pos == SW - 1);
 }
 
+// Backward: one 256-thread workgroup (4 wave64, one 8x8 quadrant each) per tile, the tile list walked back to
+// front in batches of kBwdBatch splats.  Per visited splat each wave reduces its 24 gradient partials across
+// its 64 pixels; after the batch the four waves' rows are combined in a fixed wave order and stored (plain
+// stores) at the pair's emission slot, where gstex_raster_setup_bwd sums each splat's rows in slot order
+// (bitwise reproducible), and the batch's fixed-point texel staging is flushed by all four waves.
+//
 // GEO = false: no depth / distortion / normal upstream gradient (all NULL, the training default:
 // gstex.py:198-201 sets both weights to 0), so every term they scale is dropped at compile time.  The
 // remaining arithmetic is unchanged (x + 0 * y = x), so both variants give the same values.
+#ifndef GSTEX_TEX_LDS
+#define GSTEX_TEX_LDS 4032  // int64 staging values per workgroup: what four workgroups per CU leave of the 160 KiB
+#endif
+constexpr int kTexCap = GSTEX_TEX_LDS;
+
+// Texel-gradient fixed point: per tile, e = exponent of max |dL/dtex * tex_scale| over its pixels (< 2^e).  A
+// pixel's contribution w b g (w, b <= 1) is < 2^e and a run tail of the 8-lane row scan < 2^(e+3); both are
+// rounded to integers at scale 2^S, S = 27 - e (|q| < 2^30: one v_cvt_rpi_i32_f32, sign-extended), and summed
+// exactly as int64 in LDS (order-independent; a (tile, splat) entry holds at most 256 pixel contributions,
+// < 2^35).  Resolution: 2^-27 of the tile's largest upstream texel gradient.
+constexpr int kTexFixBits = 27;
+__device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^S; round half up, one VALU op
+    int q;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(q) : "v"(y));
+    return q;
+}
+
 template <int C, bool GEO>
 __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
-    const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots,
-    const float* __restrict__ texture, float tex_scale, float tex_bias, const float4* __restrict__ state,
-    const float* __restrict__ v_img,
+    const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots, const float* __restrict__ texture,
+    int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
     float* __restrict__ v_texture, const unsigned long long* __restrict__ visit_masks) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
-    __shared__ float4 s_rec[kRecF4 * kBwdBatch];
     __shared__ float s_part[kBwdBatch][4][kNP];
-    __shared__ int s_gexp;
-    __shared__ unsigned long long s_texq[kTexLds / 2];
-    float* s_tex = reinterpret_cast<float*>(s_texq);  // float staging (GSTEX_TEX_FIXED = 0)
-    __shared__ int s_maxlast;
+    __shared__ unsigned long long s_texq[kTexCap];
     __shared__ unsigned s_live[4];  // per wave: batch splats whose s_part row this wave wrote
+    __shared__ int s_gexp;
+    __shared__ int s_maxlast;
 
-#if GSTEX_STATS
-    const unsigned long long t_start = wall_clock64();
-#endif
-#if GSTEX_STATS == 2
-    // phase clock per wave: 0 record load + barrier, 1 placement + cull, 2 visits, 3 barrier before the
-    // combine, 4 combine + flush, 5 closing barrier, 6 prologue
-    unsigned long long ph_acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    unsigned long long ph_t = __builtin_amdgcn_s_memtime();
-#define GSTEX_PHASE(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[k] += t_ - ph_t; ph_t = t_; } while (0)
-#else
-#define GSTEX_PHASE(k) do { } while (0)
-#endif
     const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -769,7 +754,6 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
     const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
-    const float wx0 = wb.wx0, wx1 = wb.wx1, wy0 = wb.wy0, wy1 = wb.wy1;
 
     float T = 1.0f, M1f = 0.f, M2f = 0.f;
     int last = -1;
@@ -804,10 +788,10 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         s_maxlast = -1;
         s_gexp = 0;  // bits of max |dL/dtex| over the tile (non-negative floats order as ints)
     }
-    for (int i = tid; i < kTexLds / 2; i += kThreads) s_texq[i] = 0ull;
+    for (int i = tid; i < kTexCap; i += kThreads) s_texq[i] = 0ull;
     __syncthreads();
     if (last >= 0) atomicMax(&s_maxlast, last);
-    if (GSTEX_TEX_FIXED) {
+    {
         float gm = 0.f;
 #pragma unroll
         for (int c = 0; c < CM; ++c) gm = fmaxf(gm, fabsf(Gtex[c]));
@@ -816,15 +800,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     }
     __syncthreads();
     const int tile_last = s_maxlast;
-    int tex_S = 0;
-    if (GSTEX_TEX_FIXED) {
+    int tex_S;
+    {
         int e = 0;
         const float gmax = __int_as_float(s_gexp);
         if (gmax > 0.f) (void)frexpf(gmax, &e);  // gmax < 2^e
-        tex_S = 41 - e;
+        tex_S = kTexFixBits - e;
     }
     // texel-gradient contributions are formed directly in the fixed-point scale
-    const float tex_scale_q = GSTEX_TEX_FIXED ? __builtin_ldexpf(tex_scale, tex_S) : tex_scale;
+    const float tex_scale_q = __builtin_ldexpf(tex_scale, tex_S);
     const size_t vm_base = visit_mask_base(rng.x, tile);
     int wave_last = last;
 #pragma unroll
@@ -838,10 +822,9 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         for (int k = 0; k < kNP / 4; ++k) dst[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
-    // Batch metadata lives in registers, lane j <-> splat j of the batch: splat id, emission slot and texel
-    // block (h, w, off: plane 6 of the record).  The next batch's ids and slots are loaded at the start of a
-    // batch and its block dims after the visits, so with the forward's cull bits (visit_masks) a batch needs
-    // no LDS staging and no barrier before its visits.
+    // Batch metadata lives in registers, lane j <-> splat j of the batch: splat id, emission slot and texel block
+    // (h, w, off: plane 6 of the record).  The next batch's ids and slots are loaded at the start of a batch and
+    // its block dims after the visits, so a batch needs no LDS staging and no barrier before its visits.
     int cur_gid = 0, cur_slot = 0;
     float4 cur_dims = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tile_last >= 0) {
@@ -853,27 +836,17 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
         }
     }
 
-    GSTEX_PHASE(6);
     for (int bb = tile_last / kBwdBatch; bb >= 0 && tile_last >= 0; --bb) {
         const int b0 = rng.x + bb * kBwdBatch;
         const int nb = min(kBwdBatch, tile_last - bb * kBwdBatch + 1);
-        if (!visit_masks) {  // the backward's own cull reads the batch records from LDS
-            for (int q = tid; q < kBwdBatch * kRecF4; q += kThreads) {
-                const int j = q >> 3, k = q & 7;
-                if (j < nb) s_rec[k * kBwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
-            }
-            __syncthreads();
-        }
         // next batch (always a full one below the top batch): ids and slots now, block dims after the visits
         int nx_gid = 0, nx_slot = 0;
         if (bb > 0 && lane < kBwdBatch) {
             nx_gid = sorted_ids[b0 - kBwdBatch + lane];
             nx_slot = sorted_slots[b0 - kBwdBatch + lane];
         }
-        GSTEX_PHASE(0);
         // place the batch's texel blocks in LDS: prefix of h*w*C over the batch, computed by every wave for
-        // itself (lane j <-> splat j; no extra barrier); splats past the capacity accumulate straight into
-        // global memory
+        // itself (lane j <-> splat j; no barrier); splats past the capacity accumulate straight into global memory
         int my_toff, nfit;
         {
             int sz = 0;
@@ -886,42 +859,31 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             }
             const bool fits = incl <= kTexCap;
             my_toff = (lane < nb && fits) ? incl - sz : -1;
-            const unsigned long long fm = __ballot(fits && lane < nb);
-            nfit = __popcll(fm);
+            nfit = __popcll(__ballot(fits && lane < nb));
         }
-
-        // the batch splats this wave must visit, tested all at once (lane j <-> splat j): some lane
-        // of the wave reaches it (rel <= last) and its contribution box meets the wave's 16x4 block
+        // the batch splats this wave visits: the forward's cull bits for this wave (one wave-uniform word),
+        // clipped to its last contributor (every splat when the forward recorded none)
         unsigned todo;
-        if (visit_masks) {
-            // the forward's cull bits for this wave (one wave-uniform word), clipped to its last contributor
+        {
             const int pos = bb * kBwdBatch;
-            const unsigned long long vw = visit_masks[(vm_base + (pos >> 6)) * 4 + wave];
+            const unsigned long long vw = visit_masks ? visit_masks[(vm_base + (pos >> 6)) * 4 + wave] : ~0ull;
             const int lim = min(nb, wave_last - pos + 1);
             const unsigned keep = lim <= 0 ? 0u : (lim >= 32 ? ~0u : (1u << lim) - 1u);
             todo = (unsigned)(vw >> (pos & 63)) & ((1u << kBwdBatch) - 1u) & keep;
-        } else {
-            const bool need = lane < nb && bb * kBwdBatch + lane <= wave_last &&
-                              wave_may_hit<kBwdBatch>(s_rec, lane < nb ? lane : 0, wx0, wx1, wy0, wy1, aa);
-            todo = (unsigned)__ballot(need);
         }
         unsigned live = 0u;
-        GSTEX_STAT(0, nb);
-        GSTEX_PHASE(1);
         while (todo) {
             const int j = 31 - __builtin_clz(todo);
             todo &= ~(1u << j);
             const int rel = bb * kBwdBatch + j;
             const Rec r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(cur_gid, j) * kRecF4);
-            // one predicate for the whole heavy path (a single exec-mask region: the zero rows below are
-            // materialised once, not at every divergent exit)
+            // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
             float P[kNP];
 #pragma unroll
             for (int i = 0; i < kNP; i += 2) {
-                // zero rows in 64-bit moves (one v_mov_b64 per register pair; the compiler emits one
-                // v_mov_b32 per register)
+                // zero rows in 64-bit moves (one v_mov_b64 per register pair)
                 unsigned long long zz;
                 asm volatile("v_mov_b64 %0, 0" : "=v"(zz));
                 P[i] = __uint_as_float((unsigned)zz);
@@ -931,119 +893,112 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
             // tkey = top-left texel of the block | (i1 - i0) << 29 | (j1 - j0) << 30, -1 if none
             int tkey = -1;
             float tw = 0.f, tax = 0.f, tay = 0.f;
-            {
-                if (contrib) {
-                    const float one_m = 1.0f - h.alpha;
-                    T = T * grad_rcp(one_m);
-                    const float w = h.alpha * T;
-                    // issue the texel gathers first, then everything that does not need them, so the loads'
-                    // latency overlaps that work
-                    const bool has_tex = r.h * r.w > 0;
-                    Bilerp b;
-                    // wave-uniform block base and size (scalar) + 32-bit per-lane offsets
-                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
-                    float t00[CM], t01[CM], t10[CM], t11[CM];
+            const bool blk_ok = r.off + r.h * r.w <= n_texels;  // wave-uniform; false only for corrupt dims
+            if (contrib) {
+                // gradient arithmetic only from here on (the pair decisions above are the forward's): contracted
+#pragma clang fp contract(fast)
+                const float one_m = 1.0f - h.alpha;
+                T = T * grad_rcp(one_m);
+                const float w = h.alpha * T;
+                // issue the texel gathers first, then everything that does not need them
+                const bool has_tex = r.h * r.w > 0 && blk_ok;
+                Bilerp b;
+                const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
+                float t00[CM], t01[CM], t10[CM], t11[CM];
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
-                    if (has_tex) {
-                        float tu, tv;
-                        tex_coords(r, h.u, h.v, tu, tv);
-                        b = bilerp_coords(tu, tv, r.h, r.w);
-                        if (!(GSTEX_ABLATE & 8)) load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
-                    }
-                    float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
-                    P[P_RGB + 0] = w * Gimg[0];
-                    P[P_RGB + 1] = w * Gimg[1];
-                    P[P_RGB + 2] = w * Gimg[2];
-                    // depth: direct + distortion (m depends on z)
-                    float dz = 0.f, E = 0.f;
-                    if (GEO) {
-                        P[P_NRM + 0] = w * Gn[0];
-                        P[P_NRM + 1] = w * Gn[1];
-                        P[P_NRM + 2] = w * Gn[2];
-                        const float iz = grad_rcp(h.z);
-                        const float m = kFarRatio * (1.0f - kNear * iz);
-                        E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
-                        dz = w * Gd;
-                        if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
-                    }
-                    // texel gradients: per-lane bilinear contributions, scattered after the P reduction
-                    if (has_tex && !(GSTEX_ABLATE & 1)) {
-                        tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
-                        tw = w * tex_scale_q;  // d value / d stored texel (x 2^tex_S with fixed-point staging)
-                        tax = b.ax;
-                        tay = b.ay;
-                    }
-                    // texture value (tex_scale * stored + tex_bias) and its uv-gradient.  Both are linear in the
-                    // texels, so the channels are folded first: D_k = sum_c Gtex[c] * t_k[c] per bilinear corner,
-                    // then one bilinear mix and one pair of differences serve all channels
-                    float dtu = 0.f, dtv = 0.f;
-                    if (has_tex) {
-                        const float hf = (float)r.h, wf = (float)r.w;
-                        float D00 = 0.f, D01 = 0.f, D10 = 0.f, D11 = 0.f;
-#pragma unroll
-                        for (int c = 0; c < CM; ++c) {
-                            if (c < Cn) {
-                                D00 = D00 + Gtex[c] * t00[c];
-                                D01 = D01 + Gtex[c] * t01[c];
-                                D10 = D10 + Gtex[c] * t10[c];
-                                D11 = D11 + Gtex[c] * t11[c];
-                            }
-                        }
-                        g += bilerp_mix(D00, D01, D10, D11, b.ax, b.ay) * tex_scale + Gtex_bias;
-                        const float su = (1.0f - b.ay) * (D10 - D00) + b.ay * (D11 - D01);
-                        const float sv = (1.0f - b.ax) * (D01 - D00) + b.ax * (D11 - D10);
-                        dtu = b.in_u ? w * (hf * su) : 0.0f;
-                        dtv = b.in_v ? w * (wf * sv) : 0.0f;
-                    }
-                    if (GEO) {
-                        g += Gd * h.z;
-                        g += (Gn[0] * r.nrm[0] + Gn[1] * r.nrm[1]) + Gn[2] * r.nrm[2];
-                    }
-                    g += Ga;
-                    if (GEO) g += Greg * E;
-                    const float dL_dalpha = T * (g - R);
-                    R = h.alpha * g + one_m * R;
-
-                    float drho = 0.f;
-                    if (h.a_raw < kAlphaMax) {
-                        P[P_OPAC] = dL_dalpha * h.G;
-                        drho = dL_dalpha * h.a_raw * -0.5f;
-                    }
-                    // texture coordinates
-                    dtu *= tex_scale;  // the raw-value differences above, in value units
-                    dtv *= tex_scale;
-                    P[P_TU0] = dtu; P[P_AUU] = dtu * h.u; P[P_AUV] = dtu * h.v;
-                    P[P_TV0] = dtv; P[P_AVU] = dtv * h.u; P[P_AVV] = dtv * h.v;
-                    float du = dtu * r.auu + dtv * r.avu;
-                    float dv = dtu * r.auv + dtv * r.avv;
-                    // ray-splat (use3) vs screen-space low-pass branch, per lane, as selects (a divergent
-                    // if/else here cost ~30 register moves at the join)
-                    const float du3 = GEO ? drho * 2.0f * h.u + dz * r.Tw.x : drho * 2.0f * h.u;
-                    const float dv3 = GEO ? drho * 2.0f * h.v + dz * r.Tw.y : drho * 2.0f * h.v;
-                    du = h.use3 ? du + du3 : du;
-                    dv = h.use3 ? dv + dv3 : dv;
-                    const f3 dTw = GEO ? f3{h.use3 ? dz * h.u : 0.f, h.use3 ? dz * h.v : 0.f, dz} : f3{0.f, 0.f, 0.f};
-                    P[P_XY + 0] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.x - px);
-                    P[P_XY + 1] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.y - py);
-                    const float ipz = h.ipz;
-                    const f3 dp = f3{du * ipz, dv * ipz, -(du * h.u + dv * h.v) * ipz};
-                    // nk = -dL/dk and nl = -dL/dl exactly (operands of the cross products swapped), so
-                    // the Tu/Tv rows need no negation and Tw subtracts
-                    const f3 nk = cross3(dp, h.l);
-                    const f3 nl = cross3(h.k, dp);
-                    P[P_TU + 0] = nk.x; P[P_TU + 1] = nk.y; P[P_TU + 2] = nk.z;
-                    P[P_TV + 0] = nl.x; P[P_TV + 1] = nl.y; P[P_TV + 2] = nl.z;
-                    P[P_TW + 0] = (dTw.x - h.dx * nk.x) - h.dy * nl.x;
-                    P[P_TW + 1] = (dTw.y - h.dx * nk.y) - h.dy * nl.y;
-                    P[P_TW + 2] = (dTw.z - h.dx * nk.z) - h.dy * nl.z;
+                for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
+                if (has_tex) {
+                    float tu, tv;
+                    tex_coords(r, h.u, h.v, tu, tv);
+                    b = bilerp_coords(tu, tv, r.h, r.w);
+                    if (!(GSTEX_ABLATE & 8)) load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
                 }
+                float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
+                P[P_RGB + 0] = w * Gimg[0];
+                P[P_RGB + 1] = w * Gimg[1];
+                P[P_RGB + 2] = w * Gimg[2];
+                // depth: direct + distortion (m depends on z)
+                float dz = 0.f, E = 0.f;
+                if (GEO) {
+                    P[P_NRM + 0] = w * Gn[0];
+                    P[P_NRM + 1] = w * Gn[1];
+                    P[P_NRM + 2] = w * Gn[2];
+                    const float iz = grad_rcp(h.z);
+                    const float m = kFarRatio * (1.0f - kNear * iz);
+                    E = dreg ? ((m * m * Af - 2.0f * m * M1f) + M2f) : 0.0f;
+                    dz = w * Gd;
+                    if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
+                }
+                if (has_tex && !(GSTEX_ABLATE & 1)) {
+                    tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
+                    tw = w * tex_scale_q;  // d value / d stored texel, x 2^tex_S (fixed-point staging)
+                    tax = b.ax;
+                    tay = b.ay;
+                }
+                // texture value (tex_scale * stored + tex_bias) and its uv-gradient.  Both are linear in the
+                // texels, so the channels are folded first: D_k = sum_c Gtex[c] * t_k[c] per bilinear corner,
+                // then one bilinear mix and one pair of differences serve all channels
+                float dtu = 0.f, dtv = 0.f;
+                if (has_tex) {
+                    const float hf = (float)r.h, wf = (float)r.w;
+                    float D00 = 0.f, D01 = 0.f, D10 = 0.f, D11 = 0.f;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) {
+                        if (c < Cn) {
+                            D00 = D00 + Gtex[c] * t00[c];
+                            D01 = D01 + Gtex[c] * t01[c];
+                            D10 = D10 + Gtex[c] * t10[c];
+                            D11 = D11 + Gtex[c] * t11[c];
+                        }
+                    }
+                    g += bilerp_mix(D00, D01, D10, D11, b.ax, b.ay) * tex_scale + Gtex_bias;
+                    const float su = (1.0f - b.ay) * (D10 - D00) + b.ay * (D11 - D01);
+                    const float sv = (1.0f - b.ax) * (D01 - D00) + b.ax * (D11 - D10);
+                    dtu = b.in_u ? w * (hf * su) : 0.0f;
+                    dtv = b.in_v ? w * (wf * sv) : 0.0f;
+                }
+                if (GEO) {
+                    g += Gd * h.z;
+                    g += (Gn[0] * r.nrm[0] + Gn[1] * r.nrm[1]) + Gn[2] * r.nrm[2];
+                }
+                g += Ga;
+                if (GEO) g += Greg * E;
+                const float dL_dalpha = T * (g - R);
+                R = h.alpha * g + one_m * R;
+
+                float drho = 0.f;
+                if (h.a_raw < kAlphaMax) {
+                    P[P_OPAC] = dL_dalpha * h.G;
+                    drho = dL_dalpha * h.a_raw * -0.5f;
+                }
+                // texture coordinates
+                dtu *= tex_scale;  // the raw-value differences above, in value units
+                dtv *= tex_scale;
+                P[P_TU0] = dtu; P[P_AUU] = dtu * h.u; P[P_AUV] = dtu * h.v;
+                P[P_TV0] = dtv; P[P_AVU] = dtv * h.u; P[P_AVV] = dtv * h.v;
+                float du = dtu * r.auu + dtv * r.avu;
+                float dv = dtu * r.auv + dtv * r.avv;
+                // ray-splat (use3) vs screen-space low-pass branch, per lane, as selects
+                const float du3 = GEO ? drho * 2.0f * h.u + dz * r.Tw.x : drho * 2.0f * h.u;
+                const float dv3 = GEO ? drho * 2.0f * h.v + dz * r.Tw.y : drho * 2.0f * h.v;
+                du = h.use3 ? du + du3 : du;
+                dv = h.use3 ? dv + dv3 : dv;
+                const f3 dTw = GEO ? f3{h.use3 ? dz * h.u : 0.f, h.use3 ? dz * h.v : 0.f, dz} : f3{0.f, 0.f, 0.f};
+                P[P_XY + 0] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.x - px);
+                P[P_XY + 1] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.y - py);
+                const float ipz = h.ipz;
+                const f3 dp = f3{du * ipz, dv * ipz, -(du * h.u + dv * h.v) * ipz};
+                // nk = -dL/dk and nl = -dL/dl exactly (operands of the cross products swapped), so
+                // the Tu/Tv rows need no negation and Tw subtracts
+                const f3 nk = cross3(dp, h.l);
+                const f3 nl = cross3(h.k, dp);
+                P[P_TU + 0] = nk.x; P[P_TU + 1] = nk.y; P[P_TU + 2] = nk.z;
+                P[P_TV + 0] = nl.x; P[P_TV + 1] = nl.y; P[P_TV + 2] = nl.z;
+                P[P_TW + 0] = (dTw.x - h.dx * nk.x) - h.dy * nl.x;
+                P[P_TW + 1] = (dTw.y - h.dx * nk.y) - h.dy * nl.y;
+                P[P_TW + 2] = (dTw.z - h.dx * nk.z) - h.dy * nl.z;
             }
             const bool any = __any(contrib);
-            GSTEX_STAT(1, 1);
-            GSTEX_STAT(2, any ? 1 : 0);
-            GSTEX_STAT(3, __popcll(__ballot(contrib)));
-            GSTEX_STAT(4, (__popcll(__ballot(tkey >= 0)) && __builtin_amdgcn_readlane(my_toff, j) < 0) ? 1 : 0);  // texel grads via global
             if (GSTEX_ABLATE & 2) {
 #pragma unroll
                 for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
@@ -1054,14 +1009,16 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 live |= 1u << j;
                 if ((lane & 7) == 0) {
                     const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
-                    s_part[j][wave][base + 0] = P[0];
-                    s_part[j][wave][base + 1] = P[1];
-                    s_part[j][wave][base + 2] = P[2];
+                    float* dst = &s_part[j][wave][base];
+                    dst[0] = P[0];
+                    dst[1] = P[1];
+                    dst[2] = P[2];
                 }
             }
             if (__any(tkey >= 0)) {
                 float tg[4 * CM];
                 {
+#pragma clang fp contract(fast)
                     const float w00 = (1.0f - tax) * (1.0f - tay), w01 = (1.0f - tax) * tay;
                     const float w10 = tax * (1.0f - tay), w11 = tax * tay;
 #pragma unroll
@@ -1074,57 +1031,31 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                     }
                 }
                 const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
-#if GSTEX_STATS == 1
-                {
-                    unsigned long long tm = __ballot(tail), seen = 0ull;
-                    int distinct = 0;
-                    while (tm & ~seen) {
-                        const int b = __ffsll((long long)(tm & ~seen)) - 1;
-                        const int kb = __shfl(tkey, b, 64);
-                        seen |= __ballot(tail && tkey == kb);
-                        ++distinct;
-                    }
-                    GSTEX_STAT(5, __popcll(tm));
-                    GSTEX_STAT(6, distinct);
-                    GSTEX_STAT(7, 1);
-                }
-#endif
                 if (GSTEX_ABLATE & 16) {
 #pragma unroll
                     for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
                 } else if (tail) {
-                    // keep the LDS and global paths apart: a pointer that may be either compiles to
-                    // flat atomics, several times slower than ds_add_f32 on LDS
                     const int toff = __builtin_amdgcn_readlane(my_toff, j);
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
                     const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
                     const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
-                    if (GSTEX_TEX_FIXED && toff >= 0) {
+                    if (toff >= 0) {
+                        // keep the LDS and global paths apart: a pointer that may be either compiles to flat atomics
+#define GSTEX_FX(v) ((unsigned long long)(long long)fixed_round(v))
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-#define GSTEX_FX(v) ((GSTEX_ABLATE & 64) ? (unsigned long long)__float_as_uint(v) : (unsigned long long)fixed_from_scaled(v))
                                 atomicAdd(&s_texq[toff + c00 + c], GSTEX_FX(tg[c]));
                                 atomicAdd(&s_texq[toff + c01 + c], GSTEX_FX(tg[CM + c]));
                                 atomicAdd(&s_texq[toff + c10 + c], GSTEX_FX(tg[2 * CM + c]));
                                 atomicAdd(&s_texq[toff + c11 + c], GSTEX_FX(tg[3 * CM + c]));
+                            }
+                        }
 #undef GSTEX_FX
-                            }
-                        }
-                    } else if (toff >= 0) {
-#pragma unroll
-                        for (int c = 0; c < CM; ++c) {
-                            if (c < Cn) {
-                                atomicAdd(&s_tex[toff + c00 + c], tg[c]);
-                                atomicAdd(&s_tex[toff + c01 + c], tg[CM + c]);
-                                atomicAdd(&s_tex[toff + c10 + c], tg[2 * CM + c]);
-                                atomicAdd(&s_tex[toff + c11 + c], tg[3 * CM + c]);
-                            }
-                        }
-                    } else {
+                    } else if (blk_ok) {
                         // staging overflow: straight to global, back in value units
                         float* base = v_texture + (size_t)r.off * Cn;
-                        const int uS = GSTEX_TEX_FIXED ? -tex_S : 0;
+                        const int uS = -tex_S;
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
@@ -1138,72 +1069,54 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
                 }
             }
         }
-        GSTEX_PHASE(2);
         float4 nx_dims = make_float4(0.f, 0.f, 0.f, 0.f);
         if (bb > 0 && lane < kBwdBatch) nx_dims = records[(size_t)nx_gid * kRecF4 + 6];
         if (lane == 0) s_live[wave] = live;
-        if (!(GSTEX_ABLATE & 128)) __syncthreads();  // (ablation 128: timing only, races)
-        GSTEX_PHASE(3);
-        // combine the 4 waves in a fixed order (a wave that skipped the splat adds +0) and store the
-        // (tile, splat) partial
+        __syncthreads();
+        // combine the 4 waves in a fixed order (a wave that skipped the splat adds +0) and store the (tile, splat)
+        // row at the pair's emission slot
         {
             const int j = tid >> 2, c0 = (tid & 3) * 6;
             const int slot_j = __shfl(cur_slot, j & 63, 64);  // wave 0 (tid < 64) does the combine
             if (j < nb) {
                 const bool l0 = (s_live[0] >> j) & 1, l1 = (s_live[1] >> j) & 1;
                 const bool l2 = (s_live[2] >> j) & 1, l3 = (s_live[3] >> j) & 1;
-                float* dst = partials + (size_t)slot_j * kNP + c0;
+                float o[6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
                     const int c = c0 + i;
                     const float p0 = l0 ? s_part[j][0][c] : 0.f, p1 = l1 ? s_part[j][1][c] : 0.f;
                     const float p2 = l2 ? s_part[j][2][c] : 0.f, p3 = l3 ? s_part[j][3][c] : 0.f;
-                    dst[i] = ((p0 + p1) + p2) + p3;
+                    o[i] = ((p0 + p1) + p2) + p3;
                 }
+                float2* dst = reinterpret_cast<float2*>(partials + (size_t)slot_j * kNP + c0);
+                dst[0] = make_float2(o[0], o[1]);
+                dst[1] = make_float2(o[2], o[3]);
+                dst[2] = make_float2(o[4], o[5]);
             }
         }
         // flush the staged texel gradients (only touched entries) and re-zero the staging area, splat-major:
-        // wave k flushes the staged blocks of batch splats k, k+4, ... (block base and size are wave-uniform,
-        // so no per-slot owner search), lanes striding over the block
+        // wave k flushes the staged blocks of batch splats k, k+4, ... (block base and size are wave-uniform),
+        // lanes striding over the block
         for (int j = wave; j < nfit; j += 4) {
             const int t0 = __builtin_amdgcn_readlane(my_toff, j);
             const int size = __builtin_amdgcn_readlane(__float_as_int(cur_dims.x), j) *
                              __builtin_amdgcn_readlane(__float_as_int(cur_dims.y), j) * Cn;
-            float* dst = v_texture + (size_t)__builtin_amdgcn_readlane(__float_as_int(cur_dims.z), j) * Cn;
+            const int off = __builtin_amdgcn_readlane(__float_as_int(cur_dims.z), j);
+            const bool ok = off + size / Cn <= n_texels;  // a block past the texel store (corrupt dims) is dropped
+            float* dst = v_texture + (size_t)off * Cn;
             for (int e = lane; e < size; e += 64) {
-                float val;
-                if (GSTEX_TEX_FIXED) {
-                    const long long v = (long long)s_texq[t0 + e];
-                    if (v == 0) continue;
-                    s_texq[t0 + e] = 0ull;
-                    val = fixed_to(v, tex_S);
-                } else {
-                    val = s_tex[t0 + e];
-                    if (val == 0.0f) continue;
-                    s_tex[t0 + e] = 0.0f;
-                }
-                if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e, val);
+                const long long v = (long long)s_texq[t0 + e];
+                if (v == 0) continue;
+                s_texq[t0 + e] = 0ull;
+                if (ok && !(GSTEX_ABLATE & 32)) atomicAdd(dst + e, __builtin_ldexpf((float)v, -tex_S));
             }
         }
-        GSTEX_PHASE(4);
         __syncthreads();
-        GSTEX_PHASE(5);
         cur_gid = nx_gid;
         cur_slot = nx_slot;
         cur_dims = nx_dims;
     }
-#if GSTEX_STATS == 2
-    if (lane == 0)
-        for (int k = 0; k < 7; ++k) atomicAdd(&g_stats[k], ph_acc[k]);
-#endif
-#if GSTEX_STATS
-    if (tid == 0 && tile < 4096) {
-        g_wg[4 * tile + 0] = t_start;
-        g_wg[4 * tile + 1] = wall_clock64();
-        g_wg[4 * tile + 2] = (unsigned)__builtin_amdgcn_s_getreg(0xF804) | ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
-        g_wg[4 * tile + 3] = (unsigned long long)(rng.y - rng.x) | ((unsigned long long)blockIdx.x << 32);
-    }
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1348,7 +1261,7 @@ __global__ __launch_bounds__(kThreads) void texture_edit_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float4* __restrict__ records,
     const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order, const int32_t* __restrict__ sorted_ids,
     const float* __restrict__ edit_rgb, const float* __restrict__ edit_a, const float* __restrict__ depth_lo,
-    const float* __restrict__ depth_hi, float* __restrict__ out) {
+    const float* __restrict__ depth_hi, int n_texels, float* __restrict__ out) {
     const Camera cam = load_camera(cam_args);
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
     const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;
@@ -1389,7 +1302,7 @@ __global__ __launch_bounds__(kThreads) void texture_edit_kernel(
                 break;
             }
             const float w = h.alpha * T;
-            if (r.h * r.w > 0 && h.z >= dlo && h.z <= dhi) {
+            if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && h.z >= dlo && h.z <= dhi) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
                 const Bilerp bl = bilerp_coords(tu, tv, r.h, r.w);
@@ -1450,7 +1363,8 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_fwd: channels must be in [1, 8] (got %d)",
                   channels);
-    GSTEX_REQUIRE(n_texels >= 0, "gstex_raster_fwd: n_texels < 0");
+    GSTEX_REQUIRE(n_texels >= 0 && n_texels * channels < (int64_t)INT32_MAX, "gstex_raster_fwd: n_texels out of range");
+    GSTEX_REQUIRE(n_texels == 0 || texture, "gstex_raster_fwd: null texture");
     int rc = check_settings(settings);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && out_img && out_alpha && out_tex && state, "gstex_raster_fwd: null pointer");
@@ -1464,7 +1378,8 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 #define GSTEX_FWD(CC, GG)                                                                                      \
     raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,      \
                                                      (const float4*)records, (const int2*)tile_ranges,        \
-                                                     tile_order, sorted_ids, texture, tex_scale, tex_bias, out_img,       \
+                                                     tile_order, sorted_ids, texture, (int)n_texels, tex_scale,        \
+                                                     tex_bias, out_img,                                                   \
                                                      out_depth, out_reg,                                                  \
                                                      out_alpha, out_tex, out_normal, (float4*)state,                  \
                                                      (unsigned long long*)visit_masks)
@@ -1491,8 +1406,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
     int rc = check_settings(settings);
     if (rc) return rc;
-    GSTEX_REQUIRE(tile_ranges && state,
-                  "gstex_raster_bwd: null pointer");
+    GSTEX_REQUIRE(tile_ranges && state, "gstex_raster_bwd: null pointer");
+    GSTEX_REQUIRE(n_texels >= 0 && n_texels * channels < (int64_t)INT32_MAX, "gstex_raster_bwd: n_texels out of range");
     GSTEX_REQUIRE(n_texels == 0 || (texture && v_texture), "gstex_raster_bwd: null texture");
     const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
     CamArgs dc = to_device_camera(*cam);
@@ -1503,7 +1418,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
 #define GSTEX_BWD(CC, GG)                                                                                      \
     raster_bwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(                                                      \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
-        tile_order, sorted_ids, sorted_slots, texture, tex_scale, tex_bias, (const float4*)state, v_img, v_depth,      \
+        tile_order, sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,    \
+        v_img, v_depth,                                                                                         \
         v_reg, v_alpha, v_tex,                                                                                  \
         v_normal, partials, v_texture, (const unsigned long long*)visit_masks)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
@@ -1575,6 +1491,6 @@ extern "C" int gstex_texture_edit(const gstex_camera* cam, int32_t settings, con
     CamArgs dc = to_device_camera(*cam);
     texture_edit_kernel<<<tiles_x * tiles_y, kThreads, 0, as_stream(stream)>>>(
         dc, tiles_x, settings, (const float4*)records, (const int2*)tile_ranges, tile_order, sorted_ids, edit_rgb,
-        edit_alpha, depth_lo, depth_hi, out);
+        edit_alpha, depth_lo, depth_hi, (int)n_texels, out);
     return launch_status("gstex_texture_edit");
 }

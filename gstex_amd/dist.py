@@ -21,31 +21,46 @@ import torch.distributed as dist
 
 
 class GradSync:
-    """overlap_tail: the last parameter (the texel store, ~73 % of the bytes at cfg3) gets its own
-    asynchronous all-reduce from a post-accumulate-grad hook, i.e. as soon as the raster backward has
-    produced it, overlapping the collective with the rest of the backward (setup_bwd, SH, activations);
-    all_reduce() then reduces the head of the buffer and waits for both."""
+    """overlap_tail: the last parameter (the texel store, ~73 % of the bytes at cfg3) gets its own asynchronous
+    all-reduce as soon as its gradient is final, overlapping the collective with the rest of the backward
+    (setup_bwd, SH, activations); all_reduce() then reduces the head of the buffer and waits for both.
+
+    A trainer that exposes ``texture_grad_sink`` / ``texture_grad_ready`` (gstex_amd.model.GStexTrainer) gets
+    the tail slice of the flat buffer as the raster backward's texel-gradient target: the kernel accumulates
+    straight into the buffer (no separate zero-filled gradient tensor, no autograd accumulation pass) and the
+    tail collective starts right after that kernel is enqueued.  Other parameter holders use a
+    post-accumulate-grad hook on the tail parameter.
+
+    The buffer layout is keyed on parameter identity and shape: a rechart that reuses the texel store in place
+    (GStexTrainer.recharge while the new charts fit its capacity) keeps the buffer; one that replaces the
+    Parameter rebuilds it.  One backward per all_reduce(): gradient accumulation over several backward passes
+    is not supported (the tail would be reduced after the first)."""
 
     def __init__(self, trainer, world_size: int, group=None, overlap_tail: bool = True):
         self.trainer = trainer
         self.world = world_size
         self.group = group
         self.overlap_tail = overlap_tail
-        self._shapes = None
+        self._key = None
         self.flat = None
         self._tail_off = 0
         self._hook = None
         self._hooked = None
         self._work = None
+        self._sink = hasattr(trainer, "texture_grad_sink")
         self.rebuild()
 
     def _params(self):
         return self.trainer.parameters()
 
+    @staticmethod
+    def _layout(params):
+        return [(id(p), tuple(p.shape)) for p in params]
+
     def rebuild(self):
         params = self._params()
-        shapes = [tuple(p.shape) for p in params]
-        if shapes == self._shapes and self.flat is not None:
+        key = self._layout(params)
+        if key == self._key and self.flat is not None:
             return False
         total = sum(p.numel() for p in params)
         dev = params[0].device
@@ -55,9 +70,13 @@ class GradSync:
             n = p.numel()
             p.grad = self.flat[off:off + n].view_as(p)
             off += n
-        self._shapes = shapes
+        self._key = key
         self._tail_off = total - params[-1].numel()
-        self._install_hook(params[-1])
+        if self._sink:
+            self.trainer.texture_grad_sink = params[-1].grad
+            self.trainer.texture_grad_ready = self._tail_ready_sink if self.overlap_tail else None
+        else:
+            self._install_hook(params[-1])
         return True
 
     def _install_hook(self, tail):
@@ -68,24 +87,35 @@ class GradSync:
         self._hooked = tail
         self._hook = tail.register_post_accumulate_grad_hook(self._tail_ready)
 
+    def _start_tail(self):
+        self._work = dist.all_reduce(self.flat[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
+                                     async_op=True)
+
+    def _tail_ready_sink(self):
+        # the raster backward has just been enqueued on the compute stream: the collective is stream-ordered
+        # after it and overlaps the rest of the backward
+        if self._work is None:
+            self._start_tail()
+
     def _tail_ready(self, param):
         # fires once the texel gradient is final for this backward; the view is still the flat buffer's
         if self._work is None and param.grad is not None and param.grad.data_ptr() == self.flat[self._tail_off:].data_ptr():
-            self._work = dist.all_reduce(self.flat[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
-                                         async_op=True)
+            self._start_tail()
 
     @property
     def nbytes(self) -> int:
         return self.flat.numel() * 4
 
     def zero(self):
+        if self._work is not None:
+            raise RuntimeError("GradSync.zero(): the previous backward's all_reduce() was never called")
         self.rebuild()
         self.flat.zero_()
 
     def all_reduce(self):
         """Average the flat gradient buffer over all ranks (the tail's collective may already be running)."""
         work, self._work = self._work, None
-        if work is not None and [tuple(p.shape) for p in self._params()] == self._shapes:
+        if work is not None and self._layout(self._params()) == self._key:
             dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
             work.wait()
         else:
@@ -99,9 +129,9 @@ class GradSync:
         # autograd may have replaced a .grad that was not a view of `flat` (e.g. first step after
         # a parameter was re-created): fold it back into the buffer before reducing.
         params = self._params()
-        if [tuple(p.shape) for p in params] != self._shapes:
+        if self._layout(params) != self._key:
             grads = [p.grad.detach().clone() if p.grad is not None else None for p in params]
-            self._shapes = None
+            self._key = None
             self.rebuild()
             for p, g in zip(params, grads):
                 if g is not None:

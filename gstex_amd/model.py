@@ -103,7 +103,8 @@ class GStexTrainer:
 
     def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
-                 fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False):
+                 fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
+                 sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -113,22 +114,32 @@ class GStexTrainer:
         self.opacities = P(scene.opacity_logits)
         self.features_dc = P(scene.features_dc)
         self.features_rest = P(scene.features_rest)
-        # the texel parameter stores the SH-DC value; the raster reads SH2RGB of it (gstex.py:1119)
+        # the texel parameter stores the SH-DC value; the raster reads SH2RGB of it (gstex.py:1119).  Like the
+        # reference's JaggedTexture (jagged_texture.py:36-64) it is a capacity store: rows [0, n_texels) are the
+        # texels of the current charts, the store only grows at a rechart, and the raster takes the whole store
+        # (texture_dims never index past n_texels), so its gradient needs no slice-backward copy
         tex_dc = (scene.texture[:, :3] - 0.5) / 0.28209479177387814
         self.texture_dc = P(tex_dc)
+        self.n_texels = int(tex_dc.shape[0])
         self.texture_dims = scene.texture_dims.to(d).contiguous()
         self.mappings = scene.mappings.to(d).contiguous()
         self.sh_degree = sh_degree
         self.settings = settings
         self.pixel_num = pixel_num if pixel_num is not None else float(scene.texture.shape[0])
         self.background = torch.tensor(background, dtype=torch.float32, device=d)
-        self.step = 0
+        self.step = start_step
+        self.sh_degree_interval = sh_degree_interval  # gstex.py:182
+        self.fix_init = fix_init  # gstex.py:209 (DTU configs): SH view directions (x, -z, y), gstex.py:1104-1108
         self.fused_adam = fused_adam
         self.fused_loss = fused_loss
         self.fused_activations = fused_activations
         # depth / distortion / normal renders: only for losses or views that read them (the reference's normal
         # and distortion weights default to 0, gstex.py:198-201, so its training loss uses none of them)
         self.geometry_outputs = geometry_outputs
+        # set by gstex_amd.dist.GradSync: the flat-buffer slice the raster backward accumulates the texel gradient
+        # into, and the callback that starts its collective (None: autograd owns the texel gradient)
+        self.texture_grad_sink = None
+        self.texture_grad_ready = None
         self._build_optimizer()
 
     # ------------------------------------------------------------------ parameters
@@ -169,6 +180,8 @@ class GStexTrainer:
             uv0, umap, vmap = get_uv_mapping(quats, self.mappings)
             viewdirs = means.detach() - view.c2w[:3, 3]
             viewdirs = viewdirs / viewdirs.norm(dim=-1, keepdim=True)
+        if self.fix_init and self.sh_degree > 0:
+            viewdirs = torch.stack([viewdirs[:, 0], -viewdirs[:, 2], viewdirs[:, 1]], -1)
         intr = (view.fx, view.fy, view.cx, view.cy)
         _, depths = ops.project_points(means, view.viewmat, intr)
         centers, extents = ops.get_aabb_2d(means, scales, 1, quats, view.viewmat, intr)
@@ -189,7 +202,8 @@ class GStexTrainer:
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
             ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
-            geometry_outputs=self.geometry_outputs)
+            geometry_outputs=self.geometry_outputs, texture_grad_sink=self.texture_grad_sink,
+            on_texture_grad=self.texture_grad_ready)
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
@@ -201,8 +215,12 @@ class GStexTrainer:
         sim = 1 - ssim(gt.permute(2, 0, 1)[None], rgb.permute(2, 0, 1)[None])
         return (1 - ssim_lambda) * l1 + ssim_lambda * sim
 
+    def sh_degree_now(self) -> int:
+        """The SH degree ramp of the reference: min(step // sh_degree_interval, sh_degree) (gstex.py:1103)."""
+        return min(self.step // self.sh_degree_interval, self.sh_degree)
+
     def forward_backward(self, view: View, gt: torch.Tensor) -> StepOutput:
-        out = self.render(view, composite=not self.fused_loss)
+        out = self.render(view, sh_degree_now=self.sh_degree_now(), composite=not self.fused_loss)
         if self.fused_loss:  # composite + clamp + L1/SSIM in one HIP launch pair (gstex_amd.loss)
             loss, rgb = photometric_loss(out["img"], out["tex"], out["alpha"], self.background, gt.contiguous())
         else:
@@ -224,19 +242,40 @@ class GStexTrainer:
     # ------------------------------------------------------------------ rechart
     @torch.no_grad()
     def recharge(self):
-        """retexture_after (gstex.py:890-895): rebuild the charts from the current scales, resample
-        the texels onto the new grid (texture_sample, jagged_texture.py:116-143) and reset the
-        texture Adam moments (gstex.py:799-826)."""
+        """retexture_after (gstex.py:890-895): rebuild the charts from the current scales, resample the texels
+        onto the new grid (texture_sample, JaggedTexture.init_from_dims, jagged_texture.py:116-143) and reset the
+        texture Adam moments (reshape_in_optim, gstex.py:799-826: exp_avg / exp_avg_sq zeroed, step kept).
+
+        The texel store is reused in place while the new charts fit its capacity (jagged_texture.py:45-64:
+        adjust_texture_size only ever grows it), so the Parameter, its optimizer entry and any flat gradient
+        buffer built over it (gstex_amd.dist.GradSync) stay valid; only a growth replaces the Parameter."""
         new_dims, mappings, _ = build_charts(self.scales.detach(), self.pixel_num)
+        n_new = int((new_dims[:, 0].long() * new_dims[:, 1].long()).sum())
         ids, uv = texture_dims_to_query(new_dims)
         query = self.texture_dims[ids].contiguous()
-        new_tex = ops.texture_sample((1, 1, 3), query, self.texture_dc.detach().contiguous(), uv.contiguous())
-        self.texture_dims = new_dims.contiguous()
-        self.mappings.copy_(mappings)
+        new_tex = ops.texture_sample((1, 1, 3), query, self.texture_dc.detach(), uv.contiguous())
         old = self.texture_dc
-        self.texture_dc = torch.nn.Parameter(new_tex.contiguous())
-        for g in self.optimizer.param_groups:
-            if g["name"] == "texture_dc":
-                g["params"] = [self.texture_dc]
-        self.optimizer.state.pop(old, None)
+        cap = old.shape[0]
+        if n_new > cap:  # adjust_texture_size: grow with zero rows (jagged_texture.py:53-64)
+            store = torch.cat([old.detach(), old.new_zeros((n_new - cap, old.shape[1]))], 0)
+            self.texture_dc = torch.nn.Parameter(store)
+            for g in self.optimizer.param_groups:
+                if g["name"] == "texture_dc":
+                    g["params"] = [self.texture_dc]
+            st = self.optimizer.state.pop(old, None)
+            if st:
+                self.optimizer.state[self.texture_dc] = {
+                    "step": st.get("step", 0),
+                    "exp_avg": torch.zeros_like(self.texture_dc),
+                    "exp_avg_sq": torch.zeros_like(self.texture_dc),
+                }
+        else:
+            st = self.optimizer.state.get(old)
+            if st:
+                st["exp_avg"].zero_()
+                st["exp_avg_sq"].zero_()
+        self.texture_dc.data[:n_new] = new_tex
+        self.texture_dims = new_dims.contiguous()
+        self.n_texels = n_new
+        self.mappings.copy_(mappings)
         return new_dims

@@ -297,7 +297,7 @@ class _TextureGaussians(torch.autograd.Function):
     def forward(ctx, texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                 block_width, settings, background, texture_transform=None, fold_aabb=False,
-                geometry_outputs=True):
+                geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -334,7 +334,20 @@ class _TextureGaussians(torch.autograd.Function):
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
              ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
              st)
-        ctx.v_texture = torch.zeros_like(texture) if ctx.needs_input_grad[15] else None
+        # backward-only buffers only when a backward can follow: not under torch.no_grad() (eval renders of
+        # trainable parameters), where apply() records no graph whatever the inputs' requires_grad
+        needs_bwd = bool(grad_enabled) and any(ctx.needs_input_grad)
+        ctx.v_texture = None
+        ctx.sink = texture_grad_sink is not None
+        ctx.on_texture_grad = on_texture_grad
+        if needs_bwd and ctx.needs_input_grad[15]:
+            if ctx.sink:  # the caller's (zeroed) gradient buffer: accumulated into, nothing returned to autograd
+                _check(texture_grad_sink.shape == texture.shape and texture_grad_sink.is_contiguous() and
+                       texture_grad_sink.dtype == torch.float32 and texture_grad_sink.device == texture.device,
+                       "texture_grad_sink must be a contiguous fp32 tensor shaped like texture on its device")
+                ctx.v_texture = texture_grad_sink
+            else:
+                ctx.v_texture = torch.zeros_like(texture)
         offsets, tile_ranges, sorted_ids, sorted_slots = bin_finish(begun, centers_c.detach(), extents_c, depths_c,
                                                                     H, W, BLOCK_WIDTH)
         order = tile_order(tile_ranges)
@@ -355,8 +368,7 @@ class _TextureGaussians(torch.autograd.Function):
             depth, reg, normal = z[0], z[1], z[2:5].permute(1, 2, 0)
             geo_ptrs = (None, None, None)
             ctx.mark_non_differentiable(depth, reg, normal)
-        # per (tile, wave, splat) "some pixel of the wave received a contribution" bits for the backward
-        needs_bwd = any(ctx.needs_input_grad)
+        # per (tile, wave, splat) cull bits of the forward for the backward
         vmask = None
         if needs_bwd:
             words = int(_lib.load().gstex_visit_mask_words(sorted_ids.shape[0], tile_ranges.shape[0]))
@@ -404,10 +416,14 @@ class _TextureGaussians(torch.autograd.Function):
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
-             ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0], ctx.tex_affine[1],
-             ptr(state), ptr(v_img), ptr(v_depth),
-             ptr(v_reg), ptr(v_alpha), ptr(v_tex), ptr(v_normal), ptr(partials), ptr(v_texture), ptr(ctx.vmask), st)
+                ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
+                ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
+                ptr(v_normal), ptr(partials), ptr(v_texture), ptr(ctx.vmask), st)
         ctx.vmask = None
+        if ctx.sink:
+            if ctx.on_texture_grad is not None:
+                ctx.on_texture_grad()  # the texel gradient is complete in stream order
+            v_texture = None
         v_means = torch.empty_like(means)
         v_scales = torch.empty_like(scales)
         v_quats = torch.empty_like(quats)
@@ -415,9 +431,9 @@ class _TextureGaussians(torch.autograd.Function):
         v_opac = torch.empty((n, 1), device=dev, dtype=torch.float32)
         v_centers = torch.empty((n, 2), device=dev, dtype=torch.float32)
         v_uv0 = torch.empty((n, 1, 2), device=dev, dtype=torch.float32)
-        _launch("gstex_raster_setup_bwd_aabb" if ctx.fold_aabb else "gstex_raster_setup_bwd", n, ptr(means), ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap),
-             ptr(vmap), ptr(nth), ptr(offsets), ptr(partials), cam, ptr(v_means), ptr(v_scales), ptr(v_quats),
-             ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
+        _launch("gstex_raster_setup_bwd_aabb" if ctx.fold_aabb else "gstex_raster_setup_bwd", n, ptr(means),
+                ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap), ptr(vmap), ptr(nth), ptr(offsets), ptr(partials), cam,
+                ptr(v_means), ptr(v_scales), ptr(v_quats), ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
         v_bg = None
         if ctx.needs_input_grad[26]:
             v_bg = (v_img * state[..., 0:1]).sum((0, 1)) if v_img is not None else torch.zeros_like(bg)
@@ -425,13 +441,13 @@ class _TextureGaussians(torch.autograd.Function):
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
-                None)
+                None, None, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
-                      fold_aabb=False, geometry_outputs=True):
+                      fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -447,6 +463,11 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     zeros without gradient) -- the photometric training step, whose loss does not read them (gstex.py:1313-1317
     with the default zero normal / distortion weights); the other outputs are unchanged.
 
+    texture_grad_sink (not in the reference API; multi-GPU training): a zeroed contiguous fp32 tensor shaped like
+    `texture` that the backward accumulates the texel gradient into (e.g. the texel slice of a flat all-reduce
+    buffer); autograd then receives no gradient for `texture`, and on_texture_grad() (if given) is called once the
+    kernel producing it has been enqueued.
+
     Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
     Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
     uv0 and background; umap/vmap are treated as constants (detached by the caller, gstex.py:977-984).
@@ -458,7 +479,8 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     return _TextureGaussians.apply(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs,
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
-                                   fold_aabb, geometry_outputs)
+                                   fold_aabb, geometry_outputs, torch.is_grad_enabled(), texture_grad_sink,
+                                   on_texture_grad)
 
 
 rasterize_gaussians = texture_gaussians  # north_star name

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 4
+#define GSTEX_ABI_VERSION 5
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -140,7 +140,8 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
  * of re-running the geometric test.  Pass the same buffer to both. */
 size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles);
 /* Backward composite. Needs the forward state and the same tile_order. Any of v_img ... v_normal may be
- * NULL (that output's gradient is zero). Writes
+ * NULL (that output's gradient is zero).  Texel blocks that run past n_texels (corrupt texture_dims) are
+ * neither read nor written. Writes
  * partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of every (tile, splat) pair and
  * accumulates (+=) texel gradients into v_texture[n_texels][C]. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,

@@ -18,6 +18,6 @@ Parity status
 * The rasterizer itself (binning/sort order, composite forward, backward) is **parity unpinned**
   with respect to the reference CUDA kernels: they are absent, and the reference has no tests,
   fixtures or golden images for this path.  The oracle is pinned instead by
-  closed-form known-answer tests (tests/test_oracle_kat.py), finite differences of its own
+  closed-form known-answer tests (tests/test_oracle.py), finite differences of its own
   forward, and the call-site contracts.
 """

@@ -72,3 +72,95 @@ def test_grad_all_reduce_world2(overlap):
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] for r in res), "flat all-reduce did not average the gradients"
     assert all(r[2] for r in res), "flat buffer not rebuilt after the texel store changed size"
+
+
+class _SinkTrainer:
+    """The parameter layout of gstex_amd.model.GStexTrainer (7 groups, texel store last) and its texel-gradient
+    sink protocol, on CPU: `backward()` plays the raster backward (accumulates into the sink and calls the ready
+    callback) plus autograd for the other parameters."""
+
+    def __init__(self, n=12, n_tex=40):
+        g = torch.Generator().manual_seed(3)
+        P = lambda *s: torch.nn.Parameter(torch.randn(*s, generator=g))  # noqa: E731
+        self.means, self.features_dc, self.features_rest = P(n, 3), P(n, 3), P(n, 15, 3)
+        self.opacities, self.scales, self.quats = P(n, 1), P(n, 3), P(n, 4)
+        self.texture_dc = P(n_tex, 3)
+        self.texture_grad_sink = None
+        self.texture_grad_ready = None
+
+    def parameters(self):
+        return [self.means, self.features_dc, self.features_rest, self.opacities, self.scales, self.quats,
+                self.texture_dc]
+
+    def backward(self, rank):
+        w = float(rank + 1)
+        loss = w * (self.means.sum() + self.features_rest.sum() + 2 * self.opacities.sum() + self.scales.sum()
+                    + self.quats.sum())
+        loss.backward()  # features_dc unused under SH colour, like the real step
+        assert self.texture_grad_sink is not None, "GradSync must hand the texel slice to the raster backward"
+        self.texture_grad_sink.add_(w * self.texture_dc.detach())  # the kernel's accumulation
+        if self.texture_grad_ready is not None:
+            self.texture_grad_ready()
+
+
+def _trainer_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = _SinkTrainer()
+        sync = GradSync(tr, world)
+        res = {}
+        mean_w = sum(r + 1 for r in range(world)) / world
+        for step in range(3):
+            sync.zero()
+            tr.backward(rank)
+            res[f"tail_started_{step}"] = sync._work is not None
+            sync.all_reduce()
+            ok = torch.allclose(tr.texture_dc.grad, mean_w * tr.texture_dc.detach())
+            ok = ok and torch.allclose(tr.means.grad, torch.full_like(tr.means, mean_w))
+            ok = ok and torch.allclose(tr.opacities.grad, torch.full_like(tr.opacities, 2 * mean_w))
+            ok = ok and bool(torch.all(tr.features_dc.grad == 0))
+            res[f"ok_{step}"] = bool(ok)
+            flat_before = sync.flat.data_ptr()
+            if step == 0:  # rechart that fits the store: same Parameter, written in place -> no rebuild
+                with torch.no_grad():
+                    tr.texture_dc.data[:30] = 1.0
+            elif step == 1:  # rechart that grows the store: a new Parameter -> rebuilt buffer and sink
+                tr.texture_dc = torch.nn.Parameter(torch.ones(55, 3))
+            sync.zero()
+            res[f"rebuilt_{step}"] = sync.flat.data_ptr() != flat_before
+            tr.backward(rank)
+            sync.all_reduce()
+            res[f"after_rechart_{step}"] = bool(torch.allclose(tr.texture_dc.grad, mean_w * tr.texture_dc.detach()))
+        # a second backward without all_reduce() in between is refused
+        sync.zero()
+        tr.backward(rank)
+        try:
+            sync.zero()
+            res["double_backward_refused"] = False
+        except RuntimeError:
+            res["double_backward_refused"] = True
+        sync.all_reduce()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trainer_layout_sink_and_recharts_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, r in res:
+        for step in range(3):
+            assert r[f"tail_started_{step}"], "the texel collective must start from the raster backward"
+            assert r[f"ok_{step}"], f"rank {rank} step {step}: wrong averaged gradients"
+            assert r[f"after_rechart_{step}"], f"rank {rank} step {step}: wrong gradients after a rechart"
+        assert not r["rebuilt_0"], "an in-place rechart must keep the flat buffer"
+        assert r["rebuilt_1"], "a grown texel store must rebuild the flat buffer"
+        assert r["double_backward_refused"]
