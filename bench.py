@@ -3,23 +3,31 @@
 "train-step ms + rendered Mpix/s, 200k splats / 1e7 texels @ 800x800".
 
 One step = one full GStex training iteration per rank on synthetic random-init data
-(gstex_amd.model.GStexTrainer): activations -> project/AABB/tiles -> SH -> texture_gaussians
-fwd -> composite -> 0.8 L1 + 0.2 (1-SSIM) -> backward -> [RCCL all-reduce of the flat gradient
-buffer when N > 1] -> 7-group Adam.  Every rank renders its own camera (cfg4: one view per GPU).
+(gstex_amd.model.GStexTrainer): activations -> project/AABB/tiles -> SH (degree 3) -> texture_gaussians
+fwd -> composite -> 0.8 L1 + 0.2 (1-SSIM) -> backward -> [RCCL all-reduce of the flat gradient buffer when
+N > 1] -> 7-group Adam.  Rank r renders camera (r + step * N) mod 8 of 8 fixed sphere poses (the reference
+draws one random training camera per rank and step, full_images_datamanager.py:320-333).
+
+The workload is stationary: the geometry parameters that decide which (pixel, splat) pairs exist (means,
+log-scales, quaternions, opacity logits; 8.8 MB at cfg3) are restored from their initial values before every
+step, inside the timed region, so the pair counts and kernel times do not drift as the scene trains and the
+result does not depend on --steps / --warmup.  Colours, texels and the Adam moments keep training.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-Rank 0 prints ONE JSON line.  `value` = whole-job rendered+trained Mpix/s = N * H * W / step time.
-`roofline` prices the dominant raster kernel with SURVEY §8d's algorithmic bytes; `cpu_baseline`
-times the CPU oracle (oracle/, fp32 forward + autograd backward) on a bounded crop of the same view.
+Rank 0 prints ONE JSON line.  `value` = whole-job rendered+trained Mpix/s = N * H * W / (wall time / K).
+`roofline` prices the dominant raster kernel with SURVEY §8d's algorithmic bytes; `cpu_baseline` times the CPU
+oracle (oracle/, fp32 forward + autograd backward) on a bounded crop of the same view; `sub` holds the other
+configs' kernel times (cfg2 raster fwd+bwd, cfg1 forward), the eval render and a rechart.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -30,7 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_TAG = "r01"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+PROFILE_TAG = "r02"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+N_POSES = 8
 
 
 def pmc_row(kernel):
@@ -51,16 +60,16 @@ def pmc_row(kernel):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n-splats", type=int, default=200_000)
     p.add_argument("--n-texels", type=float, default=1e7)
     p.add_argument("--height", type=int, default=800)
     p.add_argument("--width", type=int, default=800)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-sub", action="store_true", help="skip the cfg1/cfg2/eval/rechart sub-records")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
-    p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="diagnostics only: no HIP events around the raster launches (no roofline figures)")
     return p.parse_args()
@@ -78,11 +87,30 @@ def algorithmic_bytes(nth, dims, H, W, C=3):
     return dict(N_v=Nv, I=I, T_v=Tv, P=P, fwd=fwd, bwd=bwd)
 
 
-def cpu_baseline(scene, view, crop, threads):
-    """Oracle (fp32 forward + autograd backward) on a crop x crop window at the image centre."""
+def cpu_threads():
+    """Host threads the CPU baseline uses: the CPUs this process may run on (sched affinity), capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box does: its per-GPU CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(n, 1)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def oracle_crop(scene, view, crop, bwd=True):
+    """Oracle (fp32 forward [+ autograd backward]) on a crop x crop window at the image centre; seconds."""
     from oracle import raster as O
 
-    torch.set_num_threads(threads)
     x0 = view.W // 2 - crop // 2
     y0 = view.H // 2 - crop // 2
     cam = O.Camera(view.viewmat, view.fx, view.fy, view.cx - x0, view.cy - y0, crop, crop, 16, view.c2w[:3, 3])
@@ -94,20 +122,113 @@ def cpu_baseline(scene, view, crop, threads):
     rgbs = torch.rand((scene.n, 3), generator=g)
     leaves = dict(rgbs=rgbs, opacities=opac.detach().clone(), means=means.detach().clone(),
                   scales=scales.detach().clone(), quats=quats.detach().clone(), texture=scene.texture.clone())
-    for t in leaves.values():
-        t.requires_grad_(True)
+    if bwd:
+        for t in leaves.values():
+            t.requires_grad_(True)
     inp = O.RasterInputs(scene.texture_dims, centers.detach(), extents, depths, leaves["rgbs"], leaves["opacities"],
                          leaves["means"], leaves["scales"], 1.0, leaves["quats"], uv0, umap, vmap, leaves["texture"],
                          cam)
     t0 = time.perf_counter()
     bins = O.bin_and_sort(inp.centers, inp.extents, inp.depths, crop, crop)
     out = O._render(inp, torch.float32, bins[1], bins[2], None)["out"]
-    loss = sum(v.sum() for k, v in out.items() if k in ("img", "tex", "alpha", "depth"))
-    loss.backward()
-    dt = time.perf_counter() - t0
+    if bwd:
+        loss = sum(v.sum() for k, v in out.items() if k in ("img", "tex", "alpha", "depth"))
+        loss.backward()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(scene, view, crop, threads):
+    torch.set_num_threads(threads)
+    dt = oracle_crop(scene, view, crop)
     return dict(value=round(crop * crop / dt / 1e6, 6), unit="Mpix/s", cores=threads, kind="port",
+                cpu_model=cpu_model(), os_cpu_count=os.cpu_count(),
                 sample=f"oracle fp32 fwd+bwd of a {crop}x{crop} centre crop of the same 800x800 view "
-                       f"({scene.n} splats, {scene.texture.shape[0]} texels), {dt:.1f} s wall")
+                       f"({scene.n} splats, {scene.texture.shape[0]} texels), {dt:.1f} s wall, 1 rep")
+
+
+def _events_ms(pairs):
+    return [a.elapsed_time(b) for a, b in pairs]
+
+
+def raster_only(n_splats, n_texels, H, W, reps, dev, backward=True, seed=42, opacity=0.1):
+    """Raster-only fwd(+bwd) median over `reps` on one sphere view: preprocessing
+    + binning + texture_gaussians forward [+ backward with img/alpha/tex upstream gradients ~ N(0, 1e-3)].
+    Returns per-kernel medians, the whole call's median and the roofline fraction of fwd+bwd."""
+    from gstex_amd import ops
+    from gstex_amd.scene import make_scene, sphere_view
+
+    sc = make_scene(n_splats, n_texels, seed=seed, opacity=opacity)
+    v = sphere_view(0, H, W).to(dev)
+    means, scales, quats, opac = [t.to(dev) for t in sc.activated()]
+    uv0, umap, vmap = [t.to(dev) for t in sc.uv_mapping()]
+    rgbs = torch.rand((sc.n, 3), device=dev)
+    tex = sc.texture.to(dev)
+    dims = sc.texture_dims.to(dev)
+    leaves = (means, scales, quats, opac, rgbs, tex)
+    if backward:
+        for t in leaves:
+            t.requires_grad_(True)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    ups = [torch.randn(s, generator=g).to(dev) * 1e-3 for s in [(H, W, 3), (H, W), (H, W, 3)]]
+    intr = (v.fx, v.fy, v.cx, v.cy)
+
+    def run():
+        _, depths = ops.project_points(means, v.viewmat, intr)
+        c, e = ops.get_aabb_2d(means, scales, 1, quats, v.viewmat, intr)
+        nth = ops.get_num_tiles_hit_2d(c, e, H, W, 16)
+        outs = ops.texture_gaussians((sc.n, 1, 3), dims, c, e, depths, nth, rgbs, opac, means, scales, 1, quats,
+                                     uv0, umap, vmap, tex, v.viewmat, v.c2w, v.fx, v.fy, v.cx, v.cy, H, W, 16,
+                                     (1 << 9) | (1 << 10), background=None, geometry_outputs=not backward)
+        if backward:
+            torch.autograd.backward([outs[0], outs[3], outs[4]], ups)
+            for t in leaves:
+                t.grad = None
+        return nth
+
+    with torch.no_grad() if not backward else torch.enable_grad():
+        nth = run()
+        torch.cuda.synchronize()
+        ops.set_kernel_timing(True)
+        whole = []
+        for _ in range(reps):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            run()
+            b.record()
+            whole.append((a, b))
+        kt = ops.kernel_times()
+        ops.set_kernel_timing(False)
+    ab = algorithmic_bytes(nth.cpu(), sc.texture_dims, H, W)
+    med = {k.replace("gstex_", ""): round(statistics.median(v_), 4) for k, v_ in kt.items()}
+    res = dict(n_splats=n_splats, n_texels=int(tex.shape[0]), H=H, W=W, reps=reps,
+               call_ms_median=round(statistics.median(_events_ms(whole)), 4), kernel_ms_median=med,
+               counts={k: ab[k] for k in ("N_v", "I", "T_v", "P")})
+    f_ms = med.get("raster_fwd")
+    b_ms = med.get("raster_bwd")
+    if f_ms:
+        res["fwd_hbm_frac"] = round(ab["fwd"] / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+    if f_ms and b_ms:
+        res["fwd_bwd_hbm_frac"] = round((ab["fwd"] + ab["bwd"]) / ((f_ms + b_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+    return res
+
+
+def eval_render_ms(trainer, view, reps):
+    """The reference's eval render (gstex.py:1165-1203, measure_fps False): three C = 6 raster calls per image
+    (main render, test-colour render, settings | 1 << 15 render), no gradient.  Median ms per image."""
+    times = []
+    with torch.no_grad():
+        trainer.eval_render(view)
+        torch.cuda.synchronize()
+        for _ in range(reps):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            trainer.eval_render(view)
+            b.record()
+            times.append((a, b))
+        torch.cuda.synchronize()
+    return statistics.median(_events_ms(times))
 
 
 def main():
@@ -130,49 +251,67 @@ def main():
     H, W = args.height, args.width
     t_scene = time.perf_counter()
     scene = make_scene(args.n_splats, args.n_texels, seed=args.seed)
-    view = sphere_view(rank, H, W, n_views=max(world, 8)).to(dev)
-    trainer = GStexTrainer(scene, dev)
+    views = [sphere_view(i, H, W, n_views=N_POSES).to(dev) for i in range(N_POSES)]
+    # start_step = 3 x sh_degree_interval: SH at its full degree 3 (the regime of 12k of the 15k iterations)
+    trainer = GStexTrainer(scene, dev, start_step=3000)
     sync = GradSync(trainer, world) if world > 1 else None
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-    gt = torch.rand((H, W, 3), generator=g).to(dev)
+    gts = [torch.rand((H, W, 3), generator=g).to(dev) for _ in range(N_POSES)]
+    geom = [trainer.means, trainer.scales, trainer.quats, trainer.opacities]
+    geom0 = [p.detach().clone() for p in geom]
     setup_s = time.perf_counter() - t_scene
+    step_no = [0]
 
     def step():
+        with torch.no_grad():  # stationary workload: same geometry every step (8.8 MB copy, timed)
+            for p, p0 in zip(geom, geom0):
+                p.copy_(p0)
+        pose = (rank + step_no[0] * world) % N_POSES
+        step_no[0] += 1
         if sync is not None:
             sync.zero()  # one fill of the flat gradient buffer the .grad views live in
         else:
             trainer.zero_grad()
-        trainer.forward_backward(view, gt)
+        trainer.forward_backward(views[pose], gts[pose])
         if sync is not None:
             sync.all_reduce()
         trainer.optimizer_step()
 
     for _ in range(args.warmup):
         step()
-    # counted quantities for the roofline (this rank's view, current parameters)
+    # counted quantities for the roofline (every pose of this rank's cycle, current parameters)
     with torch.no_grad():
-        means = trainer.means
         quats = trainer.quats / trainer.quats.norm(dim=-1, keepdim=True)
         s = torch.exp(trainer.scales[:, :-1])
         scales = torch.cat([s, 1e-5 * s.mean(-1, keepdim=True)], -1)
-        intr = (view.fx, view.fy, view.cx, view.cy)
-        c, e = ops.get_aabb_2d(means, scales, 1, quats, view.viewmat, intr)
-        nth = ops.get_num_tiles_hit_2d(c, e, H, W, 16)
-        ab = algorithmic_bytes(nth.cpu(), trainer.texture_dims.cpu(), H, W)
+        abs_ = []
+        for pose in sorted({(rank + k * world) % N_POSES for k in range(args.steps)}):
+            v = views[pose]
+            c, e = ops.get_aabb_2d(trainer.means, scales, 1, quats, v.viewmat, (v.fx, v.fy, v.cx, v.cy))
+            nth = ops.get_num_tiles_hit_2d(c, e, H, W, 16)
+            abs_.append(algorithmic_bytes(nth.cpu(), trainer.texture_dims.cpu(), H, W))
+        ab = {k: sum(a[k] for a in abs_) / len(abs_) for k in abs_[0]}
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ops.set_kernel_timing(not args.no_kernel_timing)
+    step_ev = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
         step()
+        b.record()
+        step_ev.append((a, b))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kt = ops.kernel_times()
     ops.set_kernel_timing(False)
+    step_ms = _events_ms(step_ev)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -181,6 +320,7 @@ def main():
     mpix = world * H * W / (elapsed / args.steps) / 1e6
 
     avg = {k: sum(v) / len(v) for k, v in kt.items()}
+    med = {k: statistics.median(v) for k, v in kt.items()}
     f_ms = avg.get("gstex_raster_fwd", float("nan"))
     b_ms = avg.get("gstex_raster_bwd", float("nan"))
     dom, dom_ms, dom_bytes = ("raster_bwd", b_ms, ab["bwd"]) if b_ms >= f_ms else ("raster_fwd", f_ms, ab["fwd"])
@@ -188,9 +328,8 @@ def main():
     roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
                     traffic_source=f"profiles/{PROFILE_TAG}_traffic.json",
-                    bytes_per_launch=dom_bytes, launch_ms=round(dom_ms, 4),
+                    bytes_per_launch=int(dom_bytes), launch_ms=round(dom_ms, 4),
                     fwd_bwd_frac=round((ab["fwd"] + ab["bwd"]) / ((f_ms + b_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
-
     prow = pmc_row(dom)
     if prow is not None:
         roofline["traffic"] = int(prow["hbm_bytes_per_launch"])
@@ -199,6 +338,36 @@ def main():
             roofline["valu_insts_per_launch"] = int(prow["valu_insts"])
             roofline["valu_issue_frac"] = round(prow["valu_insts"] / (dom_ms * 1e-3 * 1024 * 2.4e9 / 2), 4)
 
+    sub = None
+    if rank == 0 and world == 1 and not args.no_sub:
+        sub = {}
+        try:
+            # the full-output forward (depth / distortion / normal produced: the reference kernel's contract)
+            trainer.geometry_outputs = True
+            ops.set_kernel_timing(True)
+            with torch.no_grad():
+                for _ in range(10):
+                    trainer.render(views[0], sh_degree_now=3, composite=False)
+            kf = ops.kernel_times()
+            ops.set_kernel_timing(False)
+            trainer.geometry_outputs = False
+            sub["raster_fwd_full_outputs_ms"] = round(statistics.median(kf["gstex_raster_fwd"]), 4)
+            sub["eval_render"] = dict(ms_per_image=round(eval_render_ms(trainer, views[0], 10), 4),
+                                      raster_calls=3, channels=6, note="gstex.py:1165-1203, no grad")
+            sub["eval_render"]["fps"] = round(1e3 / sub["eval_render"]["ms_per_image"], 1)
+            rc = []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                trainer.recharge()
+                torch.cuda.synchronize()
+                rc.append((time.perf_counter() - t1) * 1e3)
+            sub["rechart_ms"] = round(statistics.median(rc), 3)
+            sub["cfg2_fwd_bwd"] = raster_only(50_000, 1e6, 800, 800, 20, dev)
+            sub["cfg1_fwd"] = raster_only(1_000, 0, 256, 256, 50, dev, backward=False)
+        except Exception as ex:  # sub-records must never kill the headline line
+            sub["error"] = repr(ex)
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -206,11 +375,20 @@ def main():
         return
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
+        th = cpu_threads()
         try:
             cpu = cpu_baseline(make_scene(args.n_splats, args.n_texels, seed=args.seed), sphere_view(0, H, W),
-                               args.cpu_crop, min(args.cpu_threads, os.cpu_count() or 1))
+                               args.cpu_crop, th)
+            if sub is not None:
+                torch.set_num_threads(th)
+                sc1 = make_scene(1_000, 0, seed=42)
+                t1 = [oracle_crop(sc1, sphere_view(0, 256, 256), 256, bwd=False) for _ in range(3)]
+                sub["cfg1_fwd"]["cpu_oracle_ms_median"] = round(1e3 * statistics.median(t1), 1)
+                sc2 = make_scene(50_000, 1e6, seed=42)
+                t2 = oracle_crop(sc2, sphere_view(0, 800, 800), 128)
+                sub["cfg2_fwd_bwd"]["cpu_oracle_128x128_crop_s"] = round(t2, 2)
         except Exception as ex:  # baseline must never kill the GPU result line
-            cpu = dict(value=None, unit="Mpix/s", cores=args.cpu_threads, kind="port", sample=f"failed: {ex!r}")
+            cpu = dict(value=None, unit="Mpix/s", cores=th, kind="port", sample=f"failed: {ex!r}")
     line = {
         "metric": "train-step ms + rendered Mpix/s, 200k splats/1e7 texels @800x800",
         "value": round(mpix, 4),
@@ -219,20 +397,29 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 4),
+        "ms_per_step_median": round(statistics.median(step_ms), 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seed 42 random-init splats, charted random texels, random target image)",
+        "data": "synthetic (seed 42 random-init splats, charted random texels, random target images)",
         "config": {
-            "workload": "cfg3 full GStex train step (fwd+loss+bwd+Adam), one 800x800 view per GPU",
-            "n_splats": args.n_splats, "n_texels": int(trainer.texture_dc.shape[0]), "H": H, "W": W,
+            "workload": "cfg3 full GStex train step (fwd+loss+bwd+Adam), one 800x800 view per GPU per step",
+            "n_splats": args.n_splats, "n_texels": int(trainer.n_texels), "H": H, "W": W,
             "views_per_step": world, "parallelism": f"dp{world}",
+            "cameras": f"rank r, step s: pose (r + s*N) mod {N_POSES} of {N_POSES} fixed sphere poses",
+            "stationary": "means/scales/quats/opacity logits restored before every step (timed); colours, texels "
+                          "and Adam moments train",
+            "sh_degree": trainer.sh_degree_now(), "settings": trainer.settings,
+            "geometry_outputs": trainer.geometry_outputs,
+            "fold_aabb": True, "texture_transform": "SH2RGB on read (0.28209479, 0.5)",
         },
         "roofline": roofline,
         "cpu_baseline": cpu,
         "kernel_ms": {k.replace("gstex_", ""): round(v, 4) for k, v in avg.items()},
-        "counts": {k: ab[k] for k in ("N_v", "I", "T_v", "P")},
+        "kernel_ms_median": {k.replace("gstex_", ""): round(v, 4) for k, v in med.items()},
+        "counts": {k: int(ab[k]) for k in ("N_v", "I", "T_v", "P")},
+        "sub": sub,
         "setup_s": round(setup_s, 1),
     }
     print(json.dumps(line), flush=True)

@@ -140,6 +140,7 @@ class GStexTrainer:
         # into, and the callback that starts its collective (None: autograd owns the texel gradient)
         self.texture_grad_sink = None
         self.texture_grad_ready = None
+        self.test_colors = None  # eval-render test colours (gstex.py:309)
         self._build_optimizer()
 
     # ------------------------------------------------------------------ parameters
@@ -209,6 +210,54 @@ class GStexTrainer:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
                                      0.0, 1.0)
         return out
+
+    @torch.no_grad()
+    def eval_render(self, view: View, edit_texture: torch.Tensor | None = None):
+        """The reference's eval render (get_outputs with extra_stuff, gstex.py:1086-1203): a 6-channel texture
+        [SH2RGB(texture_dc), 0, 0, 0] and three raster calls -- the image, the test-colour render with
+        thresholded opacities (test_img / uv_im) and the settings | 1 << 15 render (edit_img, clean normals)."""
+        means = self.means
+        quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
+            means, self.quats, self.scales, self.opacities, self.mappings, view.c2w[:3, 3])
+        if self.fix_init and self.sh_degree > 0:
+            viewdirs = torch.stack([viewdirs[:, 0], -viewdirs[:, 2], viewdirs[:, 1]], -1)
+        intr = (view.fx, view.fy, view.cx, view.cy)
+        _, depths = ops.project_points(means, view.viewmat, intr)
+        centers, extents = ops.get_aabb_2d(means, scales, 1, quats, view.viewmat, intr)
+        nth = ops.get_num_tiles_hit_2d(centers, extents, view.H, view.W, ops.BLOCK_WIDTH)
+        n = means.shape[0]
+        rgbs = (sh_rest(self.sh_degree_now(), viewdirs, self.features_rest) if self.sh_degree > 0
+                else torch.sigmoid(self.features_dc))
+        tex6 = torch.zeros((self.texture_dc.shape[0], 6), device=means.device)
+        tex6[:, 0:3] = SH2RGB(self.texture_dc)
+        if self.test_colors is None or self.test_colors.shape[0] != n:
+            g = torch.Generator(device="cpu").manual_seed(0)
+            self.test_colors = torch.rand((n, 3), generator=g).to(means.device)  # gstex.py:309
+        bgz = torch.zeros_like(self.background)
+
+        def tg(cr, ct, co, st):
+            return ops.texture_gaussians(
+                (n, 1, 6), self.texture_dims, centers, extents, depths, nth, cr, co, means, scales, 1, quats, uv0,
+                umap, vmap, ct, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
+                ops.BLOCK_WIDTH, st, background=bgz)
+
+        img, depth, reg, alpha, tex, normal = tg(rgbs, tex6, opacities, self.settings)
+        upd = torch.zeros_like(tex6)
+        upd[:, 3:] = tex6[:, 3:]
+        if edit_texture is not None:
+            upd[:, :3] = edit_texture
+        test_op = opacities.clone()
+        test_op[test_op <= 0.5] = 0.0
+        test_op[test_op > 0.2] = 1.0
+        t_out = tg(self.test_colors, upd, test_op, self.settings)
+        n_out = tg(self.test_colors, upd, opacities, self.settings | (1 << 15))
+        bg = self.background[None, None, :]
+        rgb = torch.clamp(img + tex[..., 0:3] + (1 - alpha[..., None]) * bg, 0.0, 1.0)
+        return dict(rgb=rgb, depth=depth, alpha=alpha, normal=normal,
+                    test_img=t_out[0] + (1 - t_out[3][..., None]) * bg,
+                    uv_im=torch.clamp(t_out[4][..., 3:6] + (1 - t_out[3][..., None]) * bg, 0.0, 1.0),
+                    edit_img=torch.clamp(img + n_out[4][..., :3] + (1 - alpha[..., None]) * bg, 0.0, 1.0),
+                    clean_normal_img=torch.clamp(0.5 * (n_out[5] + 1) + (1 - alpha[..., None]) * bg, 0.0, 1.0))
 
     def loss(self, rgb: torch.Tensor, gt: torch.Tensor, ssim_lambda: float = 0.2) -> torch.Tensor:
         l1 = torch.abs(gt - rgb).mean()

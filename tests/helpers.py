@@ -123,3 +123,46 @@ def grad_norm_err(g, ref):
         return 0.0
     n = ref.double().norm().item()
     return (g.double() - ref.double()).norm().item() / max(n, 1e-30)
+
+
+_SCENES: dict = {}
+
+
+def make_window_case(n, n_texels, H, W, win, seed=42, view=0, C=3, settings=(1 << 9) | (1 << 10), opacity=0.1):
+    """A win x win window at the centre of the H x W sphere view `view` of the seeded make_scene(n, n_texels)
+    (the bench scenes: cfg3 = 200k / 1e7 / 800x800, cfg2 = 50k / 1e6 / 800x800): the camera's principal point
+    is shifted by the window origin (the bench's cpu_baseline crop), and only the splats that reach the window
+    are kept, their texel blocks repacked contiguously (same texels, offsets re-based) -- the other splats
+    contribute nothing to these pixels.  Returns a Case usable by oracle_run / gpu_run."""
+    from gstex_amd.scene import View
+
+    key = (n, n_texels, seed, opacity)
+    if key not in _SCENES:
+        _SCENES.clear()
+        _SCENES[key] = make_scene(n, n_texels, channels=C, seed=seed, opacity=opacity)
+    sc = _SCENES[key]
+    full = sphere_view(view, H, W)
+    x0, y0 = W // 2 - win // 2, H // 2 - win // 2
+    v = View(full.viewmat, full.c2w, full.fx, full.fy, full.cx - x0, full.cy - y0, win, win)
+    means, scales, quats, opac = sc.activated()
+    cam = O.Camera(v.viewmat, v.fx, v.fy, v.cx, v.cy, win, win, 16, v.c2w[:3, 3])
+    centers, extents = O.aabb_2d(means, scales, 1.0, quats, cam)
+    nth = O.num_tiles_hit(centers, extents, win, win)
+    keep = torch.nonzero(nth > 0).squeeze(1)
+    dims = sc.texture_dims[keep].clone()
+    hw = (dims[:, 0].long() * dims[:, 1].long())
+    rows = torch.cat([torch.arange(int(o), int(o) + int(s)) for o, s in zip(sc.texture_dims[keep, 2].tolist(),
+                                                                            hw.tolist())]) if keep.numel() else \
+        torch.zeros(0, dtype=torch.long)
+    dims[:, 2] = (torch.cumsum(hw, 0) - hw).to(torch.int32)
+    texture = sc.texture[rows].clone() if rows.numel() else torch.zeros((0, C))
+    uv0, umap, vmap = sc.uv_mapping()
+    means, scales, quats, opac = means[keep], scales[keep], quats[keep], opac[keep]
+    _, depths = O.project_points(means, cam)
+    g = torch.Generator().manual_seed(seed + 1000)
+    rgbs = torch.rand((sc.n, 3), generator=g)[keep]
+    inp = O.RasterInputs(dims, centers[keep].detach().clone(), extents[keep], depths, rgbs,
+                         opac.detach().clone(), means.detach().clone(), scales.detach().clone(), 1.0,
+                         quats.detach().clone(), uv0[keep].detach().clone(), umap[keep], vmap[keep], texture, cam,
+                         settings, None)
+    return Case(inp, v, C, nth[keep])

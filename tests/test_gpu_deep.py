@@ -1,0 +1,73 @@
+"""HIP path vs the CPU oracle at the tile depths of the benchmark configurations: the
+tolerances of test_gpu_parity.py, on windows of the bench scenes themselves.
+
+* cfg3 (200k splats, 1e7 texels, 800x800): the 96x96 window at the image centre, ~1,900 splats per tile --
+  the forward's batch loop runs >10 batches and the backward's reverse walk >100, with transmittance
+  saturation (early termination) inside the lists;
+* cfg2 (50k splats, 1e6 texels, 800x800): the 128x128 centre window;
+* cfg1 exactly (1k splats, 0 texels = 2DGS mode, 256x256): the whole image.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import DIFF, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, make_window_case, \
+    oracle_run
+from test_gpu_parity import COND_FACTOR, GRAD_RTOL, _report
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(name, case, outputs=None, min_depth=0):
+    o32, o64, aux, og = oracle_run(case, grads=True, outputs=outputs)
+    tr = np.asarray(aux["tile_ranges"])
+    depth = int((tr[:, 1] - tr[:, 0]).max()) if tr.size else 0
+    print(f"[deep] {name}: {case.inp.means.shape[0]} splats, {case.inp.texture.shape[0]} texels, "
+          f"max tile list {depth}, mean {float((tr[:, 1] - tr[:, 0]).mean()):.0f}")
+    assert depth >= min_depth, f"{name}: tile lists only {depth} deep"
+    gout, gg = gpu_run(case, grads=True, outputs=outputs)
+    _report(f"{name} fwd", {k: (gout[k].double() - o64[k]).abs().max().item() for k in gout})
+    assert_close_fwd(gout, o64)
+    # the transmittance saturates inside the lists (pixels stop before their tile's last splat)
+    last = np.asarray(aux["last"])
+    _, _, _, og32 = oracle_run(case, grads=True, grad_dtype=torch.float32, outputs=outputs)
+    errs, norm_errs, inh, inh_n = {}, {}, {}, {}
+    for k in DIFF:
+        errs[k], _ = grad_rel_err(gg[k], og[k])
+        inh[k], _ = grad_rel_err(og32[k], og[k])
+        norm_errs[k] = grad_norm_err(gg[k], og[k])
+        inh_n[k] = grad_norm_err(og32[k], og[k])
+    _report(f"{name} bwd norm-rel", norm_errs)
+    _report(f"{name} bwd max-rel", errs)
+    _report(f"{name} bwd fp32-oracle norm-rel", inh_n)
+    for k in DIFF:
+        nb = max(GRAD_RTOL, COND_FACTOR * inh_n[k])
+        assert norm_errs[k] <= nb, f"{name}: grad {k} norm-wise rel err {norm_errs[k]:.3e} > {nb:.3e}"
+        bound = max(GRAD_RTOL, COND_FACTOR * inh[k])
+        assert errs[k] <= bound, f"{name}: grad {k} max rel err {errs[k]:.3e} > {bound:.3e}"
+    return tr, last
+
+
+def test_cfg3_centre_window_deep_tiles():
+    case = make_window_case(200_000, 1e7, 800, 800, 96)
+    tr, last = _check("cfg3 96x96", case, outputs=("img", "alpha", "tex"), min_depth=1500)
+    # early termination happens: some pixel stops well before its tile's last splat
+    lens = tr[:, 1] - tr[:, 0]
+    assert int(last.max()) > 1000 and int((last < lens.max() - 100).sum()) > 0
+
+
+def test_cfg3_centre_window_all_outputs():
+    case = make_window_case(200_000, 1e7, 800, 800, 48)
+    _check("cfg3 48x48 all outputs", case, min_depth=1500)
+
+
+def test_cfg2_centre_window():
+    case = make_window_case(50_000, 1e6, 800, 800, 128)
+    _check("cfg2 128x128", case, min_depth=200)
+
+
+def test_cfg1_exact():
+    # BASELINE cfg1: 1k random splats, 0 texels (pixel_num = 0, 2DGS mode), 256 x 256, the whole image
+    case = make_case(n=1000, n_texels=0, H=256, W=256, seed=42, opacity=0.1)
+    assert case.inp.texture.shape[0] == 0 and int(case.inp.texture_dims.abs().sum()) == 0
+    _check("cfg1 256x256", case)
