@@ -77,16 +77,22 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_REC_SGPR
 #define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
 #endif
+// Backward occupancy: waves per SIMD the register allocation targets, per instantiation.  The photometric
+// training variant (C = 3, no geometry gradients) fits 5 waves (96 VGPRs, a few scratch spills; 5 workgroups
+// per CU need <= 32 KiB of LDS each, so its texel staging is smaller); the others keep 4.
+#ifndef GSTEX_BWD_WAVES_TRAIN
+#define GSTEX_BWD_WAVES_TRAIN 5
+#endif
 #ifndef GSTEX_BWD_WAVES
-#define GSTEX_BWD_WAVES 4  // register cap for this many waves per SIMD (a few scratch spills)
+#define GSTEX_BWD_WAVES 4
 #endif
-#if GSTEX_BWD_WAVES > 0
-// gfx950's unified register file: the amdgpu_num_vgpr budget is doubled (arch VGPRs + AGPRs), so a
-// cap of 512/waves registers (allocation granule 8) is requested as half that
-#define GSTEX_BWD_ATTR __attribute__((amdgpu_num_vgpr((512 / GSTEX_BWD_WAVES) / 8 * 8 / 2)))
-#else
-#define GSTEX_BWD_ATTR
-#endif
+template <int C, bool GEO>
+struct BwdShape {
+    static constexpr bool kTrain = (C == 3 && !GEO);
+    static constexpr int kWaves = kTrain ? GSTEX_BWD_WAVES_TRAIN : GSTEX_BWD_WAVES;
+    // int64 texel-staging values per workgroup: what kWaves workgroups per CU leave of the 160 KiB
+    static constexpr int kTexCap = kWaves >= 5 ? 3200 : 4032;
+};
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #ifndef GSTEX_ABLATE
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
@@ -708,10 +714,7 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
 // GEO = false: no depth / distortion / normal upstream gradient (all NULL, the training default:
 // gstex.py:198-201 sets both weights to 0), so every term they scale is dropped at compile time.  The
 // remaining arithmetic is unchanged (x + 0 * y = x), so both variants give the same values.
-#ifndef GSTEX_TEX_LDS
-#define GSTEX_TEX_LDS 4032  // int64 staging values per workgroup: what four workgroups per CU leave of the 160 KiB
-#endif
-constexpr int kTexCap = GSTEX_TEX_LDS;
+
 
 // Texel-gradient fixed point: per tile, e = exponent of max |dL/dtex * tex_scale| over its pixels (< 2^e).  A
 // pixel's contribution w b g (w, b <= 1) is < 2^e and a run tail of the 8-lane row scan < 2^(e+3); both are
@@ -726,7 +729,7 @@ __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^
 }
 
 template <int C, bool GEO>
-__global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
+__global__ __launch_bounds__(kThreads, (BwdShape<C, GEO>::kWaves)) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots, const float* __restrict__ texture,
@@ -738,6 +741,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_BWD_ATTR void raster_bwd_kernel(
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
     __shared__ float s_part[kBwdBatch][4][kNP];
+    constexpr int kTexCap = BwdShape<C, GEO>::kTexCap;
     __shared__ unsigned long long s_texq[kTexCap];
     __shared__ unsigned s_live[4];  // per wave: batch splats whose s_part row this wave wrote
     __shared__ int s_gexp;

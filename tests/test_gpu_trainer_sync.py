@@ -1,0 +1,62 @@
+"""GStexTrainer + FusedAdam + GradSync on the GPU (world size 1 over RCCL): the synced step -- flat gradient
+buffer, the raster backward accumulating the texel gradient straight into its slice, the tail collective
+started from the backward -- must train exactly like the un-synced step, across an in-place rechart.
+(World size > 1 is covered on CPU by tests/test_dist.py; the driver runs the 8-GPU bench.)"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_synced_step_matches_unsynced_across_rechart():
+    from gstex_amd.dist import GradSync
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        sc = make_scene(4000, 80_000, seed=3)
+        views = [sphere_view(i, 96, 96).to(dev) for i in range(3)]
+        g = torch.Generator().manual_seed(0)
+        gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(3)]
+        plain = GStexTrainer(sc, dev, start_step=3000)
+        synced = GStexTrainer(sc, dev, start_step=3000)
+        sync = GradSync(synced, 1)
+        store = synced.texture_dc
+        for step in range(4):
+            plain.zero_grad()
+            plain.forward_backward(views[step % 3], gts[step % 3])
+            plain.optimizer_step()
+            sync.zero()
+            synced.forward_backward(views[step % 3], gts[step % 3])
+            assert synced.texture_grad_sink is not None and synced.texture_dc.grad.data_ptr() == \
+                sync.flat[sync._tail_off:].data_ptr()
+            sync.all_reduce()
+            synced.optimizer_step()
+            if step == 1:
+                plain.recharge()
+                synced.recharge()
+        # a rechart that fits the store keeps the Parameter (and the flat buffer); one that needs more grows it
+        assert (synced.texture_dc is store) == (synced.n_texels <= store.shape[0])
+        assert synced.texture_dc.shape == plain.texture_dc.shape
+        for (name, a), b in zip(plain.param_groups().items(), synced.param_groups().values()):
+            a, b = a[0].detach().double(), b[0].detach().double()
+            # texel gradients combine tiles with fp32 atomics (summation order): tiny differences, then Adam
+            err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-30)
+            assert err < 1e-5, f"{name}: synced step differs ({err:.2e})"
+    finally:
+        dist.destroy_process_group()
