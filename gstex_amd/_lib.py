@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 REC_FLOATS = 32
 PARTIAL_FLOATS = 24
 SETTING_AA_BLUR = 1 << 9
@@ -85,15 +85,15 @@ SIGNATURES = {
     "gstex_raster_bwd": (
         c_int32,
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
-         _P, _P, _P, _P],
+         c_int64, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_setup_bwd": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_setup_bwd_aabb": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_sh_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),

@@ -6,7 +6,12 @@
 // (alpha >= 1/255, T < 1e-4, z >= near) agree between the GPU and the CPU oracle.
 //
 // Semantics follow the call-site contracts of the reference (nerfstudio/models/gstex.py) and the
-// 2DGS formulation its argument list implies.
+// 2DGS formulation its argument list implies.  Pixel (x, y) is evaluated at its
+// centre (x + 0.5, y + 0.5): the reference's own depths_to_points (gstex.py:138-139) maps rendered pixel
+// (i, j) to the ray through ((j + 0.5 - cx) / fx, (i + 0.5 - cy) / fy), which its normal loss compares
+// with the rendered normal (gstex.py:1219, 1313); 2DGS, whose depths_to_points has no +0.5, evaluates at
+// the integer point instead (lineage table).
+
 #pragma once
 
 #include <hip/hip_runtime.h>

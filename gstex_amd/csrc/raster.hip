@@ -81,29 +81,30 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 // training variant (C = 3, no geometry gradients) fits 5 waves (96 VGPRs, a few scratch spills; 5 workgroups
 // per CU need <= 32 KiB of LDS each, so its texel staging is smaller); the others keep 4.
 #ifndef GSTEX_BWD_WAVES_TRAIN
-#define GSTEX_BWD_WAVES_TRAIN 5
+#define GSTEX_BWD_WAVES_TRAIN 6
 #endif
 #ifndef GSTEX_BWD_WAVES
-#define GSTEX_BWD_WAVES 4
+#define GSTEX_BWD_WAVES 5
 #endif
 template <int C, bool GEO>
 struct BwdShape {
     static constexpr bool kTrain = (C == 3 && !GEO);
     static constexpr int kWaves = kTrain ? GSTEX_BWD_WAVES_TRAIN : GSTEX_BWD_WAVES;
-    // int64 texel-staging values per workgroup: what kWaves workgroups per CU leave of the 160 KiB
-    static constexpr int kTexCap = kWaves >= 5 ? 3200 : 4032;
 };
+// Backward per-wave texel staging: one splat's texel block (h * w * C int32 fixed-point entries) at a time, 6 KiB
+// per wave (24 waves per CU use 144 of the 160 KiB); a larger block adds its run tails straight to global memory.
+// (int64 staging at 2^-27 measured 0.15 ms slower at cfg3: ds_add_u64 moves twice the LDS data.)
+#ifndef GSTEX_TEX_STAGE
+#define GSTEX_TEX_STAGE 1536
+#endif
+constexpr int kTexStage = GSTEX_TEX_STAGE;
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #ifndef GSTEX_ABLATE
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
                         // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
-                        // 128 = no barrier before the combine (timing experiments only: racy)
+                        // (backward ablations skip work: timing experiments only)
 #endif
-#ifndef GSTEX_BWD_BATCH
-#define GSTEX_BWD_BATCH 16
-#endif
-constexpr int kBwdBatch = GSTEX_BWD_BATCH;
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
 
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     const WaveBlock wb = wave_block(tx, ty, tid);
     const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
-    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
+    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;  // pixel centres (gstex_common.h)
     const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
@@ -571,6 +572,15 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     for (int c = 0; c < CM; ++c)
         if (c < Cn) out_tex[(size_t)Cn * pix + c] = tex[c];
     if (GEOF) {
+        if (settings & GSTEX_SETTING_EVAL_NORMAL) {
+            // bit 15 (gstex.py:1198-1203, the eval "clean normal" render): the accumulated normal is returned
+            // as a unit vector (0 where nothing was accumulated); every other output is unchanged
+            const float n2 = (nrm[0] * nrm[0] + nrm[1] * nrm[1]) + nrm[2] * nrm[2];
+            const float inv = n2 > 0.0f ? 1.0f / sqrtf(n2) : 0.0f;
+            nrm[0] = nrm[0] * inv;
+            nrm[1] = nrm[1] * inv;
+            nrm[2] = nrm[2] * inv;
+        }
         out_normal[3 * pix + 0] = nrm[0];
         out_normal[3 * pix + 1] = nrm[1];
         out_normal[3 * pix + 2] = nrm[2];
@@ -705,55 +715,62 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     return key >= 0 && (ns != seg || pos == SW - 1);
 }
 
-// Backward: one 256-thread workgroup (4 wave64, one 8x8 quadrant each) per tile, the tile list walked back to
-// front in batches of kBwdBatch splats.  Per visited splat each wave reduces its 24 gradient partials across
-// its 64 pixels; after the batch the four waves' rows are combined in a fixed wave order and stored (plain
-// stores) at the pair's emission slot, where gstex_raster_setup_bwd sums each splat's rows in slot order
-// (bitwise reproducible), and the batch's fixed-point texel staging is flushed by all four waves.
+// Backward: one wave64 workgroup per (tile, 8x8 quadrant) -- the 4 quadrant waves of a tile share nothing, so
+// no wave ever waits for another (no barriers; a finished wave frees its slot at once).  The wave walks the
+// tile list back to front over the forward's cull bits for its quadrant, up to its last contributor.  Per
+// visited splat it reduces its 24 gradient partials across its 64 pixels and stores them with plain stores as
+// the (pair, quadrant) row partials[slot][quadrant] (slot = the pair's emission slot), flagging the row in
+// row_flags[slot] (byte = quadrant; rows never written stay unflagged and are never read);
+// gstex_raster_setup_bwd sums each splat's flagged rows in (slot, quadrant) order -> bitwise reproducible,
+// no float atomics for splat gradients.  Texel gradients: segmented scan along each 8-pixel row, run tails
+// added to the splat's texel block staged in the wave's LDS as int32 fixed point (exact, order-independent),
+// and the block flushed to v_texture (global float atomics, non-zero entries only) right after the visit.
 //
 // GEO = false: no depth / distortion / normal upstream gradient (all NULL, the training default:
 // gstex.py:198-201 sets both weights to 0), so every term they scale is dropped at compile time.  The
 // remaining arithmetic is unchanged (x + 0 * y = x), so both variants give the same values.
 
-
-// Texel-gradient fixed point: per tile, e = exponent of max |dL/dtex * tex_scale| over its pixels (< 2^e).  A
-// pixel's contribution w b g (w, b <= 1) is < 2^e and a run tail of the 8-lane row scan < 2^(e+3); both are
-// rounded to integers at scale 2^S, S = 27 - e (|q| < 2^30: one v_cvt_rpi_i32_f32, sign-extended), and summed
-// exactly as int64 in LDS (order-independent; a (tile, splat) entry holds at most 256 pixel contributions,
-// < 2^35).  Resolution: 2^-27 of the tile's largest upstream texel gradient.
-constexpr int kTexFixBits = 27;
+// Texel-gradient fixed point: per wave, e = exponent of max |dL/dtex * tex_scale| over its 64 pixels (< 2^e).  A
+// pixel's contribution w b g to a staged entry is < 2^e (w, b <= 1), so one visit adds < 2^(e+6) to an entry.
+// Contributions are formed at scale 2^S, S = 25 - e; each run tail of the 8-lane row scan (< 2^(S+e+3) = 2^28)
+// is rounded to int32 (one v_cvt_rpi_i32_f32) and the tails are summed exactly in int32 (|sum| < 0.99 * 2^31).
+// Resolution: 2^-25 of the wave's largest upstream texel gradient.
+constexpr int kTexFixBits = 25;
 __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^S; round half up, one VALU op
     int q;
     asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(q) : "v"(y));
     return q;
 }
 
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
 template <int C, bool GEO>
-__global__ __launch_bounds__(kThreads, (BwdShape<C, GEO>::kWaves)) void raster_bwd_kernel(
+__global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots, const float* __restrict__ texture,
     int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
-    float* __restrict__ v_texture, const unsigned long long* __restrict__ visit_masks) {
+    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture,
+    const unsigned long long* __restrict__ visit_masks) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
-    __shared__ float s_part[kBwdBatch][4][kNP];
-    constexpr int kTexCap = BwdShape<C, GEO>::kTexCap;
-    __shared__ unsigned long long s_texq[kTexCap];
-    __shared__ unsigned s_live[4];  // per wave: batch splats whose s_part row this wave wrote
-    __shared__ int s_gexp;
-    __shared__ int s_maxlast;
+    __shared__ int s_texq[kTexStage];
 
-    const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
+    const int quad = blockIdx.x & 3;
+    const int tile = tile_order ? tile_order[blockIdx.x >> 2] : (int)(blockIdx.x >> 2);  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const WaveBlock wb = wave_block(tx, ty, tid);
+    const int lane = threadIdx.x;
+    const WaveBlock wb = wave_block(tx, ty, quad * 64 + lane);
     const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
-    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
+    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;  // pixel centres (gstex_common.h)
     const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
     const bool dreg = (settings & GSTEX_SETTING_DIST_REG) != 0;
     const int2 rng = tile_ranges[tile];
@@ -781,106 +798,50 @@ __global__ __launch_bounds__(kThreads, (BwdShape<C, GEO>::kWaves)) void raster_b
             if (v_normal) { Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2]; }
         }
     }
+    // the wave's last contributor: pairs behind it receive no gradient from this quadrant (no row, no flag)
+    const int wave_last = wave_max_i(last);
+    if (wave_last < 0) return;
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
     float Gtex_bias = 0.f;  // tex_bias * sum_c dL/dtex[c]: the bias part of sum_c dL/dtex[c] * texel value
 #pragma unroll
     for (int c = 0; c < CM; ++c) Gtex_bias += Gtex[c];
     Gtex_bias *= tex_bias;
-
-    if (tid == 0) {
-        s_maxlast = -1;
-        s_gexp = 0;  // bits of max |dL/dtex| over the tile (non-negative floats order as ints)
-    }
-    for (int i = tid; i < kTexCap; i += kThreads) s_texq[i] = 0ull;
-    __syncthreads();
-    if (last >= 0) atomicMax(&s_maxlast, last);
+    int tex_S;
     {
         float gm = 0.f;
 #pragma unroll
         for (int c = 0; c < CM; ++c) gm = fmaxf(gm, fabsf(Gtex[c]));
         gm *= fabsf(tex_scale);
-        if (gm > 0.f) atomicMax(&s_gexp, __float_as_int(gm));
-    }
-    __syncthreads();
-    const int tile_last = s_maxlast;
-    int tex_S;
-    {
+        const float gmax = __int_as_float(wave_max_i(__float_as_int(gm)));  // non-negative floats order as ints
         int e = 0;
-        const float gmax = __int_as_float(s_gexp);
         if (gmax > 0.f) (void)frexpf(gmax, &e);  // gmax < 2^e
         tex_S = kTexFixBits - e;
     }
     // texel-gradient contributions are formed directly in the fixed-point scale
     const float tex_scale_q = __builtin_ldexpf(tex_scale, tex_S);
+    for (int i = lane; i < kTexStage; i += 64) s_texq[i] = 0;
     const size_t vm_base = visit_mask_base(rng.x, tile);
-    int wave_last = last;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wave_last = max(wave_last, __shfl_xor(wave_last, o, 64));
-    wave_last = __builtin_amdgcn_readfirstlane(wave_last);
 
-    // pairs after the last contributor of the tile receive zero gradient
-    for (int p = rng.x + tile_last + 1 + tid; p < rng.y; p += kThreads) {
-        float4* dst = reinterpret_cast<float4*>(partials + (size_t)sorted_slots[p] * kNP);
-#pragma unroll
-        for (int k = 0; k < kNP / 4; ++k) dst[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-
-    // Batch metadata lives in registers, lane j <-> splat j of the batch: splat id, emission slot and texel block
-    // (h, w, off: plane 6 of the record).  The next batch's ids and slots are loaded at the start of a batch and
-    // its block dims after the visits, so a batch needs no LDS staging and no barrier before its visits.
-    int cur_gid = 0, cur_slot = 0;
-    float4 cur_dims = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tile_last >= 0) {
-        const int bb0 = tile_last / kBwdBatch;
-        if (lane < min(kBwdBatch, tile_last - bb0 * kBwdBatch + 1)) {
-            cur_gid = sorted_ids[rng.x + bb0 * kBwdBatch + lane];
-            cur_slot = sorted_slots[rng.x + bb0 * kBwdBatch + lane];
-            cur_dims = records[(size_t)cur_gid * kRecF4 + 6];
+    for (int wd = wave_last >> 6; wd >= 0; --wd) {
+        const int pos0 = wd << 6;
+        // the word's splats this wave visits: the forward's cull bits for this quadrant (every splat when the
+        // forward recorded none), clipped to the wave's last contributor
+        unsigned long long todo = visit_masks ? visit_masks[(vm_base + wd) * 4 + quad] : ~0ull;
+        const int lim = wave_last - pos0 + 1;
+        if (lim < 64) todo &= (1ull << lim) - 1ull;
+        if (!todo) continue;
+        // lane k <-> position pos0 + k: splat id and emission slot, loaded once per word (coalesced)
+        int my_gid = 0, my_slot = 0;
+        if ((todo >> lane) & 1ull) {
+            my_gid = sorted_ids[rng.x + pos0 + lane];
+            my_slot = sorted_slots[rng.x + pos0 + lane];
         }
-    }
-
-    for (int bb = tile_last / kBwdBatch; bb >= 0 && tile_last >= 0; --bb) {
-        const int b0 = rng.x + bb * kBwdBatch;
-        const int nb = min(kBwdBatch, tile_last - bb * kBwdBatch + 1);
-        // next batch (always a full one below the top batch): ids and slots now, block dims after the visits
-        int nx_gid = 0, nx_slot = 0;
-        if (bb > 0 && lane < kBwdBatch) {
-            nx_gid = sorted_ids[b0 - kBwdBatch + lane];
-            nx_slot = sorted_slots[b0 - kBwdBatch + lane];
-        }
-        // place the batch's texel blocks in LDS: prefix of h*w*C over the batch, computed by every wave for
-        // itself (lane j <-> splat j; no barrier); splats past the capacity accumulate straight into global memory
-        int my_toff, nfit;
-        {
-            int sz = 0;
-            if (lane < nb) sz = __float_as_int(cur_dims.x) * __float_as_int(cur_dims.y) * Cn;
-            int incl = sz;
-#pragma unroll
-            for (int o = 1; o < kBwdBatch; o <<= 1) {
-                const int t = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += t;
-            }
-            const bool fits = incl <= kTexCap;
-            my_toff = (lane < nb && fits) ? incl - sz : -1;
-            nfit = __popcll(__ballot(fits && lane < nb));
-        }
-        // the batch splats this wave visits: the forward's cull bits for this wave (one wave-uniform word),
-        // clipped to its last contributor (every splat when the forward recorded none)
-        unsigned todo;
-        {
-            const int pos = bb * kBwdBatch;
-            const unsigned long long vw = visit_masks ? visit_masks[(vm_base + (pos >> 6)) * 4 + wave] : ~0ull;
-            const int lim = min(nb, wave_last - pos + 1);
-            const unsigned keep = lim <= 0 ? 0u : (lim >= 32 ? ~0u : (1u << lim) - 1u);
-            todo = (unsigned)(vw >> (pos & 63)) & ((1u << kBwdBatch) - 1u) & keep;
-        }
-        unsigned live = 0u;
         while (todo) {
-            const int j = 31 - __builtin_clz(todo);
-            todo &= ~(1u << j);
-            const int rel = bb * kBwdBatch + j;
-            const Rec r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(cur_gid, j) * kRecF4);
+            const int j = 63 - __builtin_clzll(todo);
+            todo &= ~(1ull << j);
+            const int rel = pos0 + j;
+            const Rec r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(my_gid, j) * kRecF4);
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
@@ -1002,22 +963,23 @@ __global__ __launch_bounds__(kThreads, (BwdShape<C, GEO>::kWaves)) void raster_b
                 P[P_TW + 1] = (dTw.y - h.dx * nk.y) - h.dy * nl.y;
                 P[P_TW + 2] = (dTw.z - h.dx * nk.z) - h.dy * nl.z;
             }
-            const bool any = __any(contrib);
-            if (GSTEX_ABLATE & 2) {
+            if (__any(contrib)) {
+                if (GSTEX_ABLATE & 2) {
 #pragma unroll
-                for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
-            } else if (any) {
-                wave_reduce24(P);
-            }
-            if (any) {
-                live |= 1u << j;
+                    for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
+                } else {
+                    wave_reduce24(P);
+                }
+                // the (pair, quadrant) row: lanes 8k hold 3 consecutive values each; the flag marks it written
+                const int slot = __builtin_amdgcn_readlane(my_slot, j);
                 if ((lane & 7) == 0) {
                     const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
-                    float* dst = &s_part[j][wave][base];
+                    float* dst = partials + ((size_t)slot * 4 + quad) * kNP + base;
                     dst[0] = P[0];
                     dst[1] = P[1];
                     dst[2] = P[2];
                 }
+                if (lane == 0) row_flags[(size_t)slot * 4 + quad] = 1;
             }
             if (__any(tkey >= 0)) {
                 float tg[4 * CM];
@@ -1035,29 +997,27 @@ __global__ __launch_bounds__(kThreads, (BwdShape<C, GEO>::kWaves)) void raster_b
                     }
                 }
                 const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
+                const int bsize = r.h * r.w * Cn;  // wave-uniform
+                const bool staged = bsize <= kTexStage;
                 if (GSTEX_ABLATE & 16) {
 #pragma unroll
                     for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
                 } else if (tail) {
-                    const int toff = __builtin_amdgcn_readlane(my_toff, j);
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
                     const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
                     const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
-                    if (toff >= 0) {
-                        // keep the LDS and global paths apart: a pointer that may be either compiles to flat atomics
-#define GSTEX_FX(v) ((unsigned long long)(long long)fixed_round(v))
+                    if (staged) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-                                atomicAdd(&s_texq[toff + c00 + c], GSTEX_FX(tg[c]));
-                                atomicAdd(&s_texq[toff + c01 + c], GSTEX_FX(tg[CM + c]));
-                                atomicAdd(&s_texq[toff + c10 + c], GSTEX_FX(tg[2 * CM + c]));
-                                atomicAdd(&s_texq[toff + c11 + c], GSTEX_FX(tg[3 * CM + c]));
+                                atomicAdd(&s_texq[c00 + c], fixed_round(tg[c]));
+                                atomicAdd(&s_texq[c01 + c], fixed_round(tg[CM + c]));
+                                atomicAdd(&s_texq[c10 + c], fixed_round(tg[2 * CM + c]));
+                                atomicAdd(&s_texq[c11 + c], fixed_round(tg[3 * CM + c]));
                             }
                         }
-#undef GSTEX_FX
-                    } else if (blk_ok) {
-                        // staging overflow: straight to global, back in value units
+                    } else {
+                        // block larger than the staging area: straight to global, back in value units
                         float* base = v_texture + (size_t)r.off * Cn;
                         const int uS = -tex_S;
 #pragma unroll
@@ -1071,55 +1031,19 @@ __global__ __launch_bounds__(kThreads, (BwdShape<C, GEO>::kWaves)) void raster_b
                         }
                     }
                 }
-            }
-        }
-        float4 nx_dims = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (bb > 0 && lane < kBwdBatch) nx_dims = records[(size_t)nx_gid * kRecF4 + 6];
-        if (lane == 0) s_live[wave] = live;
-        __syncthreads();
-        // combine the 4 waves in a fixed order (a wave that skipped the splat adds +0) and store the (tile, splat)
-        // row at the pair's emission slot
-        {
-            const int j = tid >> 2, c0 = (tid & 3) * 6;
-            const int slot_j = __shfl(cur_slot, j & 63, 64);  // wave 0 (tid < 64) does the combine
-            if (j < nb) {
-                const bool l0 = (s_live[0] >> j) & 1, l1 = (s_live[1] >> j) & 1;
-                const bool l2 = (s_live[2] >> j) & 1, l3 = (s_live[3] >> j) & 1;
-                float o[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) {
-                    const int c = c0 + i;
-                    const float p0 = l0 ? s_part[j][0][c] : 0.f, p1 = l1 ? s_part[j][1][c] : 0.f;
-                    const float p2 = l2 ? s_part[j][2][c] : 0.f, p3 = l3 ? s_part[j][3][c] : 0.f;
-                    o[i] = ((p0 + p1) + p2) + p3;
+                if (staged) {
+                    // flush the block (non-zero entries only) and leave the staging area zeroed; the wave's LDS
+                    // operations complete in order, so these reads see every tail added above
+                    float* dst = v_texture + (size_t)r.off * Cn;
+                    for (int e = lane; e < bsize; e += 64) {
+                        const int v = s_texq[e];
+                        if (v == 0) continue;
+                        s_texq[e] = 0;
+                        if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e, __builtin_ldexpf((float)v, -tex_S));
+                    }
                 }
-                float2* dst = reinterpret_cast<float2*>(partials + (size_t)slot_j * kNP + c0);
-                dst[0] = make_float2(o[0], o[1]);
-                dst[1] = make_float2(o[2], o[3]);
-                dst[2] = make_float2(o[4], o[5]);
             }
         }
-        // flush the staged texel gradients (only touched entries) and re-zero the staging area, splat-major:
-        // wave k flushes the staged blocks of batch splats k, k+4, ... (block base and size are wave-uniform),
-        // lanes striding over the block
-        for (int j = wave; j < nfit; j += 4) {
-            const int t0 = __builtin_amdgcn_readlane(my_toff, j);
-            const int size = __builtin_amdgcn_readlane(__float_as_int(cur_dims.x), j) *
-                             __builtin_amdgcn_readlane(__float_as_int(cur_dims.y), j) * Cn;
-            const int off = __builtin_amdgcn_readlane(__float_as_int(cur_dims.z), j);
-            const bool ok = off + size / Cn <= n_texels;  // a block past the texel store (corrupt dims) is dropped
-            float* dst = v_texture + (size_t)off * Cn;
-            for (int e = lane; e < size; e += 64) {
-                const long long v = (long long)s_texq[t0 + e];
-                if (v == 0) continue;
-                s_texq[t0 + e] = 0ull;
-                if (ok && !(GSTEX_ABLATE & 32)) atomicAdd(dst + e, __builtin_ldexpf((float)v, -tex_S));
-            }
-        }
-        __syncthreads();
-        cur_gid = nx_gid;
-        cur_slot = nx_slot;
-        cur_dims = nx_dims;
     }
 }
 
@@ -1133,9 +1057,9 @@ constexpr int kSetupBwdRows = 256 / kNP;  // 10 splats x 24 partial columns summ
 // splats per workgroup: phase 1 sums them kSetupBwdRows at a time, phase 2 chains them one per thread
 constexpr int kSetupBwdSplats = GSTEX_SETUP_SPW;
 #ifndef GSTEX_SETUP_INFLIGHT
-#define GSTEX_SETUP_INFLIGHT 16
+#define GSTEX_SETUP_INFLIGHT 4
 #endif
-constexpr int kSetupBwdInflight = GSTEX_SETUP_INFLIGHT;
+constexpr int kSetupBwdInflight = GSTEX_SETUP_INFLIGHT;  // slots (x 4 quadrant rows) per group of loads
 static_assert(kSetupBwdSplats % kSetupBwdRows == 0 && kSetupBwdSplats <= 256, "setup_bwd splats per workgroup");
 // FOLD_AABB: the centres were produced by get_aabb_2d from these same means / scales / quats (training
 // path), so the AABB-centre chain (aabb_bwd_kernel's arithmetic) is applied here and added in, instead of
@@ -1145,12 +1069,12 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
     const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials,
-    CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
-    float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers,
-    float* __restrict__ v_uv0) {
-    // phase 1: kNP lanes per splat, lane c sums column c of the splat's partial rows in slot order (the
-    // rows of one splat are contiguous, so each step reads one 96-B row per splat instead of one
-    // 96-B row per thread; same summation order as a plain loop); phase 2: one thread per splat chains the sums to the parameters
+    const uint32_t* __restrict__ row_flags, CamArgs cam_args, float* __restrict__ v_means,
+    float* __restrict__ v_scales, float* __restrict__ v_quats, float* __restrict__ v_rgbs, float* __restrict__ v_opac,
+    float* __restrict__ v_centers, float* __restrict__ v_uv0) {
+    // phase 1: kNP lanes per splat, lane c sums column c of the splat's flagged (slot, quadrant) rows in slot-major,
+    // quadrant-minor order (a splat's slots are contiguous, so its rows and flag words are too); phase 2: one
+    // thread per splat chains the sums to the parameters
     __shared__ float s_sum[kSetupBwdSplats][kNP];
     const int t = threadIdx.x;
     const int g0 = blockIdx.x * kSetupBwdSplats;
@@ -1160,16 +1084,26 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
             float acc = 0.f;
             if (g0 + j < n) {
                 const int cnt = nth[g0 + j];
-                const float* src = partials + (size_t)offsets[g0 + j] * kNP + c;
-                // groups of kSetupBwdInflight rows, the last one predicated: every row load of a group is in
-                // flight at once, also for the remainder (most splats hit fewer tiles than one group)
+                const size_t s0 = (size_t)offsets[g0 + j];
+                const float* src = partials + s0 * 4 * kNP + c;
+                const uint32_t* fl = row_flags + s0;
+                // groups of kSetupBwdInflight slots: their flag words, then every flagged row of the group, are
+                // loaded before any is summed (most splats hit fewer tiles than one group holds)
                 for (int e = 0; e < cnt; e += kSetupBwdInflight) {
-                    float r[kSetupBwdInflight];
+                    uint32_t f[kSetupBwdInflight];
 #pragma unroll
-                    for (int u = 0; u < kSetupBwdInflight; ++u) r[u] = e + u < cnt ? src[(size_t)(e + u) * kNP] : 0.f;
+                    for (int u = 0; u < kSetupBwdInflight; ++u) f[u] = e + u < cnt ? fl[e + u] : 0u;
+                    float r[kSetupBwdInflight * 4];
 #pragma unroll
                     for (int u = 0; u < kSetupBwdInflight; ++u)
-                        if (e + u < cnt) acc += r[u];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            r[4 * u + q] = (f[u] >> (8 * q)) & 1u ? src[((size_t)(e + u) * 4 + q) * kNP] : 0.f;
+#pragma unroll
+                    for (int u = 0; u < kSetupBwdInflight; ++u)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if ((f[u] >> (8 * q)) & 1u) acc += r[4 * u + q];
                 }
             }
             s_sum[j][c] = acc;
@@ -1274,7 +1208,7 @@ __global__ __launch_bounds__(kThreads) void texture_edit_kernel(
     const WaveBlock wb = wave_block(tx, ty, tid);
     const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
-    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;
+    const float px = (float)pxi + 0.5f, py = (float)pyi + 0.5f;  // pixel centres (gstex_common.h)
     const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
     const int2 rng = tile_ranges[tile];
     float er = 0.f, eg = 0.f, eb = 0.f, ea = 0.f, dlo = 1.0f, dhi = 0.0f;
@@ -1403,29 +1337,35 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
                                 const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
                                 const float* state, const float* v_img,
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
-                                const float* v_normal, float* partials, float* v_texture,
-                                const uint64_t* visit_masks, void* stream) {
+                                const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
+                                float* v_texture, const uint64_t* visit_masks, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
     int rc = check_settings(settings);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && state, "gstex_raster_bwd: null pointer");
+    GSTEX_REQUIRE(n_isect >= 0 && n_isect < (int64_t)INT32_MAX, "gstex_raster_bwd: n_isect out of range");
+    GSTEX_REQUIRE(n_isect == 0 || (partials && row_flags && sorted_ids && sorted_slots),
+                  "gstex_raster_bwd: null pair buffer");
     GSTEX_REQUIRE(n_texels >= 0 && n_texels * channels < (int64_t)INT32_MAX, "gstex_raster_bwd: n_texels out of range");
     GSTEX_REQUIRE(n_texels == 0 || (texture && v_texture), "gstex_raster_bwd: null texture");
+    GSTEX_REQUIRE(!(settings & GSTEX_SETTING_EVAL_NORMAL) || !v_normal,
+                  "gstex_raster_bwd: settings bit 15 (unit-normal eval render) has no normal gradient; pass v_normal = NULL");
     const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
     CamArgs dc = to_device_camera(*cam);
     hipStream_t st = as_stream(stream);
-    const int nblk = tiles_x * tiles_y;
+    if (n_isect > 0 && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
+        return launch_status("gstex_raster_bwd (row_flags)");
+    const int nblk = tiles_x * tiles_y * 4;  // one wave per (tile, 8x8 quadrant)
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
 #define GSTEX_BWD(CC, GG)                                                                                      \
-    raster_bwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(                                                      \
+    raster_bwd_kernel<CC, GG><<<nblk, 64, 0, st>>>(                                                            \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         tile_order, sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,    \
-        v_img, v_depth,                                                                                         \
-        v_reg, v_alpha, v_tex,                                                                                  \
-        v_normal, partials, v_texture, (const unsigned long long*)visit_masks)
+        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture,      \
+        (const unsigned long long*)visit_masks)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
     else if (channels == 3) GSTEX_BWD(3, true);
     else if (channels == 6 && !geo) GSTEX_BWD(6, false);
@@ -1444,9 +1384,9 @@ extern "C" size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles) {
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                                       const float* quats, const float* opacities, const float* umap,
                                       const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      const float* partials, const gstex_camera* cam, float* v_means,
-                                      float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities,
-                                      float* v_centers, float* v_uv0, void* stream) {
+                                      const float* partials, const uint32_t* row_flags, const gstex_camera* cam,
+                                      float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
+                                      float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
     GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup_bwd: invalid arguments");
     if (n == 0) return GSTEX_OK;
@@ -1454,17 +1394,17 @@ extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd: null pointer");
     setup_bwd_kernel<false><<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
-        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
-        v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, row_flags,
+        to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     return launch_status("gstex_raster_setup_bwd");
 }
 
 extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
-                                           const float* quats, const float* opacities, const float* umap,
-                                           const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                           const float* partials, const gstex_camera* cam, float* v_means,
-                                           float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities,
-                                           float* v_centers, float* v_uv0, void* stream) {
+                                      const float* quats, const float* opacities, const float* umap,
+                                      const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
+                                      const float* partials, const uint32_t* row_flags, const gstex_camera* cam,
+                                      float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
+                                      float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
     GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup_bwd_aabb: invalid arguments");
     if (n == 0) return GSTEX_OK;
@@ -1472,8 +1412,8 @@ extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const 
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd_aabb: null pointer");
     setup_bwd_kernel<true><<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
-        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, to_device_camera(*cam),
-        v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, row_flags,
+        to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     return launch_status("gstex_raster_setup_bwd_aabb");
 }
 

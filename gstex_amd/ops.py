@@ -363,6 +363,8 @@ class _TextureGaussians(torch.autograd.Function):
             reg = torch.empty((H, W), **f)
             normal = torch.empty((H, W, 3), **f)
             geo_ptrs = (ptr(depth), ptr(reg), ptr(normal))
+            if int(settings) & _lib.SETTING_EVAL_NORMAL:
+                ctx.mark_non_differentiable(normal)  # bit 15: unit normals, a forward-only eval output
         else:  # not produced by the kernel: zeros, no gradient
             z = torch.zeros((5, H, W), **f)
             depth, reg, normal = z[0], z[1], z[2:5].permute(1, 2, 0)
@@ -412,13 +414,15 @@ class _TextureGaussians(torch.autograd.Function):
         v_tex = g(v_tex, (H, W, C))
         v_normal = g(v_normal, (H, W, 3))
         n_isect = sorted_ids.shape[0]
-        partials = torch.empty((n_isect, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
+        # one partial row per (pair, 8x8 quadrant), written only where the quadrant contributes (row_flags)
+        partials = torch.empty((n_isect, 4, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
+        row_flags = torch.empty((n_isect,), device=dev, dtype=torch.int32)
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
-                ptr(v_normal), ptr(partials), ptr(v_texture), ptr(ctx.vmask), st)
+                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.vmask), st)
         ctx.vmask = None
         if ctx.sink:
             if ctx.on_texture_grad is not None:
@@ -432,7 +436,8 @@ class _TextureGaussians(torch.autograd.Function):
         v_centers = torch.empty((n, 2), device=dev, dtype=torch.float32)
         v_uv0 = torch.empty((n, 1, 2), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup_bwd_aabb" if ctx.fold_aabb else "gstex_raster_setup_bwd", n, ptr(means),
-                ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap), ptr(vmap), ptr(nth), ptr(offsets), ptr(partials), cam,
+                ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap), ptr(vmap), ptr(nth), ptr(offsets), ptr(partials),
+                ptr(row_flags), cam,
                 ptr(v_means), ptr(v_scales), ptr(v_quats), ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
         v_bg = None
         if ctx.needs_input_grad[26]:

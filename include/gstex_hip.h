@@ -38,18 +38,18 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 5
+#define GSTEX_ABI_VERSION 6
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
-/* Per-(tile, splat) gradient partial written by gstex_raster_bwd (floats). */
+/* Per-(tile, splat, quadrant) gradient partial row written by gstex_raster_bwd (floats). */
 #define GSTEX_PARTIAL_FLOATS 24
 
 /* settings bitfield (GStexModelConfig.settings, gstex.py:194-197) */
 #define GSTEX_SETTING_AA_BLUR (1 << 9)   /* 2DGS screen-space low-pass */
 #define GSTEX_SETTING_DIST_REG (1 << 10) /* 2DGS NDC depth-distortion output */
 #define GSTEX_SETTING_EDIT (1 << 13)     /* texture_edit request (gstex.py:599) */
-#define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198); accepted, no-op */
+#define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198): normal output unit-length, forward only */
 
 typedef enum {
     GSTEX_OK = 0,
@@ -141,9 +141,11 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
 size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles);
 /* Backward composite. Needs the forward state and the same tile_order. Any of v_img ... v_normal may be
  * NULL (that output's gradient is zero).  Texel blocks that run past n_texels (corrupt texture_dims) are
- * neither read nor written. Writes
- * partials[n_isect][GSTEX_PARTIAL_FLOATS] at the emission slot of every (tile, splat) pair and
- * accumulates (+=) texel gradients into v_texture[n_texels][C]. */
+ * neither read nor written.  One wave per (tile, 8x8 pixel quadrant q): for every pair (emission slot s) the
+ * quadrant contributes to, writes the row partials[(4 s + q) * GSTEX_PARTIAL_FLOATS ...] (n_isect * 4 rows
+ * allocated; rows of pairs a quadrant does not reach are never written) and sets byte q of row_flags[s]
+ * (n_isect uint32 words, zeroed by this call on the stream); accumulates (+=) texel gradients into
+ * v_texture[n_texels][C]. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* tile_order, const int32_t* sorted_ids,
@@ -151,13 +153,14 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      float tex_scale, float tex_bias, const float* state, const float* v_img,
                      const float* v_depth,
                      const float* v_reg, const float* v_alpha, const float* v_tex,
-                     const float* v_normal, float* partials, float* v_texture,
-                     const uint64_t* visit_masks, void* stream);
-/* Sums each splat's partials and chains them to the splat parameters. Outputs are overwritten. */
+                     const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
+                     float* v_texture, const uint64_t* visit_masks, void* stream);
+/* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
+ * them to the splat parameters. Outputs are overwritten. */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                            const float* quats, const float* opacities, const float* umap,
                            const float* vmap, const int32_t* num_tiles_hit,
-                           const int32_t* offsets, const float* partials,
+                           const int32_t* offsets, const float* partials, const uint32_t* row_flags,
                            const gstex_camera* cam, float* v_means, float* v_scales,
                            float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                            float* v_uv0, void* stream);
@@ -168,7 +171,7 @@ int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, f
 int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
                                 const float* quats, const float* opacities, const float* umap,
                                 const float* vmap, const int32_t* num_tiles_hit,
-                                const int32_t* offsets, const float* partials,
+                                const int32_t* offsets, const float* partials, const uint32_t* row_flags,
                                 const gstex_camera* cam, float* v_means, float* v_scales,
                                 float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                                 float* v_uv0, void* stream);

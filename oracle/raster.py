@@ -36,6 +36,7 @@ K_PROJ_CLIP = np.float32(0.01)
 
 SETTING_AA_BLUR = 1 << 9
 SETTING_DIST_REG = 1 << 10
+SETTING_EVAL_NORMAL = 1 << 15  # gstex.py:1198 eval render: unit-length normal output
 
 
 def _c(v, dtype):
@@ -324,7 +325,7 @@ def rasterize(inp: RasterInputs, grad_dtype=F64, bins=None):
     dec = _render(inp, F32, tile_ranges, sorted_ids, None)
     hi = _render(inp, grad_dtype, tile_ranges, sorted_ids, dec["decisions"])
     aux = dict(offsets=offsets, tile_ranges=tile_ranges, sorted_ids=sorted_ids, sorted_slots=sorted_slots,
-               last=dec["last"], T_final=dec["out"]["T_final"])
+               last=dec["last"], T_final=dec["out"]["T_final"], margin=dec["margin"])
     return dec["out"], hi["out"], aux
 
 
@@ -348,7 +349,7 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
     fis, far = c(K_FILTER_INV_SQ), c(K_FAR_RATIO)
 
     pix_idx, rows = [], {k: [] for k in ["img", "depth", "reg", "T", "tex", "normal", "M1", "M2"]}
-    last_all = []
+    last_all, margin_all = [], []
     new_dec = {"tiles": {}, "sgn": tab["sgn"].detach().to(F32)} if decisions is None else None
     for t in range(n_tiles):
         s, e = int(tile_ranges[t, 0]), int(tile_ranges[t, 1])
@@ -369,9 +370,12 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
             rows["tex"].append(torch.zeros(P, C, dtype=dtype)); rows["normal"].append(torch.zeros(P, 3, dtype=dtype))
             rows["M1"].append(z); rows["M2"].append(z)
             last_all.append(torch.full((P,), -1, dtype=torch.int64))
+            margin_all.append(torch.full((P,), float("inf")))
             continue
         ids = torch.from_numpy(np.asarray(sorted_ids[s:e], dtype=np.int64))
         K = ids.numel()
+        # pixel (x, y) is evaluated at its centre (x + 0.5, y + 0.5): the convention of the reference's own
+        # depths_to_points (gstex.py:138-139, ray through (j - cx + 0.5) / fx), DESIGN.md §1 lineage table
         px = (torch.from_numpy(pxi.astype(np.float32)) + 0.5).to(dtype)[None, :]  # exact in fp32
         py = (torch.from_numpy(pyi.astype(np.float32)) + 0.5).to(dtype)[None, :]
         g = {k: v[ids] for k, v in tab.items() if k != "sgn"}
@@ -419,6 +423,18 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
             first = torch.where(any_stop, stop.float().argmax(0), torch.full((P,), K, dtype=torch.int64))
             kidx = torch.arange(K)[:, None]
             incl = valid & (kidx < first[None, :])
+            # decision margins (test support): the relative distance of every threshold test the GPU repeats in
+            # fp32 (alpha >= 1/255, z >= near, T (1 - alpha) < 1e-4, rho3 <= rho2) from its threshold, over the
+            # pairs the traversal reaches.  exp is the one fp32 op that is not correctly rounded on either side
+            # (the GPU's v_exp_f32 sequence vs the host's expf can differ by an ulp), so a pixel whose forward
+            # differs from the oracle's by a flipped decision has a margin of a few 1e-7
+            big = torch.full_like(alpha, float("inf"))
+            m_a = (alpha - amin).abs() / amin
+            m_z = (zz - near).abs() / near
+            m_t = torch.where(valid, (Tafter - tmin).abs() / tmin, big)
+            m_u = (rho3 - rho2).abs() / torch.clamp(rho2, min=1e-30) if aa else big
+            m_all = torch.minimum(torch.minimum(m_a, m_z), torch.minimum(m_t, m_u))
+            margin = torch.where(nz & (kidx <= first[None, :]), m_all, big).min(0).values.float()
         else:
             aclamp = d["aclamp"]
             incl = d["incl"]
@@ -511,6 +527,7 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         rows["T"].append(Tfin); rows["tex"].append(texo); rows["normal"].append(normal)
         rows["M1"].append(M1); rows["M2"].append(M2)
         last_all.append(last)
+        margin_all.append(margin if decisions is None else torch.full((P,), float("inf")))
         if new_dec is not None:
             new_dec["tiles"][t] = dict(nz=nz, use3=use3, aclamp=aclamp, incl=incl, in_u=in_u, in_v=in_v,
                                        i0=i0, j0=j0)
@@ -525,14 +542,22 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
             x = torch.cat(rows[name], 0)[order]
             return x.reshape(H, W, width) if width else x.reshape(H, W)
 
+        normal = assemble("normal", 3)
+        if inp.settings & SETTING_EVAL_NORMAL:  # raster.hip raster_fwd_kernel: unit normal, 0 where none accumulated
+            n2 = (normal[..., 0] * normal[..., 0] + normal[..., 1] * normal[..., 1]) + normal[..., 2] * normal[..., 2]
+            inv = torch.where(n2 > 0, _div(_c(1.0, n2.dtype), _sqrt(torch.where(n2 > 0, n2, torch.ones_like(n2)))),
+                              torch.zeros_like(n2))
+            normal = normal * inv[..., None]
         out = dict(img=assemble("img", 3), depth=assemble("depth", 0), reg=assemble("reg", 0),
-                   alpha=1.0 - assemble("T", 0), tex=assemble("tex", C), normal=assemble("normal", 3),
+                   alpha=1.0 - assemble("T", 0), tex=assemble("tex", C), normal=normal,
                    T_final=assemble("T", 0), M1=assemble("M1", 0), M2=assemble("M2", 0))
         last_img = torch.cat(last_all)[order].reshape(H, W)
+        margin_img = torch.cat(margin_all)[order].reshape(H, W)
     else:
         last_img = torch.full((H, W), -1)
+        margin_img = torch.full((H, W), float("inf"))
     assert Np == H * W
-    res = dict(out=out, last=last_img)
+    res = dict(out=out, last=last_img, margin=margin_img)
     if new_dec is not None:
         res["decisions"] = new_dec
     return res

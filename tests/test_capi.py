@@ -37,7 +37,7 @@ def test_every_header_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.gstex_abi_version() == 5
+    assert lib.gstex_abi_version() == 6
 
 
 def test_workspace_size_queries(lib):
@@ -74,7 +74,7 @@ def test_raster_rejects_bad_channels_and_settings(lib):
     assert rc == 3 and "unsupported settings" in msg
     bad = _cam(block=8)
     rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, None, 0,
-                      1.0, 0.0, None, None, None, None, None, None, None, None, None, None, None)
+                      1.0, 0.0, None, None, None, None, None, None, None, 0, None, None, None, None, None)
     assert rc == 1 and "block_width" in msg
 
 

@@ -14,13 +14,12 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import DIFF, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, oracle_run, upstream
+from helpers import COND_FACTOR, DIFF, GRAD_RTOL, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, \
+    oracle_run, upstream
 from oracle import raster as O
 
 pytestmark = pytest.mark.gpu
 
-GRAD_RTOL = 1e-5
-COND_FACTOR = 4.0
 DEV = "cuda"
 
 
@@ -161,7 +160,7 @@ def _check_raster(name, outputs):
     gout, gg = gpu_run(case, grads=True, outputs=outputs)
     fwd = {k: (gout[k].double() - o64[k]).abs().max().item() for k in gout}
     _report(f"{name} fwd", fwd)
-    assert_close_fwd(gout, o64)
+    assert_close_fwd(gout, o64, margin=aux["margin"])
     _, _, _, og32 = oracle_run(case, grads=True, grad_dtype=torch.float32, outputs=outputs)
     errs, norm_errs, inherent, inherent_n = {}, {}, {}, {}
     for k in DIFF:
@@ -407,25 +406,28 @@ def test_texture_transform_equals_materialised_sh2rgb():
     for a, b in zip(o1, o2):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
     gd, gt = leaf_dc.grad.double().cpu(), leaf_tex.grad.double().cpu() * C0
-    assert float((gd - gt).norm() / gt.norm()) < 1e-6
+    # the two runs stage texel gradients at different fixed-point scales (tex_scale C0 vs 1): each is exact to
+    # 2^-25 of its wave's largest upstream texel gradient, so they agree to a few 1e-6 (parity bound: 1e-5)
+    assert float((gd - gt).norm() / gt.norm()) < 4e-6
 
 
 @pytest.mark.parametrize("gscale", [1e-20, 1e12])
 def test_texel_fixed_point_scale_invariance(gscale):
-    # the backward's per-tile fixed-point scale follows the upstream texel-gradient magnitude: scaling
-    # dL/dtex by any factor scales v_texture by the same factor to fp32 accuracy
+    # the backward's per-wave fixed-point scale follows the upstream texel-gradient magnitude: scaling dL/dtex by
+    # any factor scales v_texture by the same factor, to the staging resolution (2^-25 of the wave's largest
+    # upstream texel gradient; a factor that is not a power of two moves the rounding grid)
     case = make_case(n=300, n_texels=20000, H=64, W=80, seed=12)
     import helpers
 
     orig = helpers.upstream
 
-    def scaled(H, W, C, seed=5):
-        up = orig(H, W, C, seed)
+    def scaled(H, W, C, seed=5, mask=None):
+        up = orig(H, W, C, seed, mask)
         up = {k: torch.zeros_like(v) for k, v in up.items()} | {"tex": up["tex"] * gscale}
         return up
 
-    def unit(H, W, C, seed=5):
-        up = orig(H, W, C, seed)
+    def unit(H, W, C, seed=5, mask=None):
+        up = orig(H, W, C, seed, mask)
         return {k: torch.zeros_like(v) for k, v in up.items()} | {"tex": up["tex"]}
 
     try:
@@ -437,7 +439,7 @@ def test_texel_fixed_point_scale_invariance(gscale):
         helpers.upstream = orig
     a, b = gs["texture"].double() / gscale, gu["texture"].double()
     assert float(b.abs().max()) > 0
-    assert float((a - b).norm() / b.norm()) < 1e-6
+    assert float((a - b).norm() / b.norm()) < 4e-6
 
 
 # ---------------------------------------------------------------- fused activations / SH without the DC cat
