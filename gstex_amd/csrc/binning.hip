@@ -372,15 +372,24 @@ constexpr int kRankThreads = 256;
 constexpr int kRankTiles = 64;  // tiles per workgroup; the 4 waves each compare against a quarter of the keys
 constexpr int kRankChunk = 4096;
 
-// bucket size of tile t from tile_ranges (pairs [start, end)) or, STARTS, from the n+1 exclusive-scan starts
-template <bool STARTS>
+// Sort keys, all unique (the item index sits in the low bits), ascending = launch order:
+//   SRC 0: tile t's bucket size from tile_ranges (pairs [start, end)), 14-bit tile index;
+//   SRC 1: the same from the n+1 exclusive-scan starts;
+//   SRC 2: a backward unit's cost estimate (gstex_unit_order), 16-bit unit index.
+constexpr int kUnitOrderCap = 1 << 16;
+template <int SRC>
 __device__ __forceinline__ unsigned order_key(const int32_t* r, int t) {
-    const int c = STARTS ? r[t + 1] - r[t] : r[2 * t + 1] - r[2 * t];
-    const unsigned cnt = (unsigned)min((int)kOrderMaxCount, c);
-    return ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
+    if constexpr (SRC == 2) {
+        const unsigned c = (unsigned)min(0xFFFF, max(0, r[t]));
+        return ((0xFFFFu - c) << 16) | (unsigned)t;  // cost desc, unit asc
+    } else {
+        const int c = SRC == 1 ? r[t + 1] - r[t] : r[2 * t + 1] - r[2 * t];
+        const unsigned cnt = (unsigned)min((int)kOrderMaxCount, c);
+        return ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
+    }
 }
 
-template <bool STARTS>
+template <int SRC>
 __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, const int32_t* __restrict__ tile_ranges,
                                                                  int32_t* __restrict__ tile_order) {
     __shared__ uint4 s_key[kRankChunk / 4];
@@ -388,13 +397,13 @@ __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, co
     unsigned* s_k = reinterpret_cast<unsigned*>(s_key);
     const int part = threadIdx.x >> 6;
     const int t = blockIdx.x * kRankTiles + (threadIdx.x & 63);
-    const unsigned mine = t < n_tiles ? order_key<STARTS>(tile_ranges, t) : 0u;
+    const unsigned mine = t < n_tiles ? order_key<SRC>(tile_ranges, t) : 0u;
     int rank = 0;
     for (int c0 = 0; c0 < n_tiles; c0 += kRankChunk) {
         const int cn = min(kRankChunk, n_tiles - c0);
         __syncthreads();
         for (int i = threadIdx.x; i < kRankChunk; i += kRankThreads)
-            s_k[i] = i < cn ? order_key<STARTS>(tile_ranges, c0 + i) : ~0u;  // padding never ranks below a key
+            s_k[i] = i < cn ? order_key<SRC>(tile_ranges, c0 + i) : ~0u;  // padding never ranks below a key
         __syncthreads();
         const int nv = (cn + 3) >> 2;
         const int q0 = (nv * part) >> 2, q1 = (nv * (part + 1)) >> 2;
@@ -509,7 +518,7 @@ extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, 
                                                   ws.tile_start, ws.rank, ws.keys, ws.slot_gid);
     const bool ranked = n_tiles <= kOrderCap;
     if (ranked)
-        tile_rank_kernel<true><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, st>>>(n_tiles, ws.tile_start, ws.order);
+        tile_rank_kernel<1><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, st>>>(n_tiles, ws.tile_start, ws.order);
     tile_sort_kernel<<<n_tiles, kSortThreads, 0, st>>>(n_tiles, ranked ? ws.order : nullptr, ws.tile_start, ws.keys,
                                                        ws.scratch, ws.slot_gid, tile_ranges, sorted_ids,
                                                        sorted_slots);
@@ -524,7 +533,20 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
         iota_kernel<<<div_up(n_tiles, 256), 256, 0, as_stream(stream)>>>(n_tiles, tile_order);
         return launch_status("gstex_tile_order");
     }
-    tile_rank_kernel<false><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges,
+    tile_rank_kernel<0><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_tiles, tile_ranges,
                                                                                                 tile_order);
     return launch_status("gstex_tile_order");
+}
+
+extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, void* stream) {
+    GSTEX_REQUIRE(n_units >= 0, "gstex_unit_order: invalid n_units %d", n_units);
+    if (n_units == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(unit_cost && unit_order, "gstex_unit_order: null pointer");
+    if (n_units > kUnitOrderCap) {  // beyond the 16-bit unit index of the keys: index order
+        iota_kernel<<<div_up(n_units, 256), 256, 0, as_stream(stream)>>>(n_units, unit_order);
+        return launch_status("gstex_unit_order");
+    }
+    tile_rank_kernel<2><<<div_up(n_units, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_units, unit_cost,
+                                                                                            unit_order);
+    return launch_status("gstex_unit_order");
 }

@@ -48,7 +48,7 @@ __device__ unsigned long long g_stats[8];
 extern "C" int gstex_debug_stats(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats)) == hipSuccess ? 0 : 2;
 }
-__device__ unsigned long long g_wg[4096 * 4];
+__device__ unsigned long long g_wg[65536 * 4];
 extern "C" int gstex_debug_wg(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg), sizeof(g_wg)) == hipSuccess ? 0 : 2;
 }
@@ -59,6 +59,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #endif
 #else
 #define GSTEX_STAT(i, v) do { } while (0)
+#endif
+#ifndef GSTEX_FWD_OCC
+#define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower)
 #endif
 #ifndef GSTEX_FWD_WAVES
 #define GSTEX_FWD_WAVES 0
@@ -228,6 +231,59 @@ __host__ __device__ __forceinline__ size_t visit_mask_base(int start, int tile) 
     return (size_t)((start + 63) / 64) + (size_t)tile;
 }
 
+// Backward units: the backward splits each (tile, 8x8 quadrant) list at every kSegLen positions into segments, one
+// wave each, so no wave walks more than kSegLen positions (a deep unit as one wave was the kernel's critical path).
+// Segment k of tile t has slot seg_base(start_t, t) + k (disjoint across tiles, like the visit-mask words); unit =
+// 4 slot + quadrant.  The forward records, per unit, the number of splats it evaluated (the backward's cost
+// estimate and launch order), the tile of every slot, and per-pixel checkpoints: for each segment boundary it
+// crosses with a lane still running, the state after the segment (T and the colour / texture / depth / normal /
+// distortion accumulators), and for a wave whose last contributor lies past the first segment, its final
+// accumulators in the slot of that last segment.  The backward of segment k starts from checkpoint k instead of
+// the final state: T = T_k, and R = (back half of sum_j w_j g_j + T_final bg-term) / T_k from the accumulators.
+#ifndef GSTEX_SEG_LEN
+#define GSTEX_SEG_LEN 256
+#endif
+constexpr int kSegLen = GSTEX_SEG_LEN;
+static_assert(kSegLen % 128 == 0, "segments end at forward batch boundaries");
+__host__ __device__ __forceinline__ int seg_base(int start, int tile) { return (start + kSegLen - 1) / kSegLen + tile; }
+__host__ __device__ __forceinline__ int ck_fields(int C) { return 4 + C + 6; }  // T, img[3], tex[C], D, nrm[3], M1, M2
+
+struct AuxPtrs {
+    unsigned long long* masks;
+    int32_t* cost;       // [n_units]
+    int32_t* order;      // [n_units] (written by the backward)
+    int32_t* slot_tile;  // [n_slots]
+    float* ckpt;         // [n_units][F][64]
+    int F;
+};
+struct AuxLayout { size_t masks, cost, order, slot_tile, ckpt, bytes; int64_t n_slots, n_units; int F; };
+__host__ inline AuxLayout aux_layout(int64_t n_isect, int n_tiles, int C) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    AuxLayout a;
+    a.n_slots = (n_isect + kSegLen - 1) / kSegLen + n_tiles + 1;
+    a.n_units = a.n_slots * 4;
+    a.F = ck_fields(C);
+    size_t o = 0;
+    a.masks = o; o = al(o + (((size_t)n_isect + 63) / 64 + (size_t)n_tiles + 1) * 4 * sizeof(uint64_t));
+    a.cost = o; o = al(o + (size_t)a.n_units * 4);
+    a.order = o; o = al(o + (size_t)a.n_units * 4);
+    a.slot_tile = o; o = al(o + (size_t)a.n_slots * 4);
+    a.ckpt = o; o = al(o + (size_t)a.n_units * a.F * 64 * sizeof(float));
+    a.bytes = o;
+    return a;
+}
+__host__ inline AuxPtrs aux_ptrs(void* aux, const AuxLayout& a) {
+    char* b = (char*)aux;
+    AuxPtrs p;
+    p.masks = aux ? (unsigned long long*)(b + a.masks) : nullptr;
+    p.cost = aux ? (int32_t*)(b + a.cost) : nullptr;
+    p.order = aux ? (int32_t*)(b + a.order) : nullptr;
+    p.slot_tile = aux ? (int32_t*)(b + a.slot_tile) : nullptr;
+    p.ckpt = aux ? (float*)(b + a.ckpt) : nullptr;
+    p.F = a.F;
+    return p;
+}
+
 // The same record read from global memory at a wave-uniform address: scalar loads straight into SGPRs
 // (no LDS read, no v_readfirstlane per value).
 __device__ __forceinline__ Rec read_rec_global(const float4* __restrict__ rec) {
@@ -331,6 +387,12 @@ __device__ __forceinline__ float exp_nonpos(float x) {
     const float e = __builtin_rintf(ph);
     const float a = (ph - e) + pl;
     return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
+}
+
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
@@ -446,15 +508,15 @@ __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float
 // GEOF = false: depth / distortion / normal not produced (their outputs are NULL: a caller whose loss does
 // not use them, e.g. the photometric training step); every other output is computed unchanged.
 template <int C, bool GEOF>
-__global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
+__global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, int n_texels, float tex_scale,
     float tex_bias, float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
-    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state,
-    unsigned long long* __restrict__ visit_masks) {
+    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state, AuxPtrs aux) {
     const Camera cam = load_camera(cam_args);
+    unsigned long long* __restrict__ visit_masks = aux.masks;
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
@@ -482,8 +544,40 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
     bool done = !inside;
     const int lane = tid & 63, wave = tid >> 6;
     const size_t vm_base = visit_mask_base(rng.x, tile);
+    const int sbase = seg_base(rng.x, tile);
+    int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
+    if (aux.slot_tile)
+        for (int k = tid; k * kSegLen < rng.y - rng.x; k += kThreads) aux.slot_tile[sbase + k] = tile;
+    // one checkpoint record: field f of the wave's lane at ckpt[((slot * 4 + wave) * F + f) * 64 + lane]
+    auto write_ck = [&](int slot) {
+        float* ck = aux.ckpt + ((size_t)slot * 4 + wave) * aux.F * 64 + lane;
+        ck[0] = T;
+        ck[64] = img[0];
+        ck[128] = img[1];
+        ck[192] = img[2];
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < Cn) ck[(4 + c) * 64] = tex[c];
+        if (GEOF) {
+            float* g = ck + (4 + Cn) * 64;
+            g[0] = D;
+            g[64] = nrm[0];
+            g[128] = nrm[1];
+            g[192] = nrm[2];
+            g[256] = M1;
+            g[320] = M2;
+        }
+    };
 
     for (int b0 = rng.x; b0 < rng.y; b0 += kFwdBatch) {
+        if (aux.cost && b0 > rng.x && (b0 - rng.x) % kSegLen == 0) {
+            // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
+            const int cnt = wave_max_i(seg_visits);  // lanes leave the visit loop as they finish: the wave's count
+            if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt;
+            if (__any(!done)) write_ck(sbase + cur_seg);
+            seg_visits = 0;
+            ++cur_seg;
+        }
         if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
         for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
             const int j = q / kRecF4, k = q % kRecF4;
@@ -508,6 +602,7 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             if (done) break;
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
+            ++seg_visits;
             const Rec r = GSTEX_FWD_SLOAD ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
                                          : read_rec<kFwdBatch>(s_rec, j);
             Hit h;
@@ -557,6 +652,13 @@ __global__ __launch_bounds__(kThreads) GSTEX_FWD_ATTR void raster_fwd_kernel(
             last = b0 - rng.x + j;
           }
         }
+    }
+    if (aux.cost) {
+        const int cnt = wave_max_i(seg_visits);
+        if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt;
+        // final accumulators for the backward's earlier segments, in the slot of the wave's last segment
+        const int wl = wave_max_i(last);
+        if (wl >= kSegLen) write_ck(sbase + wl / kSegLen);
     }
     if (!inside) return;
     const size_t pix = (size_t)pyi * cam.W + pxi;
@@ -742,29 +844,26 @@ __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^
     return q;
 }
 
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return __builtin_amdgcn_readfirstlane(v);
-}
 
 template <int C, bool GEO>
 __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
-    const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
+    const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots, const float* __restrict__ texture,
     int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
-    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture,
-    const unsigned long long* __restrict__ visit_masks) {
+    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
     __shared__ int s_texq[kTexStage];
 
-    const int quad = blockIdx.x & 3;
-    const int tile = tile_order ? tile_order[blockIdx.x >> 2] : (int)(blockIdx.x >> 2);  // largest-first when given
+    // unit = 4 slot + quadrant (see AuxPtrs), launched costliest first; a unit the forward never evaluated in is empty
+    const int unit = aux.order[blockIdx.x];
+    if (aux.cost[unit] == 0) return;
+    const int quad = unit & 3, slot = unit >> 2;
+    const int tile = aux.slot_tile[slot];
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int lane = threadIdx.x;
     const WaveBlock wb = wave_block(tx, ty, quad * 64 + lane);
@@ -798,15 +897,55 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             if (v_normal) { Gn[0] = v_normal[3 * pix]; Gn[1] = v_normal[3 * pix + 1]; Gn[2] = v_normal[3 * pix + 2]; }
         }
     }
-    // the wave's last contributor: pairs behind it receive no gradient from this quadrant (no row, no flag)
+    // the wave's last contributor: pairs behind it receive no gradient from this quadrant (no row, no flag); this
+    // unit walks tile-list positions [lo, hi] of its segment
     const int wave_last = wave_max_i(last);
-    if (wave_last < 0) return;
+#if GSTEX_STATS == 3  // per-wave timeline (diagnostic builds): start, end (s_memrealtime), tile depth, wave_last
+    struct WgStamp {
+        unsigned long long t0; int depth, wl;
+        __device__ ~WgStamp() {
+            if (threadIdx.x == 0 && blockIdx.x < 65536) {
+                g_wg[4 * blockIdx.x] = t0;
+                g_wg[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+                g_wg[4 * blockIdx.x + 2] = (unsigned long long)depth;
+                g_wg[4 * blockIdx.x + 3] = (unsigned long long)(long long)wl;
+            }
+        }
+    } stamp_{__builtin_amdgcn_s_memrealtime(), rng.y - rng.x, wave_last};
+#endif
+    const int sbase = seg_base(rng.x, tile);
+    const int seg = slot - sbase, lo = seg * kSegLen;
+    if (wave_last < lo) return;
+    const int hi = min(lo + kSegLen - 1, wave_last), kf = wave_last / kSegLen;
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
     float Gtex_bias = 0.f;  // tex_bias * sum_c dL/dtex[c]: the bias part of sum_c dL/dtex[c] * texel value
 #pragma unroll
     for (int c = 0; c < CM; ++c) Gtex_bias += Gtex[c];
     Gtex_bias *= tex_bias;
+    if (seg < kf) {
+        // start from the forward's checkpoint after this segment: T_k, and R T_k = sum over the splats behind the
+        // segment of w_j g_j + T_final (bg term) = (final - checkpoint accumulators) . upstream gradients
+        const float* ck = aux.ckpt + ((size_t)slot * 4 + quad) * aux.F * 64 + lane;
+        const float* fin = aux.ckpt + ((size_t)(sbase + kf) * 4 + quad) * aux.F * 64 + lane;
+        const float Tk = ck[0];
+        float back = (Gimg[0] * (fin[64] - ck[64]) + Gimg[1] * (fin[128] - ck[128])) + Gimg[2] * (fin[192] - ck[192]);
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < Cn) back += Gtex[c] * (fin[(4 + c) * 64] - ck[(4 + c) * 64]);
+        back += Ga * (Tk - T);  // the weights behind sum to T_k - T_final
+        if (GEO) {
+            const float* fg = fin + (4 + Cn) * 64;
+            const float* cg = ck + (4 + Cn) * 64;
+            back += Gd * (fg[0] - cg[0]);
+            back += (Gn[0] * (fg[64] - cg[64]) + Gn[1] * (fg[128] - cg[128])) + Gn[2] * (fg[192] - cg[192]);
+            if (dreg) back += Greg * ((Af * (fg[320] - cg[320]) - 2.0f * M1f * (fg[256] - cg[256])) + M2f * (Tk - T));
+        }
+        if (inside) {
+            R = (back + T * R) / Tk;
+            T = Tk;
+        }
+    }
     int tex_S;
     {
         float gm = 0.f;
@@ -823,12 +962,12 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     for (int i = lane; i < kTexStage; i += 64) s_texq[i] = 0;
     const size_t vm_base = visit_mask_base(rng.x, tile);
 
-    for (int wd = wave_last >> 6; wd >= 0; --wd) {
+    for (int wd = hi >> 6; wd >= (lo >> 6); --wd) {
         const int pos0 = wd << 6;
-        // the word's splats this wave visits: the forward's cull bits for this quadrant (every splat when the
-        // forward recorded none), clipped to the wave's last contributor
-        unsigned long long todo = visit_masks ? visit_masks[(vm_base + wd) * 4 + quad] : ~0ull;
-        const int lim = wave_last - pos0 + 1;
+        // the word's splats this wave visits: the forward's cull bits for this quadrant, clipped to the segment's
+        // end (the wave's last contributor in the last segment)
+        unsigned long long todo = aux.masks[(vm_base + wd) * 4 + quad];
+        const int lim = hi - pos0 + 1;
         if (lim < 64) todo &= (1ull << lim) - 1ull;
         if (!todo) continue;
         // lane k <-> position pos0 + k: splat id and emission slot, loaded once per word (coalesced)
@@ -1296,7 +1435,7 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
                                 const float* background, const float* records, const int32_t* tile_ranges,
                                 const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                                 int64_t n_texels, float tex_scale, float tex_bias, float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
-                                float* out_normal, float* state, uint64_t* visit_masks, void* stream) {
+                                float* out_normal, float* state, int64_t n_isect, void* aux, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_fwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_fwd: channels must be in [1, 8] (got %d)",
@@ -1309,18 +1448,23 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
     const bool geo = out_depth || out_reg || out_normal;
     GSTEX_REQUIRE(!geo || (out_depth && out_reg && out_normal),
                   "gstex_raster_fwd: out_depth, out_reg and out_normal must be all given or all NULL");
+    GSTEX_REQUIRE(n_isect >= 0 && n_isect < (int64_t)INT32_MAX, "gstex_raster_fwd: n_isect out of range");
     const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
     CamArgs dc = to_device_camera(*cam);
     hipStream_t st = as_stream(stream);
     const int nblk = tiles_x * tiles_y;
+    const AuxLayout al = aux_layout(n_isect, nblk, channels);
+    const AuxPtrs ap = aux_ptrs(aux, al);
+    // units the forward never reaches keep cost 0 (the backward skips them)
+    if (aux && hipMemsetAsync(ap.cost, 0, (size_t)al.n_units * 4, st) != hipSuccess)
+        return launch_status("gstex_raster_fwd (aux)");
 #define GSTEX_FWD(CC, GG)                                                                                      \
     raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,      \
                                                      (const float4*)records, (const int2*)tile_ranges,        \
                                                      tile_order, sorted_ids, texture, (int)n_texels, tex_scale,        \
                                                      tex_bias, out_img,                                                   \
                                                      out_depth, out_reg,                                                  \
-                                                     out_alpha, out_tex, out_normal, (float4*)state,                  \
-                                                     (unsigned long long*)visit_masks)
+                                                     out_alpha, out_tex, out_normal, (float4*)state, ap)
     if (channels == 3 && geo) GSTEX_FWD(3, true);
     else if (channels == 3) GSTEX_FWD(3, false);
     else if (channels == 6 && geo) GSTEX_FWD(6, true);
@@ -1333,18 +1477,18 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
 
 extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                                 const float* background, const float* records, const int32_t* tile_ranges,
-                                const int32_t* tile_order, const int32_t* sorted_ids, const int32_t* sorted_slots,
+                                const int32_t* sorted_ids, const int32_t* sorted_slots,
                                 const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
                                 const float* state, const float* v_img,
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
-                                float* v_texture, const uint64_t* visit_masks, void* stream) {
+                                float* v_texture, void* aux, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
     int rc = check_settings(settings);
     if (rc) return rc;
-    GSTEX_REQUIRE(tile_ranges && state, "gstex_raster_bwd: null pointer");
+    GSTEX_REQUIRE(tile_ranges && state && aux, "gstex_raster_bwd: null pointer (tile_ranges, state and the forward's aux)");
     GSTEX_REQUIRE(n_isect >= 0 && n_isect < (int64_t)INT32_MAX, "gstex_raster_bwd: n_isect out of range");
     GSTEX_REQUIRE(n_isect == 0 || (partials && row_flags && sorted_ids && sorted_slots),
                   "gstex_raster_bwd: null pair buffer");
@@ -1355,17 +1499,19 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
     CamArgs dc = to_device_camera(*cam);
     hipStream_t st = as_stream(stream);
+    const AuxLayout al = aux_layout(n_isect, tiles_x * tiles_y, channels);
+    const AuxPtrs ap = aux_ptrs(aux, al);
     if (n_isect > 0 && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
-    const int nblk = tiles_x * tiles_y * 4;  // one wave per (tile, 8x8 quadrant)
+    rc = gstex_unit_order((int32_t)al.n_units, ap.cost, ap.order, stream);  // costliest units first
+    if (rc) return rc;
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
 #define GSTEX_BWD(CC, GG)                                                                                      \
-    raster_bwd_kernel<CC, GG><<<nblk, 64, 0, st>>>(                                                            \
+    raster_bwd_kernel<CC, GG><<<(unsigned)al.n_units, 64, 0, st>>>(                                            \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
-        tile_order, sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,    \
-        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture,      \
-        (const unsigned long long*)visit_masks)
+        sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
+        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
     else if (channels == 3) GSTEX_BWD(3, true);
     else if (channels == 6 && !geo) GSTEX_BWD(6, false);
@@ -1376,9 +1522,9 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     return launch_status("gstex_raster_bwd");
 }
 
-extern "C" size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles) {
-    if (n_isect < 0 || n_tiles < 0) return 0;
-    return ((size_t)((n_isect + 63) / 64) + (size_t)n_tiles + 1) * 4;
+extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels) {
+    if (n_isect < 0 || n_tiles < 0 || channels < 1 || channels > 8) return 0;
+    return aux_layout(n_isect, n_tiles, channels).bytes;
 }
 
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,

@@ -289,6 +289,15 @@ def tile_order(tile_ranges: torch.Tensor) -> torch.Tensor:
     return order
 
 
+def unit_order(unit_cost: torch.Tensor) -> torch.Tensor:
+    """gstex_unit_order: int32 unit indices by descending cost (the backward's launch order, computed inside
+    gstex_raster_bwd; exposed for tests)."""
+    uc = _i32(unit_cost, "unit_cost", (None,))
+    order = torch.empty_like(uc)
+    call("gstex_unit_order", uc.shape[0], ptr(uc), ptr(order), _stream(uc))
+    return order
+
+
 # ----------------------------------------------------------------------------------------
 # texture_gaussians
 # ----------------------------------------------------------------------------------------
@@ -371,16 +380,18 @@ class _TextureGaussians(torch.autograd.Function):
             geo_ptrs = (None, None, None)
             ctx.mark_non_differentiable(depth, reg, normal)
         # per (tile, wave, splat) cull bits of the forward for the backward
-        vmask = None
+        # the forward's record for the backward (cull bits, per-unit costs, checkpoints of deep tile lists)
+        aux = None
+        n_isect = sorted_ids.shape[0]
         if needs_bwd:
-            words = int(_lib.load().gstex_visit_mask_words(sorted_ids.shape[0], tile_ranges.shape[0]))
-            vmask = torch.empty((words,), device=dev, dtype=torch.int64)
+            nb = int(_lib.load().gstex_raster_aux_bytes(n_isect, tile_ranges.shape[0], C))
+            aux = torch.empty((nb,), device=dev, dtype=torch.uint8)
         _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
              ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), geo_ptrs[0], geo_ptrs[1], ptr(alpha),
              ptr(tex), geo_ptrs[2],
-             ptr(state), ptr(vmask), st)
-        ctx.vmask = vmask
+             ptr(state), n_isect, ptr(aux), st)
+        ctx.aux = aux
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
                               bg if bg is not None else vm)
@@ -419,11 +430,11 @@ class _TextureGaussians(torch.autograd.Function):
         row_flags = torch.empty((n_isect,), device=dev, dtype=torch.int32)
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
-        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
+        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
-                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.vmask), st)
-        ctx.vmask = None
+                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)
+        ctx.aux = None
         if ctx.sink:
             if ctx.on_texture_grad is not None:
                 ctx.on_texture_grad()  # the texel gradient is complete in stream order

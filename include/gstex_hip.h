@@ -127,34 +127,37 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
 /* Forward composite. Outputs are [H][W][k] row-major. state[H*W][4] = {T_final, M1, M2,
  * last_contributor (as int bits)} is saved for the backward pass. background is a device
  * float[3] (or NULL = black) added as T_final * background.  out_depth, out_reg and out_normal may be
- * NULL together (geometric outputs not produced; the backward then takes no gradient for them). */
+ * NULL together (geometric outputs not produced; the backward then takes no gradient for them).
+ * aux (NULL = no backward follows): a gstex_raster_aux_bytes(n_isect, n_tiles, channels) device workspace the
+ * forward fills for the backward -- its per-wave cull bits (per tile, 8x8 pixel quadrant and tile-list position),
+ * per backward unit (tile, quadrant, segment of 256 list positions) the number of splats it evaluated, and
+ * per-pixel checkpoints (transmittance and accumulators) at the segment boundaries of deep lists.  Pass the same
+ * aux, untouched, to gstex_raster_bwd. */
 int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                      int64_t n_texels, float tex_scale, float tex_bias,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
-                     float* out_tex, float* out_normal, float* state, uint64_t* visit_masks, void* stream);
-/* visit_masks (ABI 4; NULL = not recorded / not used): gstex_visit_mask_words(n_isect, n_tiles) 64-bit
- * words in which the forward records its per-wave cull (per tile, wave of 64 pixels and tile-list
- * position: can the splat reach alpha >= 1/255 in that wave's 8x8 block); the backward reads them instead
- * of re-running the geometric test.  Pass the same buffer to both. */
-size_t gstex_visit_mask_words(int64_t n_isect, int32_t n_tiles);
-/* Backward composite. Needs the forward state and the same tile_order. Any of v_img ... v_normal may be
- * NULL (that output's gradient is zero).  Texel blocks that run past n_texels (corrupt texture_dims) are
- * neither read nor written.  One wave per (tile, 8x8 pixel quadrant q): for every pair (emission slot s) the
- * quadrant contributes to, writes the row partials[(4 s + q) * GSTEX_PARTIAL_FLOATS ...] (n_isect * 4 rows
- * allocated; rows of pairs a quadrant does not reach are never written) and sets byte q of row_flags[s]
- * (n_isect uint32 words, zeroed by this call on the stream); accumulates (+=) texel gradients into
- * v_texture[n_texels][C]. */
+                     float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
+                     void* stream);
+size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels);
+/* Launch order of n_units backward units by descending unit_cost (ties by index; above 65536 units, index
+ * order).  gstex_raster_bwd calls it on its aux; exported for tests. */
+int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, void* stream);
+/* Backward composite. Needs the forward state and the forward's aux (required; the backward also writes its
+ * launch order into it).  Any of v_img ... v_normal may be NULL (that output's gradient is zero).  Texel blocks
+ * that run past n_texels (corrupt texture_dims) are neither read nor written.  One wave per backward unit (tile,
+ * 8x8 pixel quadrant q, segment): for every pair (emission slot s) the quadrant contributes to, writes the row
+ * partials[(4 s + q) * GSTEX_PARTIAL_FLOATS ...] (n_isect * 4 rows allocated; rows of pairs a quadrant does not
+ * reach are never written) and sets byte q of row_flags[s] (n_isect uint32 words, zeroed by this call on the
+ * stream); accumulates (+=) texel gradients into v_texture[n_texels][C]. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
-                     const int32_t* tile_order, const int32_t* sorted_ids,
-                     const int32_t* sorted_slots, const float* texture, int64_t n_texels,
-                     float tex_scale, float tex_bias, const float* state, const float* v_img,
-                     const float* v_depth,
-                     const float* v_reg, const float* v_alpha, const float* v_tex,
-                     const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
-                     float* v_texture, const uint64_t* visit_masks, void* stream);
+                     const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
+                     int64_t n_texels, float tex_scale, float tex_bias, const float* state,
+                     const float* v_img, const float* v_depth, const float* v_reg, const float* v_alpha,
+                     const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
+                     uint32_t* row_flags, float* v_texture, void* aux, void* stream);
 /* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
  * them to the splat parameters. Outputs are overwritten. */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,

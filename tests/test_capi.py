@@ -67,21 +67,30 @@ def test_bin_sort_rejects_non16_block(lib):
 def test_raster_rejects_bad_channels_and_settings(lib):
     cam = _cam()
     rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 9, 0, None, None, None, None, None, None, 0, 1.0,
-                      0.0, None, None, None, None, None, None, None, None, None)
+                      0.0, None, None, None, None, None, None, None, 0, None, None)
     assert rc == 1 and "channels" in msg
     rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 3, 1 << 2, None, None, None, None, None, None, 0,
-                      1.0, 0.0, None, None, None, None, None, None, None, None, None)
+                      1.0, 0.0, None, None, None, None, None, None, None, 0, None, None)
     assert rc == 3 and "unsupported settings" in msg
     bad = _cam(block=8)
-    rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, None, 0,
+    rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, 0,
                       1.0, 0.0, None, None, None, None, None, None, None, 0, None, None, None, None, None)
     assert rc == 1 and "block_width" in msg
 
 
-def test_visit_mask_words(lib):
-    # per tile ceil-aligned runs of 64-bit words, 4 waves interleaved: (ceil(I / 64) + n_tiles + 1) * 4
-    assert lib.gstex_visit_mask_words(0, 1) == 8
-    assert lib.gstex_visit_mask_words(1_915_389, 2500) == ((1_915_389 + 63) // 64 + 2501) * 4
+def test_raster_aux_bytes(lib):
+    # cull-bit words (ceil(I / 64) + n_tiles + 1) * 4 x 8 B, then per backward unit (4 per slot; ceil(I / 256) +
+    # n_tiles + 1 slots) cost + order (4 B each) and a checkpoint of (4 + C + 6) fields x 64 lanes, slot tiles
+    # (4 B per slot), each array 256-B aligned
+    def al(x):
+        return (x + 255) // 256 * 256
+
+    for n_isect, n_tiles, c in [(0, 1, 3), (1_915_389, 2500, 3), (12345, 77, 6)]:
+        slots = (n_isect + 255) // 256 + n_tiles + 1
+        expect = (al(((n_isect + 63) // 64 + n_tiles + 1) * 32) + 2 * al(slots * 16) + al(slots * 4)
+                  + al(slots * 4 * (4 + c + 6) * 64 * 4))
+        assert lib.gstex_raster_aux_bytes(n_isect, n_tiles, c) == expect
+    assert lib.gstex_raster_aux_bytes(-1, 1, 3) == 0 and lib.gstex_raster_aux_bytes(1, 1, 9) == 0
 
 
 def test_sh_rejects_degree(lib):

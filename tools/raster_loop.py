@@ -78,6 +78,12 @@ def main():
             names = ["load+barrier", "place+cull", "visits", "barrier_pre_combine", "combine+flush", "barrier_end",
                      "prologue", "-"]
         print("stats/launch:", {k: round(v / n) for k, v in zip(names, buf)})
+    if hasattr(lib, "gstex_debug_wg") and os.environ.get("GSTEX_WG_DUMP"):  # GSTEX_STATS=3: last launch's waves
+        import ctypes
+        import numpy as np
+        buf = (ctypes.c_ulonglong * (65536 * 4))()
+        lib.gstex_debug_wg(buf)
+        np.save(os.environ["GSTEX_WG_DUMP"], np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4))
     print(f"fwd+bwd+preprocess {dt * 1e3:.3f} ms/iter  visible={int((nth > 0).sum())} isect={int(nth.sum())} "
           f"kernel_ms={kt}")
 
