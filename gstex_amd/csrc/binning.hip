@@ -375,18 +375,11 @@ constexpr int kRankChunk = 4096;
 // Sort keys, all unique (the item index sits in the low bits), ascending = launch order:
 //   SRC 0: tile t's bucket size from tile_ranges (pairs [start, end)), 14-bit tile index;
 //   SRC 1: the same from the n+1 exclusive-scan starts;
-//   SRC 2: a backward unit's cost estimate (gstex_unit_order), 16-bit unit index.
-constexpr int kUnitOrderCap = 1 << 16;
 template <int SRC>
 __device__ __forceinline__ unsigned order_key(const int32_t* r, int t) {
-    if constexpr (SRC == 2) {
-        const unsigned c = (unsigned)min(0xFFFF, max(0, r[t]));
-        return ((0xFFFFu - c) << 16) | (unsigned)t;  // cost desc, unit asc
-    } else {
-        const int c = SRC == 1 ? r[t + 1] - r[t] : r[2 * t + 1] - r[2 * t];
-        const unsigned cnt = (unsigned)min((int)kOrderMaxCount, c);
-        return ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
-    }
+    const int c = SRC == 1 ? r[t + 1] - r[t] : r[2 * t + 1] - r[2 * t];
+    const unsigned cnt = (unsigned)min((int)kOrderMaxCount, c);
+    return ((kOrderMaxCount - cnt) << kOrderTileBits) | (unsigned)t;  // count desc, tile asc
 }
 
 template <int SRC>
@@ -538,15 +531,68 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
     return launch_status("gstex_tile_order");
 }
 
-extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, void* stream) {
+// Backward unit order (gstex_unit_order): a counting sort by descending cost, clamped to kUnitBuckets - 1 (the
+// forward's per-segment counts are <= 256): histogram (LDS per workgroup, one global atomic per bucket and
+// workgroup), exclusive scan of the buckets from the costliest down, scatter (each workgroup reserves one range
+// per bucket).  Order inside a bucket is unspecified -- scheduling only, outputs do not depend on it.
+constexpr int kUnitBuckets = 1024;
+constexpr int kUnitsPerBlock = 2048;
+
+__device__ __forceinline__ int unit_bucket(int c) { return kUnitBuckets - 1 - min(max(c, 0), kUnitBuckets - 1); }
+
+__global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __restrict__ cost,
+                                                        int32_t* __restrict__ hist) {
+    __shared__ int s_h[kUnitBuckets];
+    for (int i = threadIdx.x; i < kUnitBuckets; i += 256) s_h[i] = 0;
+    __syncthreads();
+    const int u0 = blockIdx.x * kUnitsPerBlock;
+    for (int u = u0 + threadIdx.x; u < min(n, u0 + kUnitsPerBlock); u += 256) atomicAdd(&s_h[unit_bucket(cost[u])], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kUnitBuckets; i += 256)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+__global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int32_t* __restrict__ hist) {
+    // in place: hist[b] -> number of units in buckets < b (bucket 0 = the costliest)
+    __shared__ int s[kUnitBuckets];
+    const int t = threadIdx.x;
+    s[t] = hist[t];
+    __syncthreads();
+    for (int o = 1; o < kUnitBuckets; o <<= 1) {
+        const int v = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    hist[t] = s[t] - hist[t];
+}
+
+__global__ __launch_bounds__(256) void unit_scatter_kernel(int n, const int32_t* __restrict__ cost,
+                                                           int32_t* __restrict__ next, int32_t* __restrict__ order) {
+    __shared__ int s_h[kUnitBuckets];
+    for (int i = threadIdx.x; i < kUnitBuckets; i += 256) s_h[i] = 0;
+    __syncthreads();
+    const int u0 = blockIdx.x * kUnitsPerBlock;
+    const int u1 = min(n, u0 + kUnitsPerBlock);
+    for (int u = u0 + threadIdx.x; u < u1; u += 256) atomicAdd(&s_h[unit_bucket(cost[u])], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kUnitBuckets; i += 256)
+        if (s_h[i]) s_h[i] = atomicAdd(&next[i], s_h[i]);  // this workgroup's range start in bucket i
+    __syncthreads();
+    for (int u = u0 + threadIdx.x; u < u1; u += 256) order[atomicAdd(&s_h[unit_bucket(cost[u])], 1)] = u;
+}
+
+extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, int32_t* scratch,
+                                void* stream) {
     GSTEX_REQUIRE(n_units >= 0, "gstex_unit_order: invalid n_units %d", n_units);
     if (n_units == 0) return GSTEX_OK;
-    GSTEX_REQUIRE(unit_cost && unit_order, "gstex_unit_order: null pointer");
-    if (n_units > kUnitOrderCap) {  // beyond the 16-bit unit index of the keys: index order
-        iota_kernel<<<div_up(n_units, 256), 256, 0, as_stream(stream)>>>(n_units, unit_order);
+    GSTEX_REQUIRE(unit_cost && unit_order && scratch, "gstex_unit_order: null pointer");
+    hipStream_t st = as_stream(stream);
+    if (hipMemsetAsync(scratch, 0, kUnitBuckets * sizeof(int32_t), st) != hipSuccess)
         return launch_status("gstex_unit_order");
-    }
-    tile_rank_kernel<2><<<div_up(n_units, kRankTiles), kRankThreads, 0, as_stream(stream)>>>(n_units, unit_cost,
-                                                                                            unit_order);
+    const int nb = div_up(n_units, kUnitsPerBlock);
+    unit_hist_kernel<<<nb, 256, 0, st>>>(n_units, unit_cost, scratch);
+    unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(scratch);
+    unit_scatter_kernel<<<nb, 256, 0, st>>>(n_units, unit_cost, scratch, unit_order);
     return launch_status("gstex_unit_order");
 }

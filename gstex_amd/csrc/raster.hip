@@ -252,11 +252,12 @@ struct AuxPtrs {
     unsigned long long* masks;
     int32_t* cost;       // [n_units]
     int32_t* order;      // [n_units] (written by the backward)
+    int32_t* order_ws;   // [1024] gstex_unit_order scratch
     int32_t* slot_tile;  // [n_slots]
     float* ckpt;         // [n_units][F][64]
     int F;
 };
-struct AuxLayout { size_t masks, cost, order, slot_tile, ckpt, bytes; int64_t n_slots, n_units; int F; };
+struct AuxLayout { size_t masks, cost, order, order_ws, slot_tile, ckpt, bytes; int64_t n_slots, n_units; int F; };
 __host__ inline AuxLayout aux_layout(int64_t n_isect, int n_tiles, int C) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     AuxLayout a;
@@ -267,6 +268,7 @@ __host__ inline AuxLayout aux_layout(int64_t n_isect, int n_tiles, int C) {
     a.masks = o; o = al(o + (((size_t)n_isect + 63) / 64 + (size_t)n_tiles + 1) * 4 * sizeof(uint64_t));
     a.cost = o; o = al(o + (size_t)a.n_units * 4);
     a.order = o; o = al(o + (size_t)a.n_units * 4);
+    a.order_ws = o; o = al(o + 1024 * 4);
     a.slot_tile = o; o = al(o + (size_t)a.n_slots * 4);
     a.ckpt = o; o = al(o + (size_t)a.n_units * a.F * 64 * sizeof(float));
     a.bytes = o;
@@ -278,6 +280,7 @@ __host__ inline AuxPtrs aux_ptrs(void* aux, const AuxLayout& a) {
     p.masks = aux ? (unsigned long long*)(b + a.masks) : nullptr;
     p.cost = aux ? (int32_t*)(b + a.cost) : nullptr;
     p.order = aux ? (int32_t*)(b + a.order) : nullptr;
+    p.order_ws = aux ? (int32_t*)(b + a.order_ws) : nullptr;
     p.slot_tile = aux ? (int32_t*)(b + a.slot_tile) : nullptr;
     p.ckpt = aux ? (float*)(b + a.ckpt) : nullptr;
     p.F = a.F;
@@ -1503,7 +1506,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     const AuxPtrs ap = aux_ptrs(aux, al);
     if (n_isect > 0 && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
-    rc = gstex_unit_order((int32_t)al.n_units, ap.cost, ap.order, stream);  // costliest units first
+    rc = gstex_unit_order((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, stream);  // costliest units first
     if (rc) return rc;
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));

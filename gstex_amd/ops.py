@@ -294,7 +294,8 @@ def unit_order(unit_cost: torch.Tensor) -> torch.Tensor:
     gstex_raster_bwd; exposed for tests)."""
     uc = _i32(unit_cost, "unit_cost", (None,))
     order = torch.empty_like(uc)
-    call("gstex_unit_order", uc.shape[0], ptr(uc), ptr(order), _stream(uc))
+    scratch = torch.empty((1024,), device=uc.device, dtype=torch.int32)
+    call("gstex_unit_order", uc.shape[0], ptr(uc), ptr(order), ptr(scratch), _stream(uc))
     return order
 
 

@@ -141,9 +141,11 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
                      void* stream);
 size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels);
-/* Launch order of n_units backward units by descending unit_cost (ties by index; above 65536 units, index
- * order).  gstex_raster_bwd calls it on its aux; exported for tests. */
-int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, void* stream);
+/* Launch order of n_units backward units by descending unit_cost (costs clamped to 1023; order within equal
+ * costs unspecified), scratch = 1024 int32 of device workspace.  gstex_raster_bwd calls it on its aux;
+ * exported for tests. */
+int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, int32_t* scratch,
+                     void* stream);
 /* Backward composite. Needs the forward state and the forward's aux (required; the backward also writes its
  * launch order into it).  Any of v_img ... v_normal may be NULL (that output's gradient is zero).  Texel blocks
  * that run past n_texels (corrupt texture_dims) are neither read nor written.  One wave per backward unit (tile,

@@ -217,19 +217,17 @@ def test_tile_order_is_largest_first(n_tiles):
     assert np.array_equal(got, expect)
 
 
-@pytest.mark.parametrize("n_units", [1, 10000, 65536, 65537])
+@pytest.mark.parametrize("n_units", [1, 10000, 65537, 200003])
 def test_unit_order_is_costliest_first(n_units):
     from gstex_amd.ops import unit_order
 
     g = np.random.default_rng(n_units)
-    cost = g.integers(0, 3000, n_units).astype(np.int32)
-    cost[g.integers(0, n_units, max(1, n_units // 50))] = 1 << 17  # beyond the 0xFFFF clamp: ties
+    cost = g.integers(0, 300, n_units).astype(np.int32)
+    cost[g.integers(0, n_units, max(1, n_units // 50))] = 1 << 17  # beyond the 1023 clamp
     got = unit_order(torch.from_numpy(cost).to(DEV)).cpu().numpy()
-    if n_units > 65536:
-        assert np.array_equal(got, np.arange(n_units)), "above 65536 units the order is the index order"
-        return
-    expect = np.lexsort((np.arange(n_units), -np.minimum(cost, 0xFFFF)))
-    assert np.array_equal(got, expect)
+    assert np.array_equal(np.sort(got), np.arange(n_units)), "not a permutation"
+    c = np.minimum(cost, 1023)[got]
+    assert np.all(np.diff(c) <= 0), "not in descending cost order"
 
 
 def test_outputs_independent_of_launch_order(monkeypatch):

@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 # same step/warmup counts as the default bench line, so the steady-state averages agree
-BENCH="python3 bench.py --no-cpu-baseline"
+BENCH="python3 bench.py --no-cpu-baseline --no-sub"  # the timed train-step loop only
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- $BENCH > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- $BENCH > "$OUT/bench_write.log" 2>&1
