@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.a
 
 ABI_VERSION = 6
 REC_FLOATS = 32
-PARTIAL_FLOATS = 24
+PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows (24 or 32 used)
 SETTING_AA_BLUR = 1 << 9
 SETTING_DIST_REG = 1 << 10
 SETTING_EDIT = 1 << 13

@@ -295,14 +295,33 @@ __device__ __forceinline__ Rect tile_rect(float cx, float cy, float ex, float ey
     return r;
 }
 
-// Raster record layout (GSTEX_REC_FLOATS = 32 floats = 128 B, one cache line).
+// Splat -> pixel in affine form.  With the anchored rows (Tu'.z = Tv'.z = 0) the homogeneous point of pixel
+// offset d = pixel - anchor is p = k x l, k = d.x Tw - Tu', l = d.y Tw - Tv', which is affine in d:
+//   p = d.x A + d.y B + P0,   A = Tv' x Tw,  B = Tw x Tu',  P0 = Tu' x Tv' = (0, 0, Pz)
+// (the d.x d.y Tw x Tw term vanishes).  The raster evaluates p this way: 6 products instead of 2 x 3 + 6, and no
+// per-pixel cancellation of the d.x d.y terms.
+struct AffineHomog { f3 A, B; float Pz; };
+__device__ __forceinline__ AffineHomog affine_homog(f3 Tu, f3 Tv, f3 Tw) {  // Tu.z = Tv.z = 0 (anchored)
+    AffineHomog a;
+    a.A = f3{Tw.z * Tv.y, -(Tw.z * Tv.x), Tw.y * Tv.x - Tw.x * Tv.y};
+    a.B = f3{-(Tu.y * Tw.z), Tu.x * Tw.z, Tu.y * Tw.x - Tu.x * Tw.y};
+    a.Pz = Tu.x * Tv.y - Tu.y * Tv.x;
+    return a;
+}
+// dL/d(A, B, P0) -> dL/d(Tu', Tv', Tw) (c = a x b: dL/da = b x dL/dc, dL/db = dL/dc x a), including the
+// gradients of the z-components of Tu', Tv' (zero-valued, but the anchored vjp holds the anchor fixed)
+__device__ __forceinline__ void affine_homog_vjp(f3 Tu, f3 Tv, f3 Tw, f3 dA, f3 dB, f3 dP0, f3& dTu, f3& dTv,
+                                                 f3& dTw) {
+    dTu = add3(cross3(dB, Tw), cross3(Tv, dP0));
+    dTv = add3(cross3(Tw, dA), cross3(dP0, Tu));
+    dTw = add3(cross3(dA, Tv), cross3(Tu, dB));
+}
+
+// Raster record layout (GSTEX_REC_FLOATS = 32 floats = 128 B, one cache line), as 8 float4 planes.
 enum RecField {
-    R_TU = 0, R_TV = 3, R_TW = 6, R_XY = 9, R_OPAC = 11, R_RGB = 12, R_NRM = 15,
-    R_TU0 = 18, R_AUU = 19, R_AUV = 20, R_TV0 = 21, R_AVU = 22, R_AVV = 23,
-    R_H = 24, R_W = 25, R_OFF = 26, R_GID = 27, R_XA = 28, R_YA = 29,
-    // contribution box (pixel-centre coordinates) in the slots the anchored form leaves free
-    // (Tu'.z and Tv'.z are identically 0 and never read)
-    R_BX0 = 2, R_BX1 = 5, R_BY0 = 30, R_BY1 = 31
+    R_A = 0, R_B = 3, R_PZ = 6, R_TW = 7, R_XY = 10, R_OPAC = 12, R_RGB = 13, R_NRM = 16,
+    R_TU0 = 19, R_AUU = 20, R_AUV = 21, R_TV0 = 22, R_AVU = 23, R_AVV = 24,
+    R_H = 25, R_W = 26, R_OFF = 27, R_XA = 28, R_YA = 29  // 30, 31 unused
 };
 
 // Screen box of the projected disc u^2 + v^2 <= c2 (compute_aabb with a general cutoff).
@@ -345,11 +364,16 @@ __device__ __forceinline__ void contribution_box(const Homog& h, float cx, float
     y1 = fmaxf(ey1, cy + r2) + 1.0f;
 }
 
-// Partial layout (GSTEX_PARTIAL_FLOATS = 24).
+// Partial-row layout: dL/d(A, B, P0) of the affine homography, the AA low-pass centre gradient, opacity, colour,
+// texture-coordinate affine, and (rows of a backward with depth / normal gradients only) normal and the direct
+// dL/dTw of the depth.  A row holds 24 values (flag 1) or, with depth / normal gradients, 32 (flag 2); rows
+// are GSTEX_PARTIAL_FLOATS = 32 floats apart.
 enum PartField {
-    P_TU = 0, P_TV = 3, P_TW = 6, P_XY = 9, P_OPAC = 11, P_RGB = 12, P_NRM = 15,
-    P_TU0 = 18, P_AUU = 19, P_AUV = 20, P_TV0 = 21, P_AVU = 22, P_AVV = 23
+    P_A = 0, P_B = 3, P_P0 = 6, P_XY = 9, P_OPAC = 11, P_RGB = 12,
+    P_TU0 = 15, P_AUU = 16, P_AUV = 17, P_TV0 = 18, P_AVU = 19, P_AVV = 20, P_NRM = 21, P_TW = 24
 };
+constexpr int kPartRow = 24;     // values per row without geometry gradients
+constexpr int kPartRowGeo = 32;  // with (27 used)
 
 // Bilinear lookup into one splat's h x w texel block (corner-aligned: texel (i,j) sits at uv
 // (i/h, j/w), matching texture_dims_to_query, jagged_texture.py:23-34; clamp to edge).

@@ -109,7 +109,7 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
                         // (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
-constexpr int kNP = GSTEX_PARTIAL_FLOATS;     // 24
+constexpr int kRowStride = GSTEX_PARTIAL_FLOATS;  // 32 floats between partial rows
 
 // ------------------------------------------------------------------------------------------
 // setup: per-splat record
@@ -139,8 +139,10 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     f3 um = mk3(umap[3 * g], umap[3 * g + 1], umap[3 * g + 2]);
     f3 vm = mk3(vmap[3 * g], vmap[3 * g + 1], vmap[3 * g + 2]);
     float r[GSTEX_REC_FLOATS];
-    r[R_TU + 0] = h.Tu.x; r[R_TU + 1] = h.Tu.y; r[R_TU + 2] = h.Tu.z;
-    r[R_TV + 0] = h.Tv.x; r[R_TV + 1] = h.Tv.y; r[R_TV + 2] = h.Tv.z;
+    const AffineHomog ah = affine_homog(h.Tu, h.Tv, h.Tw);
+    r[R_A + 0] = ah.A.x; r[R_A + 1] = ah.A.y; r[R_A + 2] = ah.A.z;
+    r[R_B + 0] = ah.B.x; r[R_B + 1] = ah.B.y; r[R_B + 2] = ah.B.z;
+    r[R_PZ] = ah.Pz;
     r[R_TW + 0] = h.Tw.x; r[R_TW + 1] = h.Tw.y; r[R_TW + 2] = h.Tw.z;
     r[R_XY + 0] = centers[2 * g]; r[R_XY + 1] = centers[2 * g + 1];
     r[R_OPAC] = opacities[g];
@@ -155,11 +157,10 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     r[R_H] = __int_as_float(tdims[3 * g]);
     r[R_W] = __int_as_float(tdims[3 * g + 1]);
     r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
-    r[R_GID] = __int_as_float(g);
     r[R_XA] = h.xa;
     r[R_YA] = h.ya;
-    contribution_box(splat_homography(cam, mu, su, sv, fr), centers[2 * g], centers[2 * g + 1], opacities[g],
-                     r[R_BX0], r[R_BX1], r[R_BY0], r[R_BY1]);
+    r[30] = 0.0f;
+    r[31] = 0.0f;
     float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
 #pragma unroll
     for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
@@ -169,13 +170,33 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
 // shared per-(pixel, splat) evaluation
 // ------------------------------------------------------------------------------------------
 struct Rec {
-    f3 Tu, Tv, Tw;
+    f3 A, B, Tw;
+    float Pz;
     float x, y, opac;
     float rgb[3], nrm[3];
     float tu0, auu, auv, tv0, avu, avv;
     int h, w, off;
     float xa, ya;
 };
+
+// Record planes (gstex_common.h RecField): A B | B Pz Tw | Tw xy | opac rgb | nrm tu0 | auu auv tv0 avu |
+// avv h w off | xa ya
+__device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, float4 d, float4 e, float4 f, float4 g,
+                                               float4 q) {
+    Rec r;
+    r.A = f3{a.x, a.y, a.z};
+    r.B = f3{a.w, b.x, b.y};
+    r.Pz = b.z;
+    r.Tw = f3{b.w, c.x, c.y};
+    r.x = c.z; r.y = c.w;
+    r.opac = d.x;
+    r.rgb[0] = d.y; r.rgb[1] = d.z; r.rgb[2] = d.w;
+    r.nrm[0] = e.x; r.nrm[1] = e.y; r.nrm[2] = e.z;
+    r.tu0 = e.w; r.auu = f.x; r.auv = f.y; r.tv0 = f.z; r.avu = f.w; r.avv = g.x;
+    r.h = __float_as_int(g.y); r.w = __float_as_int(g.z); r.off = __float_as_int(g.w);
+    r.xa = q.x; r.ya = q.y;
+    return r;
+}
 
 template <bool SGPR>
 __device__ __forceinline__ float4 uni4(float4 v) {  // wave-uniform value -> SGPRs
@@ -211,17 +232,7 @@ __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
     const float4 c = uni4<SGPR>(s[2 * NB + j]), d = uni4<SGPR>(s[3 * NB + j]);
     const float4 e = uni4<SGPR>(s[4 * NB + j]), f = uni4<SGPR>(s[5 * NB + j]);
     const float4 g = uni4<SGPR>(s[6 * NB + j]), q = uni4<SGPR>(s[7 * NB + j]);
-    Rec r;
-    r.Tu = f3{a.x, a.y, a.z};
-    r.Tv = f3{a.w, b.x, b.y};
-    r.Tw = f3{b.z, b.w, c.x};
-    r.x = c.y; r.y = c.z; r.opac = c.w;
-    r.rgb[0] = d.x; r.rgb[1] = d.y; r.rgb[2] = d.z;
-    r.nrm[0] = d.w; r.nrm[1] = e.x; r.nrm[2] = e.y;
-    r.tu0 = e.z; r.auu = e.w; r.auv = f.x; r.tv0 = f.y; r.avu = f.z; r.avv = f.w;
-    r.h = __float_as_int(g.x); r.w = __float_as_int(g.y); r.off = __float_as_int(g.z);
-    r.xa = q.x; r.ya = q.y;
-    return r;
+    return rec_from_planes(a, b, c, d, e, f, g, q);
 }
 
 // Visit-mask layout: tile t owns 64-bit words [ceil(start_t / 64) + t, + ceil(len_t / 64)) (disjoint across tiles);
@@ -290,27 +301,7 @@ __host__ inline AuxPtrs aux_ptrs(void* aux, const AuxLayout& a) {
 // The same record read from global memory at a wave-uniform address: scalar loads straight into SGPRs
 // (no LDS read, no v_readfirstlane per value).
 __device__ __forceinline__ Rec read_rec_global(const float4* __restrict__ rec) {
-    const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
-    const float4 e = rec[4], f = rec[5], g = rec[6], q = rec[7];
-    Rec r;
-    r.Tu = f3{a.x, a.y, a.z};
-    r.Tv = f3{a.w, b.x, b.y};
-    r.Tw = f3{b.z, b.w, c.x};
-    r.x = c.y; r.y = c.z; r.opac = c.w;
-    r.rgb[0] = d.x; r.rgb[1] = d.y; r.rgb[2] = d.z;
-    r.nrm[0] = d.w; r.nrm[1] = e.x; r.nrm[2] = e.y;
-    r.tu0 = e.z; r.auu = e.w; r.auv = f.x; r.tv0 = f.y; r.avu = f.z; r.avv = f.w;
-    r.h = __float_as_int(g.x); r.w = __float_as_int(g.y); r.off = __float_as_int(g.z);
-    r.xa = q.x; r.ya = q.y;
-    return r;
-}
-
-// Does splat j's contribution box overlap this wave's 16x4 block of pixel centres?
-template <int NB>
-__device__ __forceinline__ bool wave_overlaps(const float4* s, int j, float wx0, float wx1, float wy0, float wy1) {
-    const float bx0 = s[0 * NB + j].z, bx1 = s[1 * NB + j].y;
-    const float4 q = s[7 * NB + j];
-    return bx0 <= wx1 && bx1 >= wx0 && q.z <= wy1 && q.w >= wy0;
+    return rec_from_planes(rec[0], rec[1], rec[2], rec[3], rec[4], rec[5], rec[6], rec[7]);
 }
 
 // min over t in [lo, hi] of f(t) = |Q.xy + t A.xy|^2 - rm (Q.z + t A.z)^2 is <= 0?  (true when the slice
@@ -326,30 +317,28 @@ __device__ __forceinline__ bool conic_edge(float ax, float ay, float az, float q
 }
 
 // Can splat j reach alpha >= 1/255 anywhere in the wave's block of pixel centres [wx0, wx1] x [wy0, wy1]?
-// With the anchored record (Tu.z = Tv.z = 0) the homogeneous point p = k x l is affine in the pixel offset
-// d = pixel - anchor: p = (d.x A + d.y B) + (0, 0, Pz).  The pair passes iff rho3 = |p.xy|^2 / p.z^2 <= rm
-// = 2 ln(255 o) (or, with the AA filter, the disc 2 |pixel - centre|^2 <= rm): an ellipse (splats whose
-// disc crosses the camera plane were culled upstream), tested exactly against the rectangle -- anchor
-// inside, or an edge meeting it -- with a 1 % threshold margin and a 0.05 px larger rectangle, so the fp32
-// evaluation can never accept a pair the test rejected.
+// The homogeneous point is affine in the pixel offset d = pixel - anchor, p = d.x A + d.y B + (0, 0, Pz) (record
+// planes 0-1), so the pair passes iff rho3 = |p.xy|^2 / p.z^2 <= rm = 2 ln(255 o) (or, with the AA filter, the
+// disc 2 |pixel - centre|^2 <= rm): an ellipse (splats whose disc crosses the camera plane were culled
+// upstream), tested exactly against the rectangle -- anchor inside, or an edge meeting it -- with a 1 %
+// threshold margin and a 0.05 px larger rectangle, so the fp32 evaluation can never accept a pair the test
+// rejected.
 template <int NB>
-__device__ __forceinline__ bool conic_overlaps(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
-                                               bool aa) {
-    const float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], q = s[7 * NB + j];
-    const float opac = c.w;
+__device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
+                                             bool aa) {
+    const float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], d = s[3 * NB + j], q = s[7 * NB + j];
+    const float opac = d.x;
     if (!(opac * 255.0f > 1.0f)) return false;
     const float rm = 2.0f * logf(255.0f * opac) * 1.01f + 1e-2f;
     const float x0 = wx0 - 0.05f, x1 = wx1 + 0.05f, y0 = wy0 - 0.05f, y1 = wy1 + 0.05f;
     if (aa) {
-        const float ex = c.y - fminf(fmaxf(c.y, x0), x1), ey = c.z - fminf(fmaxf(c.z, y0), y1);
+        const float ex = c.z - fminf(fmaxf(c.z, x0), x1), ey = c.w - fminf(fmaxf(c.w, y0), y1);
         if (2.0f * (ex * ex + ey * ey) <= rm) return true;
     }
     const float xa = q.x, ya = q.y;
     if (xa >= x0 && xa <= x1 && ya >= y0 && ya <= y1) return true;
-    const float tux = a.x, tuy = a.y, tvx = a.w, tvy = b.x, twx = b.z, twy = b.w, twz = c.x;
-    const float Ax = twz * tvy, Ay = -(twz * tvx), Az = twy * tvx - twx * tvy;  // -(Tw x Tv)
-    const float Bx = -(tuy * twz), By = tux * twz, Bz = tuy * twx - tux * twy;  // -(Tu x Tw)
-    const float Pz = tux * tvy - tuy * tvx;                                     // (Tu x Tv).z
+    if (!GSTEX_CONIC_CULL) return true;
+    const float Ax = a.x, Ay = a.y, Az = a.z, Bx = a.w, By = b.x, Bz = b.y, Pz = b.z;
     const float dx0 = x0 - xa, dx1 = x1 - xa, dy0 = y0 - ya, dy1 = y1 - ya;
     return conic_edge(Ax, Ay, Az, dy0 * Bx, dy0 * By, Pz + dy0 * Bz, rm, dx0, dx1) ||
            conic_edge(Ax, Ay, Az, dy1 * Bx, dy1 * By, Pz + dy1 * Bz, rm, dx0, dx1) ||
@@ -357,15 +346,9 @@ __device__ __forceinline__ bool conic_overlaps(const float4* s, int j, float wx0
            conic_edge(Bx, By, Bz, dx1 * Ax, dx1 * Ay, Pz + dx1 * Az, rm, dy0, dy1);
 }
 
-template <int NB>
-__device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
-                                             bool aa) {
-    return wave_overlaps<NB>(s, j, wx0, wx1, wy0, wy1) && (!GSTEX_CONIC_CULL || conic_overlaps<NB>(s, j, wx0, wx1, wy0, wy1, aa));
-}
-
 struct Hit {
     float dx, dy, ipz, u, v, rho3, rho2, z, G, a_raw, alpha;
-    f3 k, l, p;
+    f3 p;
     bool use3;
 };
 
@@ -404,9 +387,8 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     // the callers see one predicate instead of three divergent exits (fewer exec-mask joins)
     h.dx = px - r.xa;
     h.dy = py - r.ya;
-    h.k = f3{h.dx * r.Tw.x - r.Tu.x, h.dx * r.Tw.y - r.Tu.y, h.dx * r.Tw.z};
-    h.l = f3{h.dy * r.Tw.x - r.Tv.x, h.dy * r.Tw.y - r.Tv.y, h.dy * r.Tw.z};
-    h.p = cross3(h.k, h.l);
+    // p = k x l in affine form (gstex_common.h affine_homog)
+    h.p = f3{h.dx * r.A.x + h.dy * r.B.x, h.dx * r.A.y + h.dy * r.B.y, (r.Pz + h.dx * r.A.z) + h.dy * r.B.z};
     const bool ok = h.p.z != 0.0f;
 #if GSTEX_FAST_EVAL
     h.ipz = __builtin_amdgcn_rcpf(h.p.z);
@@ -699,7 +681,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
 // Reduce-scatter butterfly over the 64 lanes, entirely on VALU cross-lane ops (no LDS traffic):
 // xor-32 and xor-16 halvings with v_permlane32_swap / v_permlane16_swap, xor-8 with DPP row_ror:8,
 // then an 8-lane all-reduce (quad_perm xor1, xor2, row_half_mirror).  On return, lane l with
-// (l & 7) == 0 holds the wave sums of values [12*b5 + 6*b4 + 3*b3 + 0..2] (b5,b4,b3 = bits of l).
+// (l & 7) == 0 holds the wave sums of values [NV/2 b5 + NV/4 b4 + NV/8 b3 + 0 .. NV/8 - 1] (b5,b4,b3 = bits of l).
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
     // every pattern used here reads a lane inside the same row, so the old value never shows: mov_dpp
@@ -707,31 +689,34 @@ __device__ __forceinline__ float dpp_f(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-__device__ __forceinline__ void wave_reduce24(float (&v)[kNP]) {
+template <int NV>
+__device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
+    static_assert(NV % 8 == 0, "reduce-scatter over 8 lane groups");
+    constexpr int H = NV / 2, Q = NV / 4, E = NV / 8;
     const int lane = threadIdx.x & 63;
     // permlane32_swap(a, b) leaves a = [a_lo, b_lo], b = [a_hi, b_hi]: a + b holds a's half-sum in
     // lanes 0-31 and b's in lanes 32-63 (likewise per row pair for permlane16_swap)
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 12]), false, false);
+    for (int i = 0; i < H; ++i) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + H]), false, false);
         v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 6]), false, false);
+    for (int i = 0; i < Q; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + Q]), false, false);
         v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
     {
         const bool hi = lane & 8;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const float send = hi ? v[i] : v[i + 3];
-            const float keep = hi ? v[i + 3] : v[i];
+        for (int i = 0; i < E; ++i) {
+            const float send = hi ? v[i] : v[i + E];
+            const float keep = hi ? v[i + E] : v[i];
             v[i] = keep + dpp_f<0x128>(send);  // row_ror:8 == lane ^ 8 inside a 16-lane row
         }
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < E; ++i) {
         v[i] = v[i] + dpp_f<0xB1>(v[i]);   // quad_perm [1,0,3,2]
         v[i] = v[i] + dpp_f<0x4E>(v[i]);   // quad_perm [2,3,0,1]
         v[i] = v[i] + dpp_f<0x141>(v[i]);  // row_half_mirror: the other quad of the 8-lane group
@@ -987,9 +972,10 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
-            float P[kNP];
+            constexpr int NP = GEO ? kPartRowGeo : kPartRow;
+            float P[NP];
 #pragma unroll
-            for (int i = 0; i < kNP; i += 2) {
+            for (int i = 0; i < NP; i += 2) {
                 // zero rows in 64-bit moves (one v_mov_b64 per register pair)
                 unsigned long long zz;
                 asm volatile("v_mov_b64 %0, 0" : "=v"(zz));
@@ -1090,38 +1076,43 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 const float dv3 = GEO ? drho * 2.0f * h.v + dz * r.Tw.y : drho * 2.0f * h.v;
                 du = h.use3 ? du + du3 : du;
                 dv = h.use3 ? dv + dv3 : dv;
-                const f3 dTw = GEO ? f3{h.use3 ? dz * h.u : 0.f, h.use3 ? dz * h.v : 0.f, dz} : f3{0.f, 0.f, 0.f};
                 P[P_XY + 0] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.x - px);
                 P[P_XY + 1] = h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.y - py);
                 const float ipz = h.ipz;
                 const f3 dp = f3{du * ipz, dv * ipz, -(du * h.u + dv * h.v) * ipz};
-                // nk = -dL/dk and nl = -dL/dl exactly (operands of the cross products swapped), so
-                // the Tu/Tv rows need no negation and Tw subtracts
-                const f3 nk = cross3(dp, h.l);
-                const f3 nl = cross3(h.k, dp);
-                P[P_TU + 0] = nk.x; P[P_TU + 1] = nk.y; P[P_TU + 2] = nk.z;
-                P[P_TV + 0] = nl.x; P[P_TV + 1] = nl.y; P[P_TV + 2] = nl.z;
-                P[P_TW + 0] = (dTw.x - h.dx * nk.x) - h.dy * nl.x;
-                P[P_TW + 1] = (dTw.y - h.dx * nk.y) - h.dy * nl.y;
-                P[P_TW + 2] = (dTw.z - h.dx * nk.z) - h.dy * nl.z;
+                // p = dx A + dy B + P0 (affine form): dL/dA = dp dx, dL/dB = dp dy, dL/dP0 = dp
+                P[P_A + 0] = dp.x * h.dx; P[P_A + 1] = dp.y * h.dx; P[P_A + 2] = dp.z * h.dx;
+                P[P_B + 0] = dp.x * h.dy; P[P_B + 1] = dp.y * h.dy; P[P_B + 2] = dp.z * h.dy;
+                P[P_P0 + 0] = dp.x; P[P_P0 + 1] = dp.y; P[P_P0 + 2] = dp.z;
+                if constexpr (GEO) {  // the depth's direct dependence on Tw (z = u Tw.x + v Tw.y + Tw.z)
+                    P[P_TW + 0] = h.use3 ? dz * h.u : 0.f;
+                    P[P_TW + 1] = h.use3 ? dz * h.v : 0.f;
+                    P[P_TW + 2] = dz;
+                }
             }
             if (__any(contrib)) {
                 if (GSTEX_ABLATE & 2) {
 #pragma unroll
-                    for (int i = 3; i < kNP; ++i) asm volatile("" ::"v"(P[i]));
+                    for (int i = 3; i < NP; ++i) asm volatile("" ::"v"(P[i]));
                 } else {
-                    wave_reduce24(P);
+                    wave_reduce<NP>(P);
                 }
-                // the (pair, quadrant) row: lanes 8k hold 3 consecutive values each; the flag marks it written
+                // the (pair, quadrant) row: lanes 8k hold NP / 8 consecutive values each; the flag (1: 24-value
+                // row, 2: 32-value row) marks it written
                 const int slot = __builtin_amdgcn_readlane(my_slot, j);
                 if ((lane & 7) == 0) {
-                    const int base = 12 * ((lane >> 5) & 1) + 6 * ((lane >> 4) & 1) + 3 * ((lane >> 3) & 1);
-                    float* dst = partials + ((size_t)slot * 4 + quad) * kNP + base;
-                    dst[0] = P[0];
-                    dst[1] = P[1];
-                    dst[2] = P[2];
+                    constexpr int E = NP / 8;
+                    const int base = (NP / 2) * ((lane >> 5) & 1) + (NP / 4) * ((lane >> 4) & 1) + E * ((lane >> 3) & 1);
+                    float* dst = partials + ((size_t)slot * 4 + quad) * kRowStride + base;
+                    if constexpr (E == 4) {
+                        *reinterpret_cast<float4*>(dst) = make_float4(P[0], P[1], P[2], P[3]);
+                    } else {
+                        dst[0] = P[0];
+                        dst[1] = P[1];
+                        dst[2] = P[2];
+                    }
                 }
-                if (lane == 0) row_flags[(size_t)slot * 4 + quad] = 1;
+                if (lane == 0) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
             }
             if (__any(tkey >= 0)) {
                 float tg[4 * CM];
@@ -1192,7 +1183,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 // ------------------------------------------------------------------------------------------
 // setup backward: sum partials per splat, chain to parameters
 // ------------------------------------------------------------------------------------------
-constexpr int kSetupBwdRows = 256 / kNP;  // 10 splats x 24 partial columns summed at once per 256-thread workgroup
+constexpr int kSetupBwdRows = 256 / kRowStride;  // 8 splats x 32 partial columns summed at once per 256-thread workgroup
 #ifndef GSTEX_SETUP_SPW
 #define GSTEX_SETUP_SPW 40
 #endif
@@ -1214,20 +1205,22 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     const uint32_t* __restrict__ row_flags, CamArgs cam_args, float* __restrict__ v_means,
     float* __restrict__ v_scales, float* __restrict__ v_quats, float* __restrict__ v_rgbs, float* __restrict__ v_opac,
     float* __restrict__ v_centers, float* __restrict__ v_uv0) {
-    // phase 1: kNP lanes per splat, lane c sums column c of the splat's flagged (slot, quadrant) rows in slot-major,
+    // phase 1: 32 lanes per splat, lane c sums column c of the splat's flagged (slot, quadrant) rows in slot-major,
     // quadrant-minor order (a splat's slots are contiguous, so its rows and flag words are too); phase 2: one
     // thread per splat chains the sums to the parameters
-    __shared__ float s_sum[kSetupBwdSplats][kNP];
+    __shared__ float s_sum[kSetupBwdSplats][kRowStride];
     const int t = threadIdx.x;
     const int g0 = blockIdx.x * kSetupBwdSplats;
-    if (t < kSetupBwdRows * kNP) {
-        const int c = t % kNP;
-        for (int j = t / kNP; j < kSetupBwdSplats; j += kSetupBwdRows) {
+    if (t < kSetupBwdRows * kRowStride) {
+        const int c = t % kRowStride;
+        // columns 24.. exist only in 32-value rows (flag 2: backward with depth / normal gradients)
+        const uint32_t need = c < kPartRow ? 0xFFu : 0x02u;
+        for (int j = t / kRowStride; j < kSetupBwdSplats; j += kSetupBwdRows) {
             float acc = 0.f;
             if (g0 + j < n) {
                 const int cnt = nth[g0 + j];
                 const size_t s0 = (size_t)offsets[g0 + j];
-                const float* src = partials + s0 * 4 * kNP + c;
+                const float* src = partials + s0 * 4 * kRowStride + c;
                 const uint32_t* fl = row_flags + s0;
                 // groups of kSetupBwdInflight slots: their flag words, then every flagged row of the group, are
                 // loaded before any is summed (most splats hit fewer tiles than one group holds)
@@ -1240,12 +1233,12 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
                     for (int u = 0; u < kSetupBwdInflight; ++u)
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
-                            r[4 * u + q] = (f[u] >> (8 * q)) & 1u ? src[((size_t)(e + u) * 4 + q) * kNP] : 0.f;
+                            r[4 * u + q] = (f[u] >> (8 * q)) & need ? src[((size_t)(e + u) * 4 + q) * kRowStride] : 0.f;
 #pragma unroll
                     for (int u = 0; u < kSetupBwdInflight; ++u)
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
-                            if ((f[u] >> (8 * q)) & 1u) acc += r[4 * u + q];
+                            if ((f[u] >> (8 * q)) & need) acc += r[4 * u + q];
                 }
             }
             s_sum[j][c] = acc;
@@ -1255,9 +1248,9 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     const int g = g0 + t;
     if (t >= kSetupBwdSplats || g >= n) return;
     const Camera cam = load_camera(cam_args);
-    float S[kNP];
+    float S[kPartRowGeo];
 #pragma unroll
-    for (int i = 0; i < kNP; ++i) S[i] = s_sum[t][i];
+    for (int i = 0; i < kPartRowGeo; ++i) S[i] = s_sum[t][i];
     const int cnt = nth[g];
     v_rgbs[3 * g + 0] = S[P_RGB + 0];
     v_rgbs[3 * g + 1] = S[P_RGB + 1];
@@ -1277,9 +1270,11 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     const float su = scales[3 * g] * glob, sv = scales[3 * g + 1] * glob;
     f3 mu = mk3(means[3 * g], means[3 * g + 1], means[3 * g + 2]);
     const Anchored an = splat_anchored(cam, mu, su, sv, fr);
-    HomogGrad hg = splat_anchored_vjp(cam, su, sv, fr, an.xn, an.yn, f3{S[P_TU], S[P_TU + 1], S[P_TU + 2]},
-                                      f3{S[P_TV], S[P_TV + 1], S[P_TV + 2]},
-                                      f3{S[P_TW], S[P_TW + 1], S[P_TW + 2]});
+    f3 dTu, dTv, dTw;
+    affine_homog_vjp(an.Tu, an.Tv, an.Tw, f3{S[P_A], S[P_A + 1], S[P_A + 2]}, f3{S[P_B], S[P_B + 1], S[P_B + 2]},
+                     f3{S[P_P0], S[P_P0 + 1], S[P_P0 + 2]}, dTu, dTv, dTw);
+    dTw = add3(dTw, f3{S[P_TW], S[P_TW + 1], S[P_TW + 2]});
+    HomogGrad hg = splat_anchored_vjp(cam, su, sv, fr, an.xn, an.yn, dTu, dTv, dTw);
     const f3 um = mk3(umap[3 * g], umap[3 * g + 1], umap[3 * g + 2]);
     const f3 vm = mk3(vmap[3 * g], vmap[3 * g + 1], vmap[3 * g + 2]);
     const float dauu = S[P_AUU], dauv = S[P_AUV], davu = S[P_AVU], davv = S[P_AVV];

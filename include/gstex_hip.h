@@ -43,7 +43,7 @@ extern "C" {
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
 /* Per-(tile, splat, quadrant) gradient partial row written by gstex_raster_bwd (floats). */
-#define GSTEX_PARTIAL_FLOATS 24
+#define GSTEX_PARTIAL_FLOATS 32
 
 /* settings bitfield (GStexModelConfig.settings, gstex.py:194-197) */
 #define GSTEX_SETTING_AA_BLUR (1 << 9)   /* 2DGS screen-space low-pass */

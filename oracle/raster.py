@@ -299,8 +299,12 @@ def _splat_table(inp: RasterInputs, dtype):
     sgn = torch.where(_dot3(tw, dirv) < 0, -1.0, 1.0).to(dtype).detach()
     um = inp.umap[:, 0, :].to(dtype).detach()
     vm = inp.vmap[:, 0, :].to(dtype).detach()
+    # affine form of the homography (gstex_common.h affine_homog): p = dx A + dy B + (0, 0, Pz)
+    A = torch.stack([Tw[:, 2] * Tv[:, 1], -(Tw[:, 2] * Tv[:, 0]), Tw[:, 1] * Tv[:, 0] - Tw[:, 0] * Tv[:, 1]], -1)
+    B = torch.stack([-(Tu[:, 1] * Tw[:, 2]), Tu[:, 0] * Tw[:, 2], Tu[:, 1] * Tw[:, 0] - Tu[:, 0] * Tw[:, 1]], -1)
+    Pz = Tu[:, 0] * Tv[:, 1] - Tu[:, 1] * Tv[:, 0]
     return dict(
-        Tu=Tu, Tv=Tv, Tw=Tw, xa=xa, ya=ya,
+        A=A, B=B, Pz=Pz, Tw=Tw, xa=xa, ya=ya,
         xy=inp.centers.to(dtype),
         opac=inp.opacities[:, 0].to(dtype),
         rgb=inp.rgbs.to(dtype),
@@ -379,18 +383,13 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         px = (torch.from_numpy(pxi.astype(np.float32)) + 0.5).to(dtype)[None, :]  # exact in fp32
         py = (torch.from_numpy(pyi.astype(np.float32)) + 0.5).to(dtype)[None, :]
         g = {k: v[ids] for k, v in tab.items() if k != "sgn"}
-        Tu, Tv, Tw = g["Tu"][:, None, :], g["Tv"][:, None, :], g["Tw"][:, None, :]
+        A, B, Tw = g["A"][:, None, :], g["B"][:, None, :], g["Tw"][:, None, :]
         ddx = px - g["xa"][:, None]
         ddy = py - g["ya"][:, None]
-        kx = ddx * Tw[..., 0] - Tu[..., 0]
-        ky = ddx * Tw[..., 1] - Tu[..., 1]
-        kz = ddx * Tw[..., 2]
-        lx_ = ddy * Tw[..., 0] - Tv[..., 0]
-        ly_ = ddy * Tw[..., 1] - Tv[..., 1]
-        lz = ddy * Tw[..., 2]
-        pxc = ky * lz - kz * ly_
-        pyc = kz * lx_ - kx * lz
-        pzc = kx * ly_ - ky * lx_
+        # p = k x l in the affine form of raster.hip eval_hit: dx A + dy B + (0, 0, Pz)
+        pxc = ddx * A[..., 0] + ddy * B[..., 0]
+        pyc = ddx * A[..., 1] + ddy * B[..., 1]
+        pzc = (g["Pz"][:, None] + ddx * A[..., 2]) + ddy * B[..., 2]
         if decisions is None:
             nz = pzc != 0
         else:
