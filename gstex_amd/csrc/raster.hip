@@ -5,18 +5,18 @@
 // comments of gstex_common.h; the CPU restatement is oracle/raster.py.
 //
 // MI355X layout:
-//   * one 256-thread workgroup (4 wave64, one 8x8 quadrant each) per 16x16 tile, launched in descending
-//     pair-count order (gstex_tile_order: LPT list scheduling over the 8 XCDs' workgroup slots);
-//   * splat records are 128-B AoS lines; the forward stages a batch of them in LDS as [field][splat] float4
-//     planes (conflict-free writes, broadcast reads), the backward reads each visited one into SGPRs;
-//   * forward early-out per wave (ballot) and per workgroup (__syncthreads_count); the forward hands its
-//     per-wave cull bits to the backward (visit_masks);
-//   * backward: reverse traversal, barrier-free between the 4 waves (an LDS ring of batch slots, the last
-//     wave to finish a batch combines and flushes it); per-splat gradient partials reduced across the wave
-//     with a reduce-scatter butterfly (permlane32/16 swaps + DPP), combined across the 4 waves in a fixed
-//     order and written with plain stores to a per-(tile, splat) row (bitwise reproducible, no float
-//     atomics); texel gradients staged per (tile, splat) as 32-bit fixed point in LDS (exact integer adds)
-//     and flushed once per batch with global fp32 atomics (only non-zero entries).
+//   * forward: one 256-thread workgroup (4 wave64, one 8x8 quadrant each) per 16x16 tile, launched in
+//     descending pair-count order (gstex_tile_order); splat records are 128-B lines staged per batch in LDS as
+//     [plane][splat] float4; each wave ballots the batch against its quadrant (exact ellipse-vs-rectangle
+//     test), walks the set bits, early-outs per lane and per workgroup; it records for the backward (aux):
+//     its cull bits, per-unit evaluation counts and per-pixel checkpoints at 256-position segment boundaries;
+//   * backward: one wave64 workgroup per unit = (tile, 8x8 quadrant, segment), launched costliest first, no
+//     barriers and no shared state between waves; a unit starts from the forward's checkpoint after its
+//     segment and walks back to front; per visit the 24 splat partials are reduced across the wave with a
+//     reduce-scatter butterfly (permlane32/16 swaps + DPP) and stored as the (pair, quadrant) row at the
+//     pair's emission slot (summed in fixed order by setup_bwd: bitwise reproducible, no float atomics);
+//     texel gradients go through a DPP segmented scan, int32 fixed-point LDS staging of the splat's block
+//     and a flush of its non-zero entries with global fp32 atomics.
 #include "gstex_common.h"
 #include "gstex_error.h"
 

@@ -107,7 +107,7 @@ int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float
                    size_t workspace_bytes, void* stream);
 
 /* Largest-first launch order of the tiles: tile_order[n_tiles] lists the tiles by descending
- * pair count (ties by tile index).  Pass it to gstex_raster_fwd / gstex_raster_bwd, whose
+ * pair count (ties by tile index).  Pass it to gstex_raster_fwd / gstex_texture_edit, whose
  * workgroups the hardware dispatches in launch order round-robin over the 8 XCDs; NULL there
  * means row-major order.  Scheduling only: outputs do not depend on it.  Above 16384 tiles the
  * order is row-major. */

@@ -40,6 +40,7 @@ def _check(name, case, outputs=None, min_depth=0):
     _report(f"{name} bwd norm-rel", norm_errs)
     _report(f"{name} bwd max-rel", errs)
     _report(f"{name} bwd fp32-oracle norm-rel", inh_n)
+    _report(f"{name} bwd fp32-oracle max-rel", inh)
     for k in DIFF:
         nb = max(GRAD_RTOL, COND_FACTOR * inh_n[k])
         assert norm_errs[k] <= nb, f"{name}: grad {k} norm-wise rel err {norm_errs[k]:.3e} > {nb:.3e}"
