@@ -38,7 +38,7 @@ constexpr int kThreads = kTilePixels;  // 256
 #define GSTEX_FAST_RCP 1  // v_rcp_f32 for backward divisions that feed no threshold decision
 #endif
 #ifndef GSTEX_FAST_EVAL
-#define GSTEX_FAST_EVAL 0  // 1: hardware v_exp_f32 / v_rcp_f32 in the pair evaluation
+#define GSTEX_FAST_EVAL 1  // hardware v_exp_f32 / v_rcp_f32 in the pair evaluation (0: expf sequence, IEEE division)
 #endif
 #ifndef GSTEX_STATS
 #define GSTEX_STATS 0  // diagnostic builds: count backward work (iterations, culled, active lanes)

@@ -6,8 +6,11 @@ nerfstudio/models/gstex.py:1059-1170.
 
 Parity unpinned w.r.t. the reference CUDA rasterizer (absent from /root/reference).
 
-Forward values are computed in fp32 with the same operation order as the kernels, so every
-threshold decision (alpha >= 1/255, T < 1e-4, z >= near, AA branch, texel cell) matches the GPU.
+Forward values are computed in fp32 with the same operation order as the kernels (correctly rounded
+division and sqrt), so the threshold decisions (alpha >= 1/255, T < 1e-4, z >= near, AA branch, texel
+cell) match the GPU except within a few ulps of a threshold: the kernels evaluate exp and the pair's
+1 / p.z with the hardware v_exp_f32 / v_rcp_f32, a few ulps from this restatement; each pixel's smallest
+decision margin is reported (aux["margin"]) so tests can tell such a flip from a defect.
 Gradients come from torch autograd of an fp64 re-evaluation that reuses those fp32 decisions —
 i.e. the exact-arithmetic gradient of the function the GPU evaluates.
 """
@@ -424,13 +427,15 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
             incl = valid & (kidx < first[None, :])
             # decision margins (test support): the relative distance of every threshold test the GPU repeats in
             # fp32 (alpha >= 1/255, z >= near, T (1 - alpha) < 1e-4, rho3 <= rho2) from its threshold, over the
-            # pairs the traversal reaches.  exp is the one fp32 op that is not correctly rounded on either side
-            # (the GPU's v_exp_f32 sequence vs the host's expf can differ by an ulp), so a pixel whose forward
-            # differs from the oracle's by a flipped decision has a margin of a few 1e-7
+            # pairs the traversal reaches.  The GPU evaluates exp and 1 / p.z with the hardware v_exp_f32 /
+            # v_rcp_f32 (raster.hip eval_hit), a few ulps from this restatement, so alpha can differ by ~5e-7
+            # relative and 1 - alpha by alpha / (1 - alpha) times that: the termination margin is measured in
+            # those units
             big = torch.full_like(alpha, float("inf"))
             m_a = (alpha - amin).abs() / amin
             m_z = (zz - near).abs() / near
-            m_t = torch.where(valid, (Tafter - tmin).abs() / tmin, big)
+            sens = torch.clamp(alpha / torch.clamp(1.0 - alpha, min=1e-6), min=1.0)
+            m_t = torch.where(valid, (Tafter - tmin).abs() / tmin / sens, big)
             m_u = (rho3 - rho2).abs() / torch.clamp(rho2, min=1e-30) if aa else big
             m_all = torch.minimum(torch.minimum(m_a, m_z), torch.minimum(m_t, m_u))
             margin = torch.where(nz & (kidx <= first[None, :]), m_all, big).min(0).values.float()

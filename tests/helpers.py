@@ -121,7 +121,7 @@ def gpu_run(case: Case, grads=True, seed=5, device="cuda", outputs=None):
     return res, gr
 
 
-FLIP_MARGIN = 2e-6  # relative distance from a threshold within which an fp32 decision may flip (exp ulp)
+FLIP_MARGIN = 1e-5  # relative distance from a threshold within which an fp32 decision may flip (exp/rcp ulps)
 FLIP_FRACTION = 1e-3  # at most this fraction of the pixels (and at least 4) may carry a flipped decision
 
 
