@@ -820,12 +820,12 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
 // gstex.py:198-201 sets both weights to 0), so every term they scale is dropped at compile time.  The
 // remaining arithmetic is unchanged (x + 0 * y = x), so both variants give the same values.
 
-// Texel-gradient fixed point: per wave, e = exponent of max |dL/dtex * tex_scale| over its 64 pixels (< 2^e).  A
-// pixel's contribution w b g to a staged entry is < 2^e (w, b <= 1), so one visit adds < 2^(e+6) to an entry.
-// Contributions are formed at scale 2^S, S = 25 - e; each run tail of the 8-lane row scan (< 2^(S+e+3) = 2^28)
-// is rounded to int32 (one v_cvt_rpi_i32_f32) and the tails are summed exactly in int32 (|sum| < 0.99 * 2^31).
-// Resolution: 2^-25 of the wave's largest upstream texel gradient.
-constexpr int kTexFixBits = 25;
+// Texel-gradient fixed point, per visit: the reduce also sums M = sum over the wave's pixels of |w tex_scale| x
+// max_c |dL/dtex[c]|, a bound on what the visit adds to any staged entry (bilinear weights <= 1).  Contributions
+// are formed at scale 2^S, S = 30 - e (M < 2^e); each run tail of the 8-lane row scan (< 2^30) is rounded to
+// int32 (one v_cvt_rpi_i32_f32) and the tails are summed exactly in int32 (|sum| <= 2^30 + rounding).
+// Resolution: 2^-30 of the visit's total.
+constexpr int kTexFixBits = 30;
 __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^S; round half up, one VALU op
     int q;
     asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(q) : "v"(y));
@@ -934,19 +934,9 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             T = Tk;
         }
     }
-    int tex_S;
-    {
-        float gm = 0.f;
+    float gabs = 0.f;  // max_c |dL/dtex[c]|: bounds this pixel's texel-gradient contributions (x w |tex_scale|)
 #pragma unroll
-        for (int c = 0; c < CM; ++c) gm = fmaxf(gm, fabsf(Gtex[c]));
-        gm *= fabsf(tex_scale);
-        const float gmax = __int_as_float(wave_max_i(__float_as_int(gm)));  // non-negative floats order as ints
-        int e = 0;
-        if (gmax > 0.f) (void)frexpf(gmax, &e);  // gmax < 2^e
-        tex_S = kTexFixBits - e;
-    }
-    // texel-gradient contributions are formed directly in the fixed-point scale
-    const float tex_scale_q = __builtin_ldexpf(tex_scale, tex_S);
+    for (int c = 0; c < CM; ++c) gabs = fmaxf(gabs, fabsf(Gtex[c]));
     for (int i = lane; i < kTexStage; i += 64) s_texq[i] = 0;
     const size_t vm_base = visit_mask_base(rng.x, tile);
 
@@ -973,6 +963,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
             constexpr int NP = GEO ? kPartRowGeo : kPartRow;
+            // a spare slot of the row (zero when stored): the texel fixed-point bound
+            constexpr int kMBound = GEO ? 27 : P_NRM;
             float P[NP];
 #pragma unroll
             for (int i = 0; i < NP; i += 2) {
@@ -1024,7 +1016,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 }
                 if (has_tex && !(GSTEX_ABLATE & 1)) {
                     tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
-                    tw = w * tex_scale_q;  // d value / d stored texel, x 2^tex_S (fixed-point staging)
+                    tw = w * tex_scale;  // d value / d stored texel
+                    P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
                     tax = b.ax;
                     tay = b.ay;
                 }
@@ -1090,6 +1083,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     P[P_TW + 2] = dz;
                 }
             }
+            float vis_M = 0.f;  // sum over the wave's pixels of |w tex_scale| max_c |dL/dtex[c]| for this splat
             if (__any(contrib)) {
                 if (GSTEX_ABLATE & 2) {
 #pragma unroll
@@ -1097,6 +1091,10 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 } else {
                     wave_reduce<NP>(P);
                 }
+                // take the bound out of the spare slot (kMBound) before the row is stored
+                constexpr int kML = GEO ? 48 : 56, kMI = GEO ? 3 : 0;  // its lane and index after the reduce-scatter
+                vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
+                if (lane == kML) P[kMI] = 0.0f;
                 // the (pair, quadrant) row: lanes 8k hold NP / 8 consecutive values each; the flag (1: 24-value
                 // row, 2: 32-value row) marks it written
                 const int slot = __builtin_amdgcn_readlane(my_slot, j);
@@ -1115,6 +1113,13 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if (lane == 0) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
             }
             if (__any(tkey >= 0)) {
+                // fixed point for this visit: every staged entry receives at most vis_M in value units (bilinear
+                // weights <= 1), so at scale 2^S, S = 30 - e (vis_M < 2^e), the tails (each < 2^30) and their int32
+                // sums stay in range; resolution 2^-30 of the visit's total
+                int e_m = 0;
+                if (vis_M > 0.f) (void)frexpf(vis_M, &e_m);
+                const int tex_S = kTexFixBits - e_m;
+                const float twq = tw * __builtin_ldexpf(1.0f, tex_S);
                 float tg[4 * CM];
                 {
 #pragma clang fp contract(fast)
@@ -1122,7 +1127,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     const float w10 = tax * (1.0f - tay), w11 = tax * tay;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) {
-                        const float gt = (c < Cn) ? tw * Gtex[c] : 0.0f;
+                        const float gt = (c < Cn) ? twq * Gtex[c] : 0.0f;
                         tg[c] = gt * w00;
                         tg[CM + c] = gt * w01;
                         tg[2 * CM + c] = gt * w10;
