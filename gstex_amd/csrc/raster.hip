@@ -94,11 +94,11 @@ struct BwdShape {
     static constexpr bool kTrain = (C == 3 && !GEO);
     static constexpr int kWaves = kTrain ? GSTEX_BWD_WAVES_TRAIN : GSTEX_BWD_WAVES;
 };
-// Backward per-wave texel staging: one splat's texel block (h * w * C int32 fixed-point entries) at a time, 6 KiB
-// per wave (24 waves per CU use 144 of the 160 KiB); a larger block adds its run tails straight to global memory.
-// (int64 staging at 2^-27 measured 0.15 ms slower at cfg3: ds_add_u64 moves twice the LDS data.)
+// Backward per-wave texel staging: one splat's texel block (h * w * C int32 fixed-point entries) at a time, 4 KiB
+// per wave (341 texels at C = 3; cfg3's largest block is 169); a larger block adds its run tails straight to global
+// memory.  Measured: 6 KiB staging 3 % slower than 4, 3 and 2 KiB (equal); int64 staging +0.15 ms.)
 #ifndef GSTEX_TEX_STAGE
-#define GSTEX_TEX_STAGE 1536
+#define GSTEX_TEX_STAGE 1024
 #endif
 constexpr int kTexStage = GSTEX_TEX_STAGE;
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;

@@ -11,9 +11,11 @@ if [ -d scratch/head ]; then
   (cd scratch/head && timeout -k 10 180 python3 -u tools/raster_loop.py --photometric --iters 20) > $OUT/loop_head.log 2>&1 || { echo "loop_head FAILED"; tail -5 $OUT/loop_head.log; exit 1; }
   echo "head: $(tail -1 $OUT/loop_head.log)"
 fi
+for rep in $(seq 1 ${REPEAT:-1}); do
 for v in $VARIANTS; do
-  GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 180 python3 -u tools/raster_loop.py --photometric --iters 20 > $OUT/loop_$v.log 2>&1 || { echo "loop_$v FAILED"; tail -5 $OUT/loop_$v.log; exit 1; }
+  GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 180 python3 -u tools/raster_loop.py --photometric --iters ${ITERS:-20} > $OUT/loop_$v.log 2>&1 || { echo "loop_$v FAILED"; tail -5 $OUT/loop_$v.log; exit 1; }
   echo "$v: $(tail -1 $OUT/loop_$v.log)"
+done
 done
 [ -n "$NOTESTS" ] && exit 0
 K=${1:-}
