@@ -83,6 +83,7 @@ SIGNATURES = {
     ),
     "gstex_raster_aux_bytes": (c_size_t, [c_int64, c_int32, c_int32]),
     "gstex_unit_order": (c_int32, [c_int32, _P, _P, _P, _P]),
+    "gstex_unit_order_scratch_words": (c_size_t, []),
     "gstex_raster_bwd": (
         c_int32,
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,

@@ -531,32 +531,65 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
     return launch_status("gstex_tile_order");
 }
 
-// Backward unit order (gstex_unit_order): a counting sort by descending cost, clamped to kUnitBuckets - 1 (the
-// forward's per-segment counts are <= 256): histogram (LDS per workgroup, one global atomic per bucket and
-// workgroup), exclusive scan of the buckets from the costliest down, scatter (each workgroup reserves one range
-// per bucket).  Order inside a bucket is unspecified -- scheduling only, outputs do not depend on it.
+// Backward unit order (gstex_unit_order).  Key = cost (bits 0-23) | XCD group (bits 24-26); units of cost 0 have no
+// work and get no position (order[] = -1 there).  Counting sort by descending cost (clamped to kUnitBuckets - 1)
+// within each group, then the groups interleaved: the k-th unit of group g goes to launch position 8 k + g, which
+// the hardware's round-robin dispatch places on XCD g (performance only: the map is not guaranteed), so the units
+// of one 2x2-tile macro-block share one XCD's L2 (texel blocks, records).  If the groups are too uneven for that
+// (8 max_g len_g > n_units), the order is the plain descending-cost one.  Order inside a bucket is unspecified --
+// scheduling only, outputs do not depend on it.
 constexpr int kUnitBuckets = 1024;
-constexpr int kUnitsPerBlock = 2048;
+constexpr int kUnitGroups = 8;
+constexpr int kUnitBins = kUnitBuckets * kUnitGroups;
+constexpr int kUnitsPerBlock = 4096;
+// scratch (int32): [0, 8192) histogram, [8192, 16384) group-interleaved starts, [16384, 24576) plain starts,
+// [24576] mode (1 = group-interleaved)
+constexpr int kUnitScratch = 3 * kUnitBins + 16;
 
-__device__ __forceinline__ int unit_bucket(int c) { return kUnitBuckets - 1 - min(max(c, 0), kUnitBuckets - 1); }
+__device__ __forceinline__ int unit_bin(int key) {
+    const int c = key & 0xFFFFFF, g = (key >> 24) & (kUnitGroups - 1);
+    return g * kUnitBuckets + (kUnitBuckets - 1 - min(c, kUnitBuckets - 1));
+}
 
-__global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __restrict__ cost,
+__global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __restrict__ key,
                                                         int32_t* __restrict__ hist) {
-    __shared__ int s_h[kUnitBuckets];
-    for (int i = threadIdx.x; i < kUnitBuckets; i += 256) s_h[i] = 0;
+    __shared__ int s_h[kUnitBins];
+    for (int i = threadIdx.x; i < kUnitBins; i += 256) s_h[i] = 0;
     __syncthreads();
     const int u0 = blockIdx.x * kUnitsPerBlock;
-    for (int u = u0 + threadIdx.x; u < min(n, u0 + kUnitsPerBlock); u += 256) atomicAdd(&s_h[unit_bucket(cost[u])], 1);
+    for (int u = u0 + threadIdx.x; u < min(n, u0 + kUnitsPerBlock); u += 256) {
+        const int k = key[u];
+        if (k & 0xFFFFFF) atomicAdd(&s_h[unit_bin(k)], 1);
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < kUnitBuckets; i += 256)
+    for (int i = threadIdx.x; i < kUnitBins; i += 256)
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
-__global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int32_t* __restrict__ hist) {
-    // in place: hist[b] -> number of units in buckets < b (bucket 0 = the costliest)
+__global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int n, int32_t* __restrict__ ws) {
+    // per group: exclusive scan of its buckets (costliest first) -> the group-interleaved starts; across groups
+    // (bucket-major, group-minor) -> the plain starts
     __shared__ int s[kUnitBuckets];
+    __shared__ int s_len[kUnitGroups];
     const int t = threadIdx.x;
-    s[t] = hist[t];
+    const int32_t* hist = ws;
+    int tot = 0;  // units in bucket t over all groups
+    for (int g = 0; g < kUnitGroups; ++g) {
+        const int h = hist[g * kUnitBuckets + t];
+        tot += h;
+        s[t] = h;
+        __syncthreads();
+        for (int o = 1; o < kUnitBuckets; o <<= 1) {
+            const int v = t >= o ? s[t - o] : 0;
+            __syncthreads();
+            s[t] += v;
+            __syncthreads();
+        }
+        ws[kUnitBins + g * kUnitBuckets + t] = s[t] - h;
+        if (t == kUnitBuckets - 1) s_len[g] = s[t];
+        __syncthreads();
+    }
+    s[t] = tot;
     __syncthreads();
     for (int o = 1; o < kUnitBuckets; o <<= 1) {
         const int v = t >= o ? s[t - o] : 0;
@@ -564,35 +597,58 @@ __global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int32_t* __rest
         s[t] += v;
         __syncthreads();
     }
-    hist[t] = s[t] - hist[t];
+    int run = s[t] - tot;
+    for (int g = 0; g < kUnitGroups; ++g) {
+        ws[2 * kUnitBins + g * kUnitBuckets + t] = run;
+        run += hist[g * kUnitBuckets + t];
+    }
+    if (t == 0) {
+        int mx = 0;
+        for (int g = 0; g < kUnitGroups; ++g) mx = max(mx, s_len[g]);
+        ws[3 * kUnitBins] = (long long)kUnitGroups * mx <= (long long)n ? 1 : 0;
+    }
 }
 
-__global__ __launch_bounds__(256) void unit_scatter_kernel(int n, const int32_t* __restrict__ cost,
-                                                           int32_t* __restrict__ next, int32_t* __restrict__ order) {
-    __shared__ int s_h[kUnitBuckets];
-    for (int i = threadIdx.x; i < kUnitBuckets; i += 256) s_h[i] = 0;
+__global__ __launch_bounds__(256) void unit_scatter_kernel(int n, const int32_t* __restrict__ key,
+                                                           int32_t* __restrict__ ws, int32_t* __restrict__ order) {
+    __shared__ int s_h[kUnitBins];
+    const bool grouped = ws[3 * kUnitBins] != 0;
+    int32_t* next = ws + (grouped ? kUnitBins : 2 * kUnitBins);
+    for (int i = threadIdx.x; i < kUnitBins; i += 256) s_h[i] = 0;
     __syncthreads();
     const int u0 = blockIdx.x * kUnitsPerBlock;
     const int u1 = min(n, u0 + kUnitsPerBlock);
-    for (int u = u0 + threadIdx.x; u < u1; u += 256) atomicAdd(&s_h[unit_bucket(cost[u])], 1);
+    for (int u = u0 + threadIdx.x; u < u1; u += 256) {
+        const int k = key[u];
+        if (k & 0xFFFFFF) atomicAdd(&s_h[unit_bin(k)], 1);
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < kUnitBuckets; i += 256)
-        if (s_h[i]) s_h[i] = atomicAdd(&next[i], s_h[i]);  // this workgroup's range start in bucket i
+    for (int i = threadIdx.x; i < kUnitBins; i += 256)
+        if (s_h[i]) s_h[i] = atomicAdd(&next[i], s_h[i]);  // this workgroup's range start in bin i
     __syncthreads();
-    for (int u = u0 + threadIdx.x; u < u1; u += 256) order[atomicAdd(&s_h[unit_bucket(cost[u])], 1)] = u;
+    for (int u = u0 + threadIdx.x; u < u1; u += 256) {
+        const int k = key[u];
+        if (!(k & 0xFFFFFF)) continue;
+        const int b = unit_bin(k);
+        const int r = atomicAdd(&s_h[b], 1);
+        order[grouped ? kUnitGroups * r + b / kUnitBuckets : r] = u;
+    }
 }
 
-extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, int32_t* scratch,
+extern "C" size_t gstex_unit_order_scratch_words(void) { return kUnitScratch; }
+
+extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_key, int32_t* unit_order, int32_t* scratch,
                                 void* stream) {
     GSTEX_REQUIRE(n_units >= 0, "gstex_unit_order: invalid n_units %d", n_units);
     if (n_units == 0) return GSTEX_OK;
-    GSTEX_REQUIRE(unit_cost && unit_order && scratch, "gstex_unit_order: null pointer");
+    GSTEX_REQUIRE(unit_key && unit_order && scratch, "gstex_unit_order: null pointer");
     hipStream_t st = as_stream(stream);
-    if (hipMemsetAsync(scratch, 0, kUnitBuckets * sizeof(int32_t), st) != hipSuccess)
+    if (hipMemsetAsync(scratch, 0, kUnitBins * sizeof(int32_t), st) != hipSuccess ||
+        hipMemsetAsync(unit_order, 0xFF, (size_t)n_units * sizeof(int32_t), st) != hipSuccess)
         return launch_status("gstex_unit_order");
     const int nb = div_up(n_units, kUnitsPerBlock);
-    unit_hist_kernel<<<nb, 256, 0, st>>>(n_units, unit_cost, scratch);
-    unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(scratch);
-    unit_scatter_kernel<<<nb, 256, 0, st>>>(n_units, unit_cost, scratch, unit_order);
+    unit_hist_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch);
+    unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(n_units, scratch);
+    unit_scatter_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch, unit_order);
     return launch_status("gstex_unit_order");
 }

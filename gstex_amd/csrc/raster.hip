@@ -77,6 +77,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_CONIC_CULL
 #define GSTEX_CONIC_CULL 1  // per-wave ellipse-vs-rectangle cull on top of the contribution box
 #endif
+#ifndef GSTEX_XCD_GROUPS
+#define GSTEX_XCD_GROUPS 1  // backward units of one 2x2-tile macro-block dispatched to one XCD (unit_order groups)
+#endif
 #ifndef GSTEX_REC_SGPR
 #define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
 #endif
@@ -261,9 +264,9 @@ __host__ __device__ __forceinline__ int ck_fields(int C) { return 4 + C + 6; }  
 
 struct AuxPtrs {
     unsigned long long* masks;
-    int32_t* cost;       // [n_units]
+    int32_t* cost;       // [n_units] evaluation count | XCD group (2x2-tile macro-block) << 24
     int32_t* order;      // [n_units] (written by the backward)
-    int32_t* order_ws;   // [1024] gstex_unit_order scratch
+    int32_t* order_ws;   // gstex_unit_order scratch
     int32_t* slot_tile;  // [n_slots]
     float* ckpt;         // [n_units][F][64]
     int F;
@@ -279,7 +282,7 @@ __host__ inline AuxLayout aux_layout(int64_t n_isect, int n_tiles, int C) {
     a.masks = o; o = al(o + (((size_t)n_isect + 63) / 64 + (size_t)n_tiles + 1) * 4 * sizeof(uint64_t));
     a.cost = o; o = al(o + (size_t)a.n_units * 4);
     a.order = o; o = al(o + (size_t)a.n_units * 4);
-    a.order_ws = o; o = al(o + 1024 * 4);
+    a.order_ws = o; o = al(o + gstex_unit_order_scratch_words() * 4);
     a.slot_tile = o; o = al(o + (size_t)a.n_slots * 4);
     a.ckpt = o; o = al(o + (size_t)a.n_units * a.F * 64 * sizeof(float));
     a.bytes = o;
@@ -531,6 +534,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
     const size_t vm_base = visit_mask_base(rng.x, tile);
     const int sbase = seg_base(rng.x, tile);
     int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
+    const int xgroup = GSTEX_XCD_GROUPS ? (((tx >> 1) + (ty >> 1) * ((tiles_x + 1) >> 1)) & 7) << 24 : 0;  // XCD group
     if (aux.slot_tile)
         for (int k = tid; k * kSegLen < rng.y - rng.x; k += kThreads) aux.slot_tile[sbase + k] = tile;
     // one checkpoint record: field f of the wave's lane at ckpt[((slot * 4 + wave) * F + f) * 64 + lane]
@@ -558,7 +562,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
         if (aux.cost && b0 > rng.x && (b0 - rng.x) % kSegLen == 0) {
             // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
             const int cnt = wave_max_i(seg_visits);  // lanes leave the visit loop as they finish: the wave's count
-            if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt;
+            if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt ? (cnt | xgroup) : 0;
             if (__any(!done)) write_ck(sbase + cur_seg);
             seg_visits = 0;
             ++cur_seg;
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
     }
     if (aux.cost) {
         const int cnt = wave_max_i(seg_visits);
-        if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt;
+        if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt ? (cnt | xgroup) : 0;
         // final accumulators for the backward's earlier segments, in the slot of the wave's last segment
         const int wl = wave_max_i(last);
         if (wl >= kSegLen) write_ck(sbase + wl / kSegLen);
@@ -849,7 +853,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 
     // unit = 4 slot + quadrant (see AuxPtrs), launched costliest first; a unit the forward never evaluated in is empty
     const int unit = aux.order[blockIdx.x];
-    if (aux.cost[unit] == 0) return;
+    if (unit < 0) return;  // a launch position no unit was placed at (empty units take none)
     const int quad = unit & 3, slot = unit >> 2;
     const int tile = aux.slot_tile[slot];
     const int tx = tile % tiles_x, ty = tile / tiles_x;

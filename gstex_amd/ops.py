@@ -290,11 +290,11 @@ def tile_order(tile_ranges: torch.Tensor) -> torch.Tensor:
 
 
 def unit_order(unit_cost: torch.Tensor) -> torch.Tensor:
-    """gstex_unit_order: int32 unit indices by descending cost (the backward's launch order, computed inside
-    gstex_raster_bwd; exposed for tests)."""
+    """gstex_unit_order: the backward's launch order from unit keys (cost | XCD group << 24), computed inside
+    gstex_raster_bwd; exposed for tests.  -1 at positions no unit takes."""
     uc = _i32(unit_cost, "unit_cost", (None,))
     order = torch.empty_like(uc)
-    scratch = torch.empty((1024,), device=uc.device, dtype=torch.int32)
+    scratch = torch.empty((int(_lib.load().gstex_unit_order_scratch_words()),), device=uc.device, dtype=torch.int32)
     call("gstex_unit_order", uc.shape[0], ptr(uc), ptr(order), ptr(scratch), _stream(uc))
     return order
 

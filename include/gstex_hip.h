@@ -141,11 +141,15 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
                      void* stream);
 size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels);
-/* Launch order of n_units backward units by descending unit_cost (costs clamped to 1023; order within equal
- * costs unspecified), scratch = 1024 int32 of device workspace.  gstex_raster_bwd calls it on its aux;
- * exported for tests. */
-int gstex_unit_order(int32_t n_units, const int32_t* unit_cost, int32_t* unit_order, int32_t* scratch,
+/* Launch order of n_units backward units: unit_key = cost (bits 0-23, clamped to 1023) | XCD group (bits 24-26).
+ * Units of cost 0 get no position; the others are sorted by descending cost within their group and the groups
+ * interleaved (k-th unit of group g at position 8 k + g: round-robin dispatch puts it on XCD g), or, when the
+ * groups are too uneven (8 x the largest group > n_units), sorted by descending cost overall.  unit_order[n_units]
+ * holds -1 at unused positions; order within equal costs is unspecified.  scratch =
+ * gstex_unit_order_scratch_words() int32 of device workspace.  gstex_raster_bwd calls it on its aux. */
+int gstex_unit_order(int32_t n_units, const int32_t* unit_key, int32_t* unit_order, int32_t* scratch,
                      void* stream);
+size_t gstex_unit_order_scratch_words(void);
 /* Backward composite. Needs the forward state and the forward's aux (required; the backward also writes its
  * launch order into it).  Any of v_img ... v_normal may be NULL (that output's gradient is zero).  Texel blocks
  * that run past n_texels (corrupt texture_dims) are neither read nor written.  One wave per backward unit (tile,

@@ -80,14 +80,14 @@ def test_raster_rejects_bad_channels_and_settings(lib):
 
 def test_raster_aux_bytes(lib):
     # cull-bit words (ceil(I / 64) + n_tiles + 1) * 4 x 8 B, then per backward unit (4 per slot; ceil(I / 256) +
-    # n_tiles + 1 slots) cost + order (4 B each), the order's 1024-bucket scratch, slot tiles
+    # n_tiles + 1 slots) cost + order (4 B each), the order's scratch, slot tiles
     # (4 B per slot) and a checkpoint of (4 + C + 6) fields x 64 lanes per unit, each array 256-B aligned
     def al(x):
         return (x + 255) // 256 * 256
 
     for n_isect, n_tiles, c in [(0, 1, 3), (1_915_389, 2500, 3), (12345, 77, 6)]:
         slots = (n_isect + 255) // 256 + n_tiles + 1
-        expect = (al(((n_isect + 63) // 64 + n_tiles + 1) * 32) + 2 * al(slots * 16) + al(1024 * 4) + al(slots * 4)
+        expect = (al(((n_isect + 63) // 64 + n_tiles + 1) * 32) + 2 * al(slots * 16) + al(lib.gstex_unit_order_scratch_words() * 4) + al(slots * 4)
                   + al(slots * 4 * (4 + c + 6) * 64 * 4))
         assert lib.gstex_raster_aux_bytes(n_isect, n_tiles, c) == expect
     assert lib.gstex_raster_aux_bytes(-1, 1, 3) == 0 and lib.gstex_raster_aux_bytes(1, 1, 9) == 0

@@ -217,17 +217,32 @@ def test_tile_order_is_largest_first(n_tiles):
     assert np.array_equal(got, expect)
 
 
-@pytest.mark.parametrize("n_units", [1, 10000, 65537, 200003])
-def test_unit_order_is_costliest_first(n_units):
+@pytest.mark.parametrize("n_units,groups", [(1, 1), (10000, 8), (200003, 8), (40000, 1)])
+def test_unit_order(n_units, groups):
+    """gstex_unit_order: units of cost 0 take no position; the others by descending cost inside their XCD group,
+    the k-th of group g at position 8 k + g -- or, with groups too uneven (a single group here), by descending cost
+    overall."""
     from gstex_amd.ops import unit_order
 
     g = np.random.default_rng(n_units)
-    cost = g.integers(0, 300, n_units).astype(np.int32)
+    cost = g.integers(0, 300, n_units).astype(np.int64)
     cost[g.integers(0, n_units, max(1, n_units // 50))] = 1 << 17  # beyond the 1023 clamp
-    got = unit_order(torch.from_numpy(cost).to(DEV)).cpu().numpy()
-    assert np.array_equal(np.sort(got), np.arange(n_units)), "not a permutation"
-    c = np.minimum(cost, 1023)[got]
-    assert np.all(np.diff(c) <= 0), "not in descending cost order"
+    grp = g.integers(0, groups, n_units)
+    key = (cost | (grp << 24)).astype(np.int32)
+    got = unit_order(torch.from_numpy(key).to(DEV)).cpu().numpy()
+    placed = got[got >= 0]
+    assert np.array_equal(np.sort(placed), np.nonzero(cost > 0)[0]), "every non-empty unit exactly once"
+    c = np.minimum(cost, 1023)
+    counts = np.bincount(grp[cost > 0], minlength=8)
+    if 8 * counts.max() <= n_units:
+        pos = np.nonzero(got >= 0)[0]
+        assert np.all(grp[got[pos]] == pos % 8), "unit not at a position of its group"
+        for r in range(8):
+            seq = got[r::8]
+            seq = seq[seq >= 0]
+            assert np.all(np.diff(c[seq]) <= 0)
+    else:
+        assert np.all(got[:len(placed)] >= 0) and np.all(np.diff(c[placed]) <= 0)
 
 
 def test_outputs_independent_of_launch_order(monkeypatch):
