@@ -77,6 +77,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_CONIC_CULL
 #define GSTEX_CONIC_CULL 1  // per-wave ellipse-vs-rectangle cull on top of the contribution box
 #endif
+#ifndef GSTEX_XCD_MB
+#define GSTEX_XCD_MB 2
+#endif
 #ifndef GSTEX_XCD_GROUPS
 #define GSTEX_XCD_GROUPS 1  // backward units of one 2x2-tile macro-block dispatched to one XCD (unit_order groups)
 #endif
@@ -534,7 +537,9 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
     const size_t vm_base = visit_mask_base(rng.x, tile);
     const int sbase = seg_base(rng.x, tile);
     int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
-    const int xgroup = GSTEX_XCD_GROUPS ? (((tx >> 1) + (ty >> 1) * ((tiles_x + 1) >> 1)) & 7) << 24 : 0;  // XCD group
+    // XCD group of the tile's backward units: its GSTEX_XCD_MB x GSTEX_XCD_MB-tile macro-block
+    const int xgroup = GSTEX_XCD_GROUPS
+        ? (((tx / GSTEX_XCD_MB) + (ty / GSTEX_XCD_MB) * ((tiles_x + GSTEX_XCD_MB - 1) / GSTEX_XCD_MB)) & 7) << 24 : 0;
     if (aux.slot_tile)
         for (int k = tid; k * kSegLen < rng.y - rng.x; k += kThreads) aux.slot_tile[sbase + k] = tile;
     // one checkpoint record: field f of the wave's lane at ckpt[((slot * 4 + wave) * F + f) * 64 + lane]
