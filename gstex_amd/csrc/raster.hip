@@ -32,7 +32,9 @@ constexpr int kThreads = kTilePixels;  // 256
 #define GSTEX_WAVE_8X8 1  // each wave covers an 8x8 quadrant of the tile (0: 16x4 rows)
 #endif
 #ifndef GSTEX_SEG_W
-#define GSTEX_SEG_W (GSTEX_WAVE_8X8 ? 8 : 16)  // texel-gradient segment width in lanes = one pixel row
+// texel-gradient segment width in lanes: half a pixel row (8x8 waves; 2 scan steps, twice the run tails of a
+// whole row: measured 4% faster backward than 8, 2 is slower again)
+#define GSTEX_SEG_W (GSTEX_WAVE_8X8 ? 4 : 16)
 #endif
 #ifndef GSTEX_FAST_RCP
 #define GSTEX_FAST_RCP 1  // v_rcp_f32 for backward divisions that feed no threshold decision
@@ -87,10 +89,11 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
 #endif
 // Backward occupancy: waves per SIMD the register allocation targets, per instantiation.  The photometric
-// training variant (C = 3, no geometry gradients) fits 5 waves (96 VGPRs, a few scratch spills; 5 workgroups
-// per CU need <= 32 KiB of LDS each, so its texel staging is smaller); the others keep 4.
+// training variant (C = 3, no geometry gradients) fits 7 (72 VGPRs, no spills; 8 forces 64 VGPRs with scratch
+// spills and is 3 % slower); the others 5.  Measured: warming the next visit's record line with a scalar load
+// during the current visit gains nothing (records hit in cache).
 #ifndef GSTEX_BWD_WAVES_TRAIN
-#define GSTEX_BWD_WAVES_TRAIN 6
+#define GSTEX_BWD_WAVES_TRAIN 7
 #endif
 #ifndef GSTEX_BWD_WAVES
 #define GSTEX_BWD_WAVES 5
@@ -835,6 +838,11 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
 // int32 (one v_cvt_rpi_i32_f32) and the tails are summed exactly in int32 (|sum| <= 2^30 + rounding).
 // Resolution: 2^-30 of the visit's total.
 constexpr int kTexFixBits = 30;
+#ifndef GSTEX_FLUSH_U
+#define GSTEX_FLUSH_U 4
+#endif
+constexpr int kFlushU = GSTEX_FLUSH_U;  // staging entries per lane per flush pass
+static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging area");
 __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^S; round half up, one VALU op
     int q;
     asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(q) : "v"(y));
@@ -914,6 +922,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     const int seg = slot - sbase, lo = seg * kSegLen;
     if (wave_last < lo) return;
     const int hi = min(lo + kSegLen - 1, wave_last), kf = wave_last / kSegLen;
+    GSTEX_STAT(0, 1);
     const float Af = 1.0f - T;
     float R = (Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2;
     float Gtex_bias = 0.f;  // tex_bias * sum_c dL/dtex[c]: the bias part of sum_c dL/dtex[c] * texel value
@@ -971,6 +980,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
+            GSTEX_STAT(1, 1);
+            GSTEX_STAT(3, __popcll(__ballot(contrib)));
             constexpr int NP = GEO ? kPartRowGeo : kPartRow;
             // a spare slot of the row (zero when stored): the texel fixed-point bound
             constexpr int kMBound = GEO ? 27 : P_NRM;
@@ -1094,6 +1105,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             }
             float vis_M = 0.f;  // sum over the wave's pixels of |w tex_scale| max_c |dL/dtex[c]| for this splat
             if (__any(contrib)) {
+                GSTEX_STAT(2, 1);
                 if (GSTEX_ABLATE & 2) {
 #pragma unroll
                     for (int i = 3; i < NP; ++i) asm volatile("" ::"v"(P[i]));
@@ -1143,9 +1155,11 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                         tg[3 * CM + c] = gt * w11;
                     }
                 }
-                const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
+                const bool tail = (GSTEX_ABLATE & 128) ? tkey >= 0 : seg_reduce_rows<4 * CM>(tkey, tg);
                 const int bsize = r.h * r.w * Cn;  // wave-uniform
                 const bool staged = bsize <= kTexStage;
+                GSTEX_STAT(5, __popcll(__ballot(tail)));
+                GSTEX_STAT(7, 1);
                 if (GSTEX_ABLATE & 16) {
 #pragma unroll
                     for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
@@ -1178,15 +1192,24 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                         }
                     }
                 }
-                if (staged) {
+                if (staged && !(GSTEX_ABLATE & 64)) {
                     // flush the block (non-zero entries only) and leave the staging area zeroed; the wave's LDS
                     // operations complete in order, so these reads see every tail added above
                     float* dst = v_texture + (size_t)r.off * Cn;
-                    for (int e = lane; e < bsize; e += 64) {
-                        const int v = s_texq[e];
-                        if (v == 0) continue;
-                        s_texq[e] = 0;
-                        if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e, __builtin_ldexpf((float)v, -tex_S));
+                    // kFlushU entries per lane per pass, their LDS reads issued together (one wait per pass); entries
+                    // past the block are zero (the staging area is kept zeroed) and kTexStage is a multiple of the pass
+                    for (int e0 = lane; e0 < bsize; e0 += 64 * kFlushU) {
+                        int v[kFlushU];
+                        GSTEX_STAT(4, 1);
+#pragma unroll
+                        for (int k = 0; k < kFlushU; ++k) v[k] = s_texq[e0 + 64 * k];
+#pragma unroll
+                        for (int k = 0; k < kFlushU; ++k) {
+                            GSTEX_STAT(6, __popcll(__ballot(v[k] != 0)));
+                            if (v[k] == 0) continue;
+                            s_texq[e0 + 64 * k] = 0;
+                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, __builtin_ldexpf((float)v[k], -tex_S));
+                        }
                     }
                 }
             }

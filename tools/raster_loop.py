@@ -73,7 +73,7 @@ def main():
         buf = (ctypes.c_ulonglong * 8)()
         lib.gstex_debug_stats(buf)
         n = args.iters + 1
-        names = ["batch_splats", "visits", "visits_any", "contrib_lanes", "global_tex", "tails", "distinct", "tail_visits"]
+        names = ["units", "visits", "visits_any", "contrib_lanes", "flush_passes", "tail_lanes", "flushed_entries", "tex_visits"]
         if os.environ.get("GSTEX_STATS_PHASES"):  # GSTEX_STATS=2: wave-clock sums per backward phase
             names = ["load+barrier", "place+cull", "visits", "barrier_pre_combine", "combine+flush", "barrier_end",
                      "prologue", "-"]
