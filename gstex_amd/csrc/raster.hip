@@ -701,6 +701,9 @@ __device__ __forceinline__ float dpp_f(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+#ifndef GSTEX_DPP_ASM
+#define GSTEX_DPP_ASM 1
+#endif
 template <int NV>
 __device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
     static_assert(NV % 8 == 0, "reduce-scatter over 8 lane groups");
@@ -717,6 +720,53 @@ __device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
     for (int i = 0; i < Q; ++i) {
         const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + Q]), false, false);
         v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    if (GSTEX_DPP_ASM && (E == 3 || E == 4)) {
+        // the last four stages as single v_add_f32_dpp instructions (the compiler emits a DPP move plus an add):
+        // row_ror:8 (lane ^ 8 inside a 16-lane row), quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror (the other
+        // quad of the 8-lane group).  dpp(x) + y rounds as y + dpp(x).  The leading s_nop covers the VALU-write ->
+        // DPP-read hazard for the inputs (the asm is opaque to the hazard recognizer); inside, each value is DPP-read
+        // again only after the other E - 1 >= 2 values' writes; the trailing s_nop covers a following DPP read.
+        const bool hi = lane & 8;
+        float keep[4], send[4];
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            send[i] = hi ? v[i] : v[i + E];
+            keep[i] = hi ? v[i + E] : v[i];
+        }
+#define GSTEX_DPP_ADD(CTRL, D, S) "v_add_f32_dpp %" #D ", %" #S ", %" #D " " CTRL " row_mask:0xf bank_mask:0xf\n"
+#define GSTEX_DPP_SELF(CTRL, D) "v_add_f32_dpp %" #D ", %" #D ", %" #D " " CTRL " row_mask:0xf bank_mask:0xf\n"
+        if constexpr (E == 3) {
+            asm volatile("s_nop 1\n"
+                         GSTEX_DPP_ADD("row_ror:8", 0, 3) GSTEX_DPP_ADD("row_ror:8", 1, 4) GSTEX_DPP_ADD("row_ror:8", 2, 5)
+                         GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 0) GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 1)
+                         GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 2)
+                         GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 0) GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 1)
+                         GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 2)
+                         GSTEX_DPP_SELF("row_half_mirror", 0) GSTEX_DPP_SELF("row_half_mirror", 1)
+                         GSTEX_DPP_SELF("row_half_mirror", 2)
+                         "s_nop 1"
+                         : "+v"(keep[0]), "+v"(keep[1]), "+v"(keep[2])
+                         : "v"(send[0]), "v"(send[1]), "v"(send[2]));
+        } else {
+            asm volatile("s_nop 1\n"
+                         GSTEX_DPP_ADD("row_ror:8", 0, 4) GSTEX_DPP_ADD("row_ror:8", 1, 5) GSTEX_DPP_ADD("row_ror:8", 2, 6)
+                         GSTEX_DPP_ADD("row_ror:8", 3, 7)
+                         GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 0) GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 1)
+                         GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 2) GSTEX_DPP_SELF("quad_perm:[1,0,3,2]", 3)
+                         GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 0) GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 1)
+                         GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 2) GSTEX_DPP_SELF("quad_perm:[2,3,0,1]", 3)
+                         GSTEX_DPP_SELF("row_half_mirror", 0) GSTEX_DPP_SELF("row_half_mirror", 1)
+                         GSTEX_DPP_SELF("row_half_mirror", 2) GSTEX_DPP_SELF("row_half_mirror", 3)
+                         "s_nop 1"
+                         : "+v"(keep[0]), "+v"(keep[1]), "+v"(keep[2]), "+v"(keep[3])
+                         : "v"(send[0]), "v"(send[1]), "v"(send[2]), "v"(send[3]));
+        }
+#undef GSTEX_DPP_ADD
+#undef GSTEX_DPP_SELF
+#pragma unroll
+        for (int i = 0; i < E; ++i) v[i] = keep[i];
+        return;
     }
     {
         const bool hi = lane & 8;
@@ -797,8 +847,50 @@ __device__ __forceinline__ void seg_step(int seg, float (&v)[NV]) {
 // Segments = maximal runs of equal key inside a 16-lane row (a lane whose key differs from its left
 // neighbour starts a segment, so a non-contributing lane splits a run instead of being bridged).
 // Returns true for the last lane of a segment with key >= 0; it then holds the segment's sums.
+// 1.0f in the lanes whose bit of the wave mask m is set, else 0 (one v_cndmask with the mask as lane select)
+__device__ __forceinline__ float mask_one(unsigned long long m) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, 0, 1.0, %1" : "=v"(r) : "s"(m));
+    return r;
+}
+#ifndef GSTEX_SEG_MASK
+#define GSTEX_SEG_MASK 1
+#endif
+// Mask form (GSTEX_SEG_MASK): the segment heads as one wave mask H (ballot of key changes, plus every group's first
+// lane); lane l joins lane l - OFF iff no head lies in (l - OFF, l], i.e. bit l of ~(H | H << 1 | ... | H << (OFF-1)),
+// computed on the scalar unit; the run tails are the lanes before a head or at a group's end.
+template <int NV>
+__device__ __forceinline__ bool seg_reduce_rows_mask(int key, float (&v)[NV]) {
+    constexpr int SW = GSTEX_SEG_W;
+    static_assert(SW == 2 || SW == 4 || SW == 8 || SW == 16, "segment width");
+    constexpr unsigned long long kFirst = SW == 2 ? 0x5555555555555555ull : SW == 4 ? 0x1111111111111111ull
+                                        : SW == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
+    constexpr unsigned long long kLast = kFirst << (SW - 1);
+    const int left = dpp_bc_i<0x111>(key);  // row_shr:1 (lanes at a group start are heads regardless)
+    const unsigned long long H = __ballot(left != key) | kFirst;
+    const unsigned long long live = __ballot(key >= 0);
+    unsigned long long cover = H;  // heads in (l - off, l] for the current off
+#pragma unroll
+    for (int off = 1; off < SW; off <<= 1) {
+        const float mf = mask_one(~cover);
+        asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            if (off == 1) fmac_dpp_shr<1>(v[i], mf);
+            else if (off == 2) fmac_dpp_shr<2>(v[i], mf);
+            else if (off == 4) fmac_dpp_shr<4>(v[i], mf);
+            else fmac_dpp_shr<8>(v[i], mf);
+        }
+        asm volatile("s_nop 1" ::: "memory");
+        cover = cover | (cover << off);
+    }
+    const unsigned long long tails = ((H >> 1) | kLast) & live;
+    return mask_one(tails) != 0.0f;
+}
+
 template <int NV>
 __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
+    if (GSTEX_SEG_MASK) return seg_reduce_rows_mask<NV>(key, v);
     constexpr int SW = GSTEX_SEG_W;
     const int pos = threadIdx.x & (SW - 1);
     const int left = dpp_bc_i<0x111>(key);  // unused at pos 0 (a forced head)
@@ -837,17 +929,27 @@ __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
 // are formed at scale 2^S, S = 30 - e (M < 2^e); each run tail of the 8-lane row scan (< 2^30) is rounded to
 // int32 (one v_cvt_rpi_i32_f32) and the tails are summed exactly in int32 (|sum| <= 2^30 + rounding).
 // Resolution: 2^-30 of the visit's total.
-constexpr int kTexFixBits = 30;
-#ifndef GSTEX_FLUSH_U
-#define GSTEX_FLUSH_U 4
-#endif
-constexpr int kFlushU = GSTEX_FLUSH_U;  // staging entries per lane per flush pass
-static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging area");
 __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^S; round half up, one VALU op
     int q;
     asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(q) : "v"(y));
     return q;
 }
+constexpr int kTexFixBits = 30;
+#ifndef GSTEX_TEX_FIXED
+#define GSTEX_TEX_FIXED 1
+#endif
+// 1: run tails staged as int32 fixed point at the per-visit scale; 0: staged as fp32 (ds_add_f32; the wave's LDS
+// atomics apply in program order, so the staged sums are deterministic either way).  Measured: fp32 LDS atomics
+// make the backward 2x slower (3.2 vs 1.57 ms) although they save the conversions.
+constexpr bool kTexFixed = GSTEX_TEX_FIXED;
+using TexQ = std::conditional_t<kTexFixed, int, float>;
+__device__ __forceinline__ void stage_add(int* a, float y) { atomicAdd(a, fixed_round(y)); }
+__device__ __forceinline__ void stage_add(float* a, float y) { atomicAdd(a, y); }
+#ifndef GSTEX_FLUSH_U
+#define GSTEX_FLUSH_U 4
+#endif
+constexpr int kFlushU = GSTEX_FLUSH_U;  // staging entries per lane per flush pass
+static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging area");
 
 
 template <int C, bool GEO>
@@ -862,7 +964,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
-    __shared__ int s_texq[kTexStage];
+    __shared__ TexQ s_texq[kTexStage];
 
     // unit = 4 slot + quadrant (see AuxPtrs), launched costliest first; a unit the forward never evaluated in is empty
     const int unit = aux.order[blockIdx.x];
@@ -1037,7 +1139,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if (has_tex && !(GSTEX_ABLATE & 1)) {
                     tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
                     tw = w * tex_scale;  // d value / d stored texel
-                    P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
+                    if (kTexFixed) P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
                     tax = b.ax;
                     tay = b.ay;
                 }
@@ -1114,8 +1216,10 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 }
                 // take the bound out of the spare slot (kMBound) before the row is stored
                 constexpr int kML = GEO ? 48 : 56, kMI = GEO ? 3 : 0;  // its lane and index after the reduce-scatter
-                vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
-                if (lane == kML) P[kMI] = 0.0f;
+                if (kTexFixed) {
+                    vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
+                    if (lane == kML) P[kMI] = 0.0f;
+                }
                 // the (pair, quadrant) row: lanes 8k hold NP / 8 consecutive values each; the flag (1: 24-value
                 // row, 2: 32-value row) marks it written
                 const int slot = __builtin_amdgcn_readlane(my_slot, j);
@@ -1138,9 +1242,9 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // weights <= 1), so at scale 2^S, S = 30 - e (vis_M < 2^e), the tails (each < 2^30) and their int32
                 // sums stay in range; resolution 2^-30 of the visit's total
                 int e_m = 0;
-                if (vis_M > 0.f) (void)frexpf(vis_M, &e_m);
-                const int tex_S = kTexFixBits - e_m;
-                const float twq = tw * __builtin_ldexpf(1.0f, tex_S);
+                if (kTexFixed && vis_M > 0.f) (void)frexpf(vis_M, &e_m);
+                const int tex_S = kTexFixed ? kTexFixBits - e_m : 0;
+                const float twq = kTexFixed ? tw * __builtin_ldexpf(1.0f, tex_S) : tw;
                 float tg[4 * CM];
                 {
 #pragma clang fp contract(fast)
@@ -1171,23 +1275,24 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-                                atomicAdd(&s_texq[c00 + c], fixed_round(tg[c]));
-                                atomicAdd(&s_texq[c01 + c], fixed_round(tg[CM + c]));
-                                atomicAdd(&s_texq[c10 + c], fixed_round(tg[2 * CM + c]));
-                                atomicAdd(&s_texq[c11 + c], fixed_round(tg[3 * CM + c]));
+                                stage_add(&s_texq[c00 + c], tg[c]);
+                                stage_add(&s_texq[c01 + c], tg[CM + c]);
+                                stage_add(&s_texq[c10 + c], tg[2 * CM + c]);
+                                stage_add(&s_texq[c11 + c], tg[3 * CM + c]);
                             }
                         }
                     } else {
                         // block larger than the staging area: straight to global, back in value units
                         float* base = v_texture + (size_t)r.off * Cn;
                         const int uS = -tex_S;
+                        auto val = [&](float y) { return kTexFixed ? __builtin_ldexpf(y, uS) : y; };
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
-                                atomicAdd(base + c00 + c, __builtin_ldexpf(tg[c], uS));
-                                atomicAdd(base + c01 + c, __builtin_ldexpf(tg[CM + c], uS));
-                                atomicAdd(base + c10 + c, __builtin_ldexpf(tg[2 * CM + c], uS));
-                                atomicAdd(base + c11 + c, __builtin_ldexpf(tg[3 * CM + c], uS));
+                                atomicAdd(base + c00 + c, val(tg[c]));
+                                atomicAdd(base + c01 + c, val(tg[CM + c]));
+                                atomicAdd(base + c10 + c, val(tg[2 * CM + c]));
+                                atomicAdd(base + c11 + c, val(tg[3 * CM + c]));
                             }
                         }
                     }
@@ -1199,7 +1304,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     // kFlushU entries per lane per pass, their LDS reads issued together (one wait per pass); entries
                     // past the block are zero (the staging area is kept zeroed) and kTexStage is a multiple of the pass
                     for (int e0 = lane; e0 < bsize; e0 += 64 * kFlushU) {
-                        int v[kFlushU];
+                        TexQ v[kFlushU];
                         GSTEX_STAT(4, 1);
 #pragma unroll
                         for (int k = 0; k < kFlushU; ++k) v[k] = s_texq[e0 + 64 * k];
@@ -1208,7 +1313,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                             GSTEX_STAT(6, __popcll(__ballot(v[k] != 0)));
                             if (v[k] == 0) continue;
                             s_texq[e0 + 64 * k] = 0;
-                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, __builtin_ldexpf((float)v[k], -tex_S));
+                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, kTexFixed ? __builtin_ldexpf((float)v[k], -tex_S) : (float)v[k]);
                         }
                     }
                 }
