@@ -111,6 +111,10 @@ struct BwdShape {
 #endif
 constexpr int kTexStage = GSTEX_TEX_STAGE;
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
+#ifndef GSTEX_FWD_DEFER
+#define GSTEX_FWD_DEFER 1
+#endif
+constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in one visit later (C = 3)
 #ifndef GSTEX_ABLATE
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
@@ -536,6 +540,24 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
     float D = 0.f, M1 = 0.f, M2 = 0.f, reg = 0.f;
     int last = -1;
     bool done = !inside;
+    // Deferred texel accumulation (kFwdDefer): a visit's four texel gathers are issued into the pending registers
+    // and folded into tex[] at the lane's next contributing visit (or at a checkpoint / the end), so their latency
+    // overlaps the next visit's record read and pair evaluation.  Same values, same order of accumulation.
+    constexpr bool kDefer = kFwdDefer && C == 3;
+    bool pend = false;
+    float p00[CM], p01[CM], p10[CM], p11[CM], pax = 0.f, pay = 0.f, pw = 0.f;
+    auto fold_pending = [&]() {
+        if (kDefer && pend) {
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                if (c < Cn) {
+                    const float val = bilerp_mix(p00[c], p01[c], p10[c], p11[c], pax, pay) * tex_scale + tex_bias;
+                    tex[c] = tex[c] + val * pw;
+                }
+            }
+            pend = false;
+        }
+    };
     const int lane = tid & 63, wave = tid >> 6;
     const size_t vm_base = visit_mask_base(rng.x, tile);
     const int sbase = seg_base(rng.x, tile);
@@ -571,6 +593,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
             // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
             const int cnt = wave_max_i(seg_visits);  // lanes leave the visit loop as they finish: the wave's count
             if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt ? (cnt | xgroup) : 0;
+            fold_pending();
             if (__any(!done)) write_ck(sbase + cur_seg);
             seg_visits = 0;
             ++cur_seg;
@@ -613,7 +636,25 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
             }
             const float w = h.alpha * T;
             // (a block running past the texel store -- corrupt texture_dims -- contributes no texture)
-            if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && !(GSTEX_ABLATE & 4)) {
+            if (kDefer) {
+                const bool has_tex = r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && !(GSTEX_ABLATE & 4);
+                float tu = 0.f, tv = 0.f;
+                if (has_tex) tex_coords(r, h.u, h.v, tu, tv);
+                const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
+                fold_pending();  // the previous visit's texels (issued one visit ago) before their registers are reused
+                if (has_tex) {
+                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
+                    if (GSTEX_ABLATE & 512) {
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) p00[c] = p01[c] = p10[c] = p11[c] = __int_as_float(b.i0 + c);
+                    } else
+                    load_texel_quad<CM>(rs, b, r.w, Cn, p00, p01, p10, p11);
+                    pax = b.ax;
+                    pay = b.ay;
+                    pw = w;
+                    pend = true;
+                }
+            } else if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && !(GSTEX_ABLATE & 4)) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
                 const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
@@ -650,6 +691,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
           }
         }
     }
+    fold_pending();
     if (aux.cost) {
         const int cnt = wave_max_i(seg_visits);
         if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt ? (cnt | xgroup) : 0;
