@@ -102,11 +102,42 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(int n, const i
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = ex;
 }
 
+// Short inputs (the per-tile scans): one workgroup walks the tiles with a running carry, one launch instead of three.
+__global__ __launch_bounds__(kScanThreads) void scan_single_kernel(int n, const int32_t* __restrict__ in,
+                                                                   int32_t* __restrict__ out) {
+    __shared__ int s_wave[kScanThreads / 64];
+    int carry = 0;
+    for (int b0 = 0; b0 < n; b0 += kScanTile) {
+        const int base = b0 + threadIdx.x * kScanItems;
+        int vals[kScanItems];
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k) {
+            vals[k] = (base + k < n) ? in[base + k] : 0;
+            v += vals[k];
+        }
+        int total;
+        int ex = block_excl_scan(v, s_wave, &total) + carry;
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k) {
+            if (base + k < n) out[base + k] = ex;
+            ex += vals[k];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+}
+constexpr int kScanSingleMaxTiles = 16;
+
 int run_scan(int n, const int32_t* in, int32_t* out, int32_t* block_sums, hipStream_t st) {
     int nb = div_up(n, kScanTile);
     if (nb == 0) {
         (void)hipMemsetAsync(out, 0, sizeof(int32_t), st);
         return launch_status("scan(empty)");
+    }
+    if (nb <= kScanSingleMaxTiles) {
+        scan_single_kernel<<<1, kScanThreads, 0, st>>>(n, in, out);
+        return launch_status("scan");
     }
     scan_partials_kernel<<<nb, kScanThreads, 0, st>>>(n, in, block_sums);
     scan_block_sums_kernel<<<1, kScanThreads, 0, st>>>(nb, block_sums);
@@ -538,18 +569,10 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
 // of one 2x2-tile macro-block share one XCD's L2 (texel blocks, records).  If the groups are too uneven for that
 // (8 max_g len_g > n_units), the order is the plain descending-cost one.  Order inside a bucket is unspecified --
 // scheduling only, outputs do not depend on it.
-constexpr int kUnitBuckets = 1024;
-constexpr int kUnitGroups = 8;
-constexpr int kUnitBins = kUnitBuckets * kUnitGroups;
 constexpr int kUnitsPerBlock = 4096;
 // scratch (int32): [0, 8192) histogram, [8192, 16384) group-interleaved starts, [16384, 24576) plain starts,
 // [24576] mode (1 = group-interleaved)
 constexpr int kUnitScratch = 3 * kUnitBins + 16;
-
-__device__ __forceinline__ int unit_bin(int key) {
-    const int c = key & 0xFFFFFF, g = (key >> 24) & (kUnitGroups - 1);
-    return g * kUnitBuckets + (kUnitBuckets - 1 - min(c, kUnitBuckets - 1));
-}
 
 __global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __restrict__ key,
                                                         int32_t* __restrict__ hist) {
@@ -567,50 +590,53 @@ __global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __
 }
 
 __global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int n, int32_t* __restrict__ ws) {
-    // per group: exclusive scan of its buckets (costliest first) -> the group-interleaved starts; across groups
-    // (bucket-major, group-minor) -> the plain starts
-    __shared__ int s[kUnitBuckets];
-    __shared__ int s_len[kUnitGroups];
-    const int t = threadIdx.x;
-    const int32_t* hist = ws;
-    int tot = 0;  // units in bucket t over all groups
+    // thread t = bucket t: per group, the exclusive scan of its buckets (costliest first) -> the group-interleaved
+    // starts; over all groups (bucket-major, group-minor) -> the plain starts.  The 9 scans run together: wave
+    // scans, then one exchange of the 16 wave totals.
+    constexpr int NV = kUnitGroups + 1, NW = kUnitBuckets / 64;
+    __shared__ int s_tot[NW][NV];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int h[NV], x[NV];
+    h[kUnitGroups] = 0;
+#pragma unroll
     for (int g = 0; g < kUnitGroups; ++g) {
-        const int h = hist[g * kUnitBuckets + t];
-        tot += h;
-        s[t] = h;
-        __syncthreads();
-        for (int o = 1; o < kUnitBuckets; o <<= 1) {
-            const int v = t >= o ? s[t - o] : 0;
-            __syncthreads();
-            s[t] += v;
-            __syncthreads();
-        }
-        ws[kUnitBins + g * kUnitBuckets + t] = s[t] - h;
-        if (t == kUnitBuckets - 1) s_len[g] = s[t];
-        __syncthreads();
+        h[g] = ws[g * kUnitBuckets + t];
+        h[kUnitGroups] += h[g];
     }
-    s[t] = tot;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x[i] = wave_incl_scan(h[i]);
+    if (lane == 63)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) s_tot[wave][i] = x[i];
     __syncthreads();
-    for (int o = 1; o < kUnitBuckets; o <<= 1) {
-        const int v = t >= o ? s[t - o] : 0;
-        __syncthreads();
-        s[t] += v;
-        __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int off = 0;
+        for (int w = 0; w < wave; ++w) off += s_tot[w][i];
+        x[i] += off - h[i];  // exclusive
     }
-    int run = s[t] - tot;
+#pragma unroll
+    for (int g = 0; g < kUnitGroups; ++g) ws[kUnitBins + g * kUnitBuckets + t] = x[g];
+    int run = x[kUnitGroups];
+#pragma unroll
     for (int g = 0; g < kUnitGroups; ++g) {
         ws[2 * kUnitBins + g * kUnitBuckets + t] = run;
-        run += hist[g * kUnitBuckets + t];
+        run += h[g];
     }
     if (t == 0) {
         int mx = 0;
-        for (int g = 0; g < kUnitGroups; ++g) mx = max(mx, s_len[g]);
+        for (int g = 0; g < kUnitGroups; ++g) {
+            int len = 0;
+            for (int w = 0; w < NW; ++w) len += s_tot[w][g];
+            mx = max(mx, len);
+        }
         ws[3 * kUnitBins] = (long long)kUnitGroups * mx <= (long long)n ? 1 : 0;
     }
 }
 
 __global__ __launch_bounds__(256) void unit_scatter_kernel(int n, const int32_t* __restrict__ key,
-                                                           int32_t* __restrict__ ws, int32_t* __restrict__ order) {
+                                                           int32_t* __restrict__ ws, int32_t* __restrict__ order,
+                                                           int bias) {
     __shared__ int s_h[kUnitBins];
     const bool grouped = ws[3 * kUnitBins] != 0;
     int32_t* next = ws + (grouped ? kUnitBins : 2 * kUnitBins);
@@ -631,7 +657,7 @@ __global__ __launch_bounds__(256) void unit_scatter_kernel(int n, const int32_t*
         if (!(k & 0xFFFFFF)) continue;
         const int b = unit_bin(k);
         const int r = atomicAdd(&s_h[b], 1);
-        order[grouped ? kUnitGroups * r + b / kUnitBuckets : r] = u;
+        order[grouped ? kUnitGroups * r + b / kUnitBuckets : r] = u + bias;
     }
 }
 
@@ -649,6 +675,16 @@ extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_key, int32_
     const int nb = div_up(n_units, kUnitsPerBlock);
     unit_hist_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch);
     unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(n_units, scratch);
-    unit_scatter_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch, unit_order);
+    unit_scatter_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch, unit_order, 0);
     return launch_status("gstex_unit_order");
 }
+
+namespace gstex {
+int unit_order_from_hist(int32_t n_units, const int32_t* unit_key, int32_t* unit_order, int32_t* scratch,
+                         hipStream_t st) {
+    if (n_units <= 0) return GSTEX_OK;
+    unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(n_units, scratch);
+    unit_scatter_kernel<<<div_up(n_units, kUnitsPerBlock), 256, 0, st>>>(n_units, unit_key, scratch, unit_order, 1);
+    return launch_status("unit_order_from_hist");
+}
+}  // namespace gstex

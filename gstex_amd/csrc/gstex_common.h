@@ -374,6 +374,19 @@ enum PartField {
     P_A = 0, P_B = 3, P_P0 = 6, P_XY = 9, P_OPAC = 11, P_RGB = 12,
     P_TU0 = 15, P_AUU = 16, P_AUV = 17, P_TV0 = 18, P_AVU = 19, P_AVV = 20, P_NRM = 21, P_TW = 24
 };
+// Backward unit order (binning.hip gstex_unit_order): counting-sort bins = XCD group x descending cost bucket.
+constexpr int kUnitBuckets = 1024;
+constexpr int kUnitGroups = 8;
+constexpr int kUnitBins = kUnitBuckets * kUnitGroups;
+__device__ __forceinline__ int unit_bin(int key) {
+    const int c = key & 0xFFFFFF, g = (key >> 24) & (kUnitGroups - 1);
+    return g * kUnitBuckets + (kUnitBuckets - 1 - min(c, kUnitBuckets - 1));
+}
+// Internal entry (binning.hip) for the raster backward: the order from a histogram the forward already built in
+// scratch[0, kUnitBins); order[] entries are unit + 1 (0 = no unit at that launch position; the caller zeroed it).
+int unit_order_from_hist(int32_t n_units, const int32_t* unit_key, int32_t* unit_order, int32_t* scratch,
+                         hipStream_t st);
+
 constexpr int kPartRow = 24;     // values per row without geometry gradients
 constexpr int kPartRowGeo = 32;  // with (27 used)
 

@@ -592,7 +592,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
         if (aux.cost && b0 > rng.x && (b0 - rng.x) % kSegLen == 0) {
             // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
             const int cnt = wave_max_i(seg_visits);  // lanes leave the visit loop as they finish: the wave's count
-            if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt ? (cnt | xgroup) : 0;
+            if (lane == 0 && cnt) {
+                aux.cost[(sbase + cur_seg) * 4 + wave] = cnt | xgroup;
+                atomicAdd(&aux.order_ws[unit_bin(cnt | xgroup)], 1);  // the backward's unit-order histogram
+            }
             fold_pending();
             if (__any(!done)) write_ck(sbase + cur_seg);
             seg_visits = 0;
@@ -694,7 +697,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
     fold_pending();
     if (aux.cost) {
         const int cnt = wave_max_i(seg_visits);
-        if (lane == 0) aux.cost[(sbase + cur_seg) * 4 + wave] = cnt ? (cnt | xgroup) : 0;
+        if (lane == 0 && cnt) {
+            aux.cost[(sbase + cur_seg) * 4 + wave] = cnt | xgroup;
+            atomicAdd(&aux.order_ws[unit_bin(cnt | xgroup)], 1);
+        }
         // final accumulators for the backward's earlier segments, in the slot of the wave's last segment
         const int wl = wave_max_i(last);
         if (wl >= kSegLen) write_ck(sbase + wl / kSegLen);
@@ -1009,7 +1015,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     __shared__ TexQ s_texq[kTexStage];
 
     // unit = 4 slot + quadrant (see AuxPtrs), launched costliest first; a unit the forward never evaluated in is empty
-    const int unit = aux.order[blockIdx.x];
+    const int unit = aux.order[blockIdx.x] - 1;  // entries are unit + 1
     if (unit < 0) return;  // a launch position no unit was placed at (empty units take none)
     const int quad = unit & 3, slot = unit >> 2;
     const int tile = aux.slot_tile[slot];
@@ -1637,8 +1643,9 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
     const int nblk = tiles_x * tiles_y;
     const AuxLayout al = aux_layout(n_isect, nblk, channels);
     const AuxPtrs ap = aux_ptrs(aux, al);
-    // units the forward never reaches keep cost 0 (the backward skips them)
-    if (aux && hipMemsetAsync(ap.cost, 0, (size_t)al.n_units * 4, st) != hipSuccess)
+    // one fill: unit costs (units the forward never reaches keep 0; the backward skips them), the launch order
+    // (0 = no unit at that position) and the unit-order histogram the forward builds (contiguous in the layout)
+    if (aux && hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
         return launch_status("gstex_raster_fwd (aux)");
 #define GSTEX_FWD(CC, GG)                                                                                      \
     raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,      \
@@ -1685,7 +1692,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     const AuxPtrs ap = aux_ptrs(aux, al);
     if (n_isect > 0 && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
-    rc = gstex_unit_order((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, stream);  // costliest units first
+    // costliest units first, from the histogram the forward built (order entries are unit + 1)
+    rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
     if (rc) return rc;
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
