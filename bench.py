@@ -263,9 +263,8 @@ def main():
     step_no = [0]
 
     def step():
-        with torch.no_grad():  # stationary workload: same geometry every step (8.8 MB copy, timed)
-            for p, p0 in zip(geom, geom0):
-                p.copy_(p0)
+        with torch.no_grad():  # stationary workload: same geometry every step (8.8 MB copy, timed, one launch)
+            torch._foreach_copy_(geom, geom0)
         pose = (rank + step_no[0] * world) % N_POSES
         step_no[0] += 1
         if sync is not None:

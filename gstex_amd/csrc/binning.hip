@@ -569,7 +569,10 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
 // of one 2x2-tile macro-block share one XCD's L2 (texel blocks, records).  If the groups are too uneven for that
 // (8 max_g len_g > n_units), the order is the plain descending-cost one.  Order inside a bucket is unspecified --
 // scheduling only, outputs do not depend on it.
-constexpr int kUnitsPerBlock = 4096;
+#ifndef GSTEX_UNITS_PER_BLOCK
+#define GSTEX_UNITS_PER_BLOCK 1024  // measured: 4096 17.5 us, 2048 12.6, 1024 10.3 (unit scatter at cfg3)
+#endif
+constexpr int kUnitsPerBlock = GSTEX_UNITS_PER_BLOCK;
 // scratch (int32): [0, 8192) histogram, [8192, 16384) group-interleaved starts, [16384, 24576) plain starts,
 // [24576] mode (1 = group-interleaved)
 constexpr int kUnitScratch = 3 * kUnitBins + 16;

@@ -206,6 +206,17 @@ def get_num_tiles_hit_2d(centers, extents, H: int, W: int, block_width: int) -> 
 # binning
 # ----------------------------------------------------------------------------------------
 _PINNED = {}
+_ZEROS = {}
+
+
+def _zero_scalar(device) -> torch.Tensor:
+    """One cached fp32 zero per device, the storage of the geometry outputs a photometric forward does not
+    produce (returned as broadcast views)."""
+    key = str(device)
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros((), device=device, dtype=torch.float32)
+    return z
 
 
 def _start_count(x: torch.Tensor):
@@ -375,9 +386,10 @@ class _TextureGaussians(torch.autograd.Function):
             geo_ptrs = (ptr(depth), ptr(reg), ptr(normal))
             if int(settings) & _lib.SETTING_EVAL_NORMAL:
                 ctx.mark_non_differentiable(normal)  # bit 15: unit normals, a forward-only eval output
-        else:  # not produced by the kernel: zeros, no gradient
-            z = torch.zeros((5, H, W), **f)
-            depth, reg, normal = z[0], z[1], z[2:5].permute(1, 2, 0)
+        else:  # not produced by the kernel: zeros, no gradient (read-only broadcast views of one cached zero:
+            # no fill per call; an in-place write into them raises instead of corrupting later calls)
+            z = _zero_scalar(f["device"])
+            depth, reg, normal = z.expand(H, W), z.expand(H, W), z.expand(H, W, 3)
             geo_ptrs = (None, None, None)
             ctx.mark_non_differentiable(depth, reg, normal)
         # per (tile, wave, splat) cull bits of the forward for the backward
