@@ -1387,6 +1387,99 @@ static_assert(kSetupBwdSplats % kSetupBwdRows == 0 && kSetupBwdSplats <= 256, "s
 // FOLD_AABB: the centres were produced by get_aabb_2d from these same means / scales / quats (training
 // path), so the AABB-centre chain (aabb_bwd_kernel's arithmetic) is applied here and added in, instead of
 // a separate launch plus autograd's accumulation kernels; the sums are the same two terms added once.
+#ifndef GSTEX_SETUP_SPLIT
+#define GSTEX_SETUP_SPLIT 1
+#endif
+// Split form (GSTEX_SETUP_SPLIT): setup_bwd_sum_kernel, 32 lanes per splat (lane c = column c), sums the splat's
+// flagged rows in the same (slot, quadrant) order and writes the 32 sums over the splat's first row (slot
+// offsets[g], quadrant 0), whose values it has already read -- no other splat reads that row; then
+// setup_bwd_chain_kernel, one thread per splat, chains the sums to the parameters.  (The fused kernel below keeps
+// 216 of its 256 threads idle through the chain and serialises its 5 splat groups' load chains.)
+#ifndef GSTEX_SUM_SLOTS
+#define GSTEX_SUM_SLOTS 8
+#endif
+constexpr int kSumSlots = GSTEX_SUM_SLOTS;  // slots whose rows one lane group has in flight at once
+// 32 lanes per splat: lane 8 q + m reads float4 m (columns 4m .. 4m+3) of the quadrant-q rows, kSumSlots slots at a
+// time, and sums them in slot order; the 4 quadrant sums are then combined (q0 + q1) + (q2 + q3) across lanes.
+// Deterministic (fixed order), like the fused kernel's slot-major quadrant-minor order it replaces.
+__global__ __launch_bounds__(256) void setup_bwd_sum_kernel(int n, const int32_t* __restrict__ nth,
+                                                           const int32_t* __restrict__ offsets,
+                                                           float* __restrict__ partials,
+                                                           const uint32_t* __restrict__ row_flags) {
+    const int l = threadIdx.x & 31, q = l >> 3, m = l & 7;
+    const int g = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const bool live = g < n;
+    const int cnt = live ? nth[g] : 0;
+    const size_t s0 = live ? (size_t)offsets[g] : 0;
+    // columns 24.. exist only in 32-value rows (flag 2: backward with depth / normal gradients)
+    const uint32_t need = m < kPartRow / 4 ? 0xFFu : 0x02u;
+    const float4* rows = reinterpret_cast<const float4*>(partials + s0 * 4 * kRowStride) + q * (kRowStride / 4) + m;
+    const uint32_t* fl = row_flags + s0;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = 0; e < cnt; e += kSumSlots) {
+        uint32_t f[kSumSlots];
+#pragma unroll
+        for (int u = 0; u < kSumSlots; ++u) f[u] = e + u < cnt ? fl[e + u] : 0u;
+        float4 r[kSumSlots];
+#pragma unroll
+        for (int u = 0; u < kSumSlots; ++u)
+            r[u] = (f[u] >> (8 * q)) & need ? rows[(size_t)(e + u) * (4 * kRowStride / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < kSumSlots; ++u) {
+            if ((f[u] >> (8 * q)) & need) {
+                acc.x += r[u].x;
+                acc.y += r[u].y;
+                acc.z += r[u].z;
+                acc.w += r[u].w;
+            }
+        }
+    }
+    // (q0 + q1) + (q2 + q3): lane l adds lane l ^ 8, then lane l ^ 16 (inside the 32-lane splat group)
+    auto xadd = [](float4 a, int mask) {
+        return make_float4(a.x + __shfl_xor(a.x, mask, 32), a.y + __shfl_xor(a.y, mask, 32),
+                           a.z + __shfl_xor(a.z, mask, 32), a.w + __shfl_xor(a.w, mask, 32));
+    };
+    acc = xadd(acc, 8);
+    acc = xadd(acc, 16);
+    // the sums over the splat's first row, whose values every lane has read above: no other splat reads it
+    if (live && cnt > 0 && q == 0)
+        reinterpret_cast<float4*>(partials + s0 * 4 * kRowStride)[m] = acc;
+}
+
+template <bool FOLD_AABB>
+__device__ __forceinline__ void setup_bwd_chain(int g, const float (&S)[kPartRowGeo], int cnt, const Camera& cam,
+    const float* __restrict__ means, const float* __restrict__ scales, float glob,
+    const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
+    float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
+    float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers, float* __restrict__ v_uv0);
+
+template <bool FOLD_AABB>
+__global__ __launch_bounds__(256) void setup_bwd_chain_kernel(
+    int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
+    const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
+    const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials,
+    CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
+    float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers, float* __restrict__ v_uv0) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    const Camera cam = load_camera(cam_args);
+    const int cnt = nth[g];
+    float S[kPartRowGeo];
+    if (cnt > 0) {
+        const float4* src = reinterpret_cast<const float4*>(partials + (size_t)offsets[g] * 4 * kRowStride);
+#pragma unroll
+        for (int i = 0; i < kPartRowGeo / 4; ++i) {
+            const float4 v = src[i];
+            S[4 * i] = v.x; S[4 * i + 1] = v.y; S[4 * i + 2] = v.z; S[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kPartRowGeo; ++i) S[i] = 0.f;
+    }
+    setup_bwd_chain<FOLD_AABB>(g, S, cnt, cam, means, scales, glob, quats, umap, vmap, v_means, v_scales, v_quats,
+                               v_rgbs, v_opac, v_centers, v_uv0);
+}
+
 template <bool FOLD_AABB>
 __global__ __launch_bounds__(256) void setup_bwd_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
@@ -1441,7 +1534,16 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     float S[kPartRowGeo];
 #pragma unroll
     for (int i = 0; i < kPartRowGeo; ++i) S[i] = s_sum[t][i];
-    const int cnt = nth[g];
+    setup_bwd_chain<FOLD_AABB>(g, S, nth[g], cam, means, scales, glob, quats, umap, vmap, v_means, v_scales, v_quats,
+                               v_rgbs, v_opac, v_centers, v_uv0);
+}
+
+template <bool FOLD_AABB>
+__device__ __forceinline__ void setup_bwd_chain(int g, const float (&S)[kPartRowGeo], int cnt, const Camera& cam,
+    const float* __restrict__ means, const float* __restrict__ scales, float glob,
+    const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
+    float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
+    float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers, float* __restrict__ v_uv0) {
     v_rgbs[3 * g + 0] = S[P_RGB + 0];
     v_rgbs[3 * g + 1] = S[P_RGB + 1];
     v_rgbs[3 * g + 2] = S[P_RGB + 2];
@@ -1717,10 +1819,29 @@ extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32
     return aux_layout(n_isect, n_tiles, channels).bytes;
 }
 
+template <bool FOLD_AABB>
+int setup_bwd_launch(int32_t n, const float* means, const float* scales, float glob_scale, const float* quats,
+                     const float* umap, const float* vmap, const int32_t* nth, const int32_t* offsets,
+                     float* partials, const uint32_t* row_flags, const gstex_camera* cam, float* v_means,
+                     float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
+                     float* v_uv0, hipStream_t st, const char* name) {
+    if (GSTEX_SETUP_SPLIT) {
+        setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags);
+        setup_bwd_chain_kernel<FOLD_AABB><<<div_up(n, 256), 256, 0, st>>>(
+            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, to_device_camera(*cam), v_means,
+            v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+    } else {
+        setup_bwd_kernel<FOLD_AABB><<<div_up(n, kSetupBwdSplats), 256, 0, st>>>(
+            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, row_flags,
+            to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+    }
+    return launch_status(name);
+}
+
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                                       const float* quats, const float* opacities, const float* umap,
                                       const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      const float* partials, const uint32_t* row_flags, const gstex_camera* cam,
+                                      float* partials, const uint32_t* row_flags, const gstex_camera* cam,
                                       float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
                                       float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
@@ -1729,16 +1850,15 @@ extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float
     GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd: null pointer");
-    setup_bwd_kernel<false><<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
-        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, row_flags,
-        to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
-    return launch_status("gstex_raster_setup_bwd");
+    return setup_bwd_launch<false>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
+                                   row_flags, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
+                                   as_stream(stream), "gstex_raster_setup_bwd");
 }
 
 extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
                                       const float* quats, const float* opacities, const float* umap,
                                       const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      const float* partials, const uint32_t* row_flags, const gstex_camera* cam,
+                                      float* partials, const uint32_t* row_flags, const gstex_camera* cam,
                                       float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
                                       float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
@@ -1747,10 +1867,9 @@ extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const 
     GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd_aabb: null pointer");
-    setup_bwd_kernel<true><<<div_up(n, kSetupBwdSplats), 256, 0, as_stream(stream)>>>(
-        n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials, row_flags,
-        to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
-    return launch_status("gstex_raster_setup_bwd_aabb");
+    return setup_bwd_launch<true>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
+                                   row_flags, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
+                                   as_stream(stream), "gstex_raster_setup_bwd_aabb");
 }
 
 extern "C" int gstex_texture_edit(const gstex_camera* cam, int32_t settings, const float* records,

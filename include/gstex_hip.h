@@ -165,11 +165,12 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
                      uint32_t* row_flags, float* v_texture, void* aux, void* stream);
 /* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
- * them to the splat parameters. Outputs are overwritten. */
+ * them to the splat parameters. Outputs are overwritten.  partials is consumed: each splat's sums are written
+ * over its first row (the rows are backward scratch, not read again). */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                            const float* quats, const float* opacities, const float* umap,
                            const float* vmap, const int32_t* num_tiles_hit,
-                           const int32_t* offsets, const float* partials, const uint32_t* row_flags,
+                           const int32_t* offsets, float* partials, const uint32_t* row_flags,
                            const gstex_camera* cam, float* v_means, float* v_scales,
                            float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                            float* v_uv0, void* stream);
@@ -180,7 +181,7 @@ int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, f
 int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
                                 const float* quats, const float* opacities, const float* umap,
                                 const float* vmap, const int32_t* num_tiles_hit,
-                                const int32_t* offsets, const float* partials, const uint32_t* row_flags,
+                                const int32_t* offsets, float* partials, const uint32_t* row_flags,
                                 const gstex_camera* cam, float* v_means, float* v_scales,
                                 float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                                 float* v_uv0, void* stream);
