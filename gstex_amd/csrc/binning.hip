@@ -24,6 +24,9 @@ constexpr int kScanItems = 4;
 constexpr int kScanTile = kScanThreads * kScanItems;
 constexpr int kSortThreads = 256;
 constexpr int kSortCap = 4096;  // keys per LDS sort (32 KiB)
+#ifndef GSTEX_SORT_REGS
+#define GSTEX_SORT_REGS 1
+#endif
 
 // Inclusive wave64 scan.
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -316,7 +319,65 @@ __device__ __forceinline__ void write_sorted(int pos, unsigned long long key, co
     sorted_ids[pos] = slot_gid[slot];
 }
 
-// 4. one workgroup per tile
+// Bitonic sort of P = 256 E keys held E per thread (thread t: positions [t E, t E + E)), ascending.  Stages with a
+// partner distance j < E swap inside the thread's registers; j < 64 E stays inside the wave's segment of the
+// LDS buffer, whose operations the wave issues and the LDS completes in order (no barrier, only a compiler barrier:
+// a lane's partner reads must not move above its own writes); only j >= 64 E (3 stages at most) needs the
+// workgroup barrier.  (bitonic_lds: a barrier after each of the up to 78 stages.)
+template <int E>
+__device__ __forceinline__ int pad(int p) { return p + p / E; }
+template <int E>
+__device__ __forceinline__ void bitonic_regs(unsigned long long (&k)[E], unsigned long long* s, int P) {
+    const int base = threadIdx.x * E;
+    for (int kk = 2; kk <= P; kk <<= 1) {
+        for (int j = kk >> 1; j >= E; j >>= 1) {
+            const bool block = j >= 64 * E;
+            // one pad slot per thread chunk: lanes' chunks start 2 (E + 1) dwords apart, not 2 E (bank conflicts)
+#pragma unroll
+            for (int e = 0; e < E; ++e) s[pad<E>(base + e)] = k[e];
+            if (block) __syncthreads();
+            else asm volatile("" ::: "memory");  // compiler barrier: other lanes' LDS values (the LDS is in order)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = base + e;
+                const unsigned long long v = s[pad<E>(i ^ j)];
+                const bool lo = (i & j) == 0, up = (i & kk) == 0;
+                k[e] = (lo == up) ? (k[e] < v ? k[e] : v) : (k[e] < v ? v : k[e]);
+            }
+            if (block) __syncthreads();
+            else asm volatile("" ::: "memory");  // compiler barrier: other lanes' LDS values (the LDS is in order)
+        }
+#pragma unroll
+        for (int jj = E / 2; jj >= 1; jj >>= 1) {
+            if (jj >= kk) continue;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                if (e & jj) continue;
+                const bool up = ((base + e) & kk) == 0;
+                const unsigned long long a = k[e], b = k[e + jj];
+                const bool sw = (a > b) == up;
+                k[e] = sw ? b : a;
+                k[e + jj] = sw ? a : b;
+            }
+        }
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void tile_sort_regs(const unsigned long long* src, int K, int start,
+                                               unsigned long long* s, const int32_t* slot_gid, int32_t* sorted_ids,
+                                               int32_t* sorted_slots) {
+    constexpr int P = 256 * E;
+    unsigned long long k[E];
+    const int base = threadIdx.x * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) k[e] = base + e < K ? src[base + e] : ~0ull;
+    bitonic_regs<E>(k, s, P);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (base + e < K) write_sorted(start + base + e, k[e], slot_gid, sorted_ids, sorted_slots);
+}
+
 // 4. one workgroup per tile, launched largest bucket first (order[]): the big image-centre buckets no
 //    longer start last and set the kernel's tail
 __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
@@ -324,7 +385,7 @@ __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
     unsigned long long* __restrict__ keys, unsigned long long* __restrict__ scratch,
     const int32_t* __restrict__ slot_gid, int32_t* __restrict__ tile_ranges, int32_t* __restrict__ sorted_ids,
     int32_t* __restrict__ sorted_slots) {
-    __shared__ unsigned long long s_keys[kSortCap];
+    __shared__ unsigned long long s_keys[kSortCap + kSortThreads];  // + the register sort's pad slots
     const int t = order ? order[blockIdx.x] : (int)blockIdx.x;
     const int start = tile_start[t], end = tile_start[t + 1];
     const int K = end - start;
@@ -335,6 +396,15 @@ __global__ __launch_bounds__(kSortThreads) void tile_sort_kernel(
     if (K == 0) return;
     unsigned long long* src = keys + start;
     if (K <= kSortCap) {
+        if (GSTEX_SORT_REGS) {
+            static_assert(kSortCap == 16 * kSortThreads, "register sort covers the LDS capacity");
+            if (K <= 256) tile_sort_regs<1>(src, K, start, s_keys, slot_gid, sorted_ids, sorted_slots);
+            else if (K <= 512) tile_sort_regs<2>(src, K, start, s_keys, slot_gid, sorted_ids, sorted_slots);
+            else if (K <= 1024) tile_sort_regs<4>(src, K, start, s_keys, slot_gid, sorted_ids, sorted_slots);
+            else if (K <= 2048) tile_sort_regs<8>(src, K, start, s_keys, slot_gid, sorted_ids, sorted_slots);
+            else tile_sort_regs<16>(src, K, start, s_keys, slot_gid, sorted_ids, sorted_slots);
+            return;
+        }
         int P = 1;
         while (P < K) P <<= 1;
         for (int i = threadIdx.x; i < P; i += kSortThreads) s_keys[i] = (i < K) ? src[i] : ~0ull;

@@ -119,6 +119,14 @@ def test_binning_large_bucket_merge_path():
     assert (tr[:, 1] - tr[:, 0]).max() > 4096 * 2
 
 
+@pytest.mark.parametrize("n", [200, 450, 1000, 2000, 4000])
+def test_binning_register_sort_sizes(n):
+    # every splat on the same 4 tiles: buckets of ~n keys exercise each register-sort width (256 E keys, E = 1..16)
+    case = make_case(n=n, n_texels=0, H=32, W=32, seed=9, cube=0.3)
+    tr = _bins_equal(case)
+    assert 0 < (tr[:, 1] - tr[:, 0]).max() <= 4096
+
+
 def test_binning_equal_depths_tie_break():
     case = make_case(n=400, n_texels=0, H=48, W=48, seed=7)
     case.inp.depths = torch.full_like(case.inp.depths, 3.0)  # every key ties on depth -> id order
