@@ -408,7 +408,9 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     h.dx = px - r.xa;
     h.dy = py - r.ya;
     // p = k x l in affine form (gstex_common.h affine_homog)
-    h.p = f3{h.dx * r.A.x + h.dy * r.B.x, h.dx * r.A.y + h.dy * r.B.y, (r.Pz + h.dx * r.A.z) + h.dy * r.B.z};
+    // explicit fused multiply-adds (oracle/raster.py restates them: exact product, one rounding)
+    h.p = f3{__builtin_fmaf(h.dx, r.A.x, h.dy * r.B.x), __builtin_fmaf(h.dx, r.A.y, h.dy * r.B.y),
+             __builtin_fmaf(h.dy, r.B.z, __builtin_fmaf(h.dx, r.A.z, r.Pz))};
     const bool ok = h.p.z != 0.0f;
 #if GSTEX_FAST_EVAL
     h.ipz = __builtin_amdgcn_rcpf(h.p.z);
@@ -417,12 +419,12 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
 #endif
     h.u = h.p.x * h.ipz;
     h.v = h.p.y * h.ipz;
-    h.rho3 = h.u * h.u + h.v * h.v;
+    h.rho3 = __builtin_fmaf(h.u, h.u, h.v * h.v);
     float dx = r.x - px, dy = r.y - py;
-    h.rho2 = kFilterInvSq * (dx * dx + dy * dy);
+    h.rho2 = kFilterInvSq * __builtin_fmaf(dx, dx, dy * dy);
     h.use3 = !aa || (h.rho3 <= h.rho2);
     float rho = h.use3 ? h.rho3 : h.rho2;
-    h.z = h.use3 ? (h.u * r.Tw.x + h.v * r.Tw.y) + r.Tw.z : r.Tw.z;
+    h.z = h.use3 ? __builtin_fmaf(h.u, r.Tw.x, __builtin_fmaf(h.v, r.Tw.y, r.Tw.z)) : r.Tw.z;
 #if GSTEX_FAST_EVAL
     h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);  // exp(-rho/2) = 2^(-rho/(2 ln 2))
 #else

@@ -56,6 +56,14 @@ def _div(a, b):
     return a / b
 
 
+def _fma(a, b, c):
+    """fp32 fused multiply-add (a * b + c, one rounding) as raster.hip's __builtin_fmaf: the fp64 product is exact
+    and the fp64 sum's own rounding can change the fp32 result only at a rounding midpoint (p < 2^-28)."""
+    if isinstance(a, torch.Tensor) and a.dtype == F32:
+        return (a.double() * b.double() + (c.double() if isinstance(c, torch.Tensor) else float(c))).float()
+    return a * b + c
+
+
 def _sqrt(a):
     if a.dtype == F32:
         return torch.sqrt(a.double()).float()
@@ -389,10 +397,10 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         A, B, Tw = g["A"][:, None, :], g["B"][:, None, :], g["Tw"][:, None, :]
         ddx = px - g["xa"][:, None]
         ddy = py - g["ya"][:, None]
-        # p = k x l in the affine form of raster.hip eval_hit: dx A + dy B + (0, 0, Pz)
-        pxc = ddx * A[..., 0] + ddy * B[..., 0]
-        pyc = ddx * A[..., 1] + ddy * B[..., 1]
-        pzc = (g["Pz"][:, None] + ddx * A[..., 2]) + ddy * B[..., 2]
+        # p = k x l in the affine form of raster.hip eval_hit: dx A + dy B + (0, 0, Pz), its fused multiply-adds
+        pxc = _fma(ddx, A[..., 0], ddy * B[..., 0])
+        pyc = _fma(ddx, A[..., 1], ddy * B[..., 1])
+        pzc = _fma(ddy, B[..., 2], _fma(ddx, A[..., 2], g["Pz"][:, None]))
         if decisions is None:
             nz = pzc != 0
         else:
@@ -402,16 +410,16 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         ipz = _div(_c(1.0, dtype), pzs)  # raster.hip eval_hit: one reciprocal, two products
         u = pxc * ipz
         v = pyc * ipz
-        rho3 = u * u + v * v
+        rho3 = _fma(u, u, v * v)
         dx = g["xy"][:, None, 0] - px
         dy = g["xy"][:, None, 1] - py
-        rho2 = fis * (dx * dx + dy * dy)
+        rho2 = fis * _fma(dx, dx, dy * dy)
         if decisions is None:
             use3 = (rho3 <= rho2) if aa else torch.ones_like(rho3, dtype=torch.bool)
         else:
             use3 = d["use3"]
         rho = torch.where(use3, rho3, rho2)
-        zz = torch.where(use3, (u * Tw[..., 0] + v * Tw[..., 1]) + Tw[..., 2], Tw[..., 2].expand_as(u))
+        zz = torch.where(use3, _fma(u, Tw[..., 0], _fma(v, Tw[..., 1], Tw[..., 2])), Tw[..., 2].expand_as(u))
         G = torch.exp(-0.5 * rho)
         a_raw = g["opac"][:, None] * G
         if decisions is None:
