@@ -505,8 +505,8 @@ __device__ __forceinline__ void load_texel_quad(__amdgpu_buffer_rsrc_t rs, const
 }
 
 __device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float& tu, float& tv) {
-    tu = r.tu0 + (u * r.auu + v * r.auv);
-    tv = r.tv0 + (u * r.avu + v * r.avv);
+    tu = __builtin_fmaf(u, r.auu, __builtin_fmaf(v, r.auv, r.tu0));  // fused (oracle/raster.py restates it)
+    tv = __builtin_fmaf(u, r.avu, __builtin_fmaf(v, r.avv, r.tv0));
 }
 
 // ------------------------------------------------------------------------------------------

@@ -462,8 +462,8 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         w_ = tdims[ids, 1][:, None]
         off = tdims[ids, 2][:, None]
         has_tex = (h_ * w_) > 0
-        tu = g["tu0"][:, None] + (u * g["auu"][:, None] + v * g["auv"][:, None])
-        tv = g["tv0"][:, None] + (u * g["avu"][:, None] + v * g["avv"][:, None])
+        tu = _fma(u, g["auu"][:, None], _fma(v, g["auv"][:, None], g["tu0"][:, None]))  # raster.hip tex_coords
+        tv = _fma(u, g["avu"][:, None], _fma(v, g["avv"][:, None], g["tv0"][:, None]))
         hf = h_.to(dtype)
         wf = w_.to(dtype)
         xr = tu * hf
