@@ -476,6 +476,27 @@ __device__ __forceinline__ void load_texel_rs(__amdgpu_buffer_rsrc_t rs, int idx
 
 // The 4 bilinear texels of a splat block: byte offsets from one 24-bit multiply-add (v_mul_u32_u24 is
 // full rate; the block index i*w + j < 2^24) plus wave-uniform row/column steps.
+// Forward variant (C = 3): the far corners at i0 + 1 / j0 + 1 without the clamp to the block's edge.  When the
+// coordinate is clamped to the last row / column its weight is exactly 0 (ax = 0 / ay = 0) and the lerp returns
+// the near value bit for bit, so the far texel only has to be finite: one row down past the block reads 0 (buffer
+// range check), one column right reads the next row's first texel.
+__device__ __forceinline__ void load_texel_quad_unclamped(__amdgpu_buffer_rsrc_t rs, const Bilerp& b, int w,
+                                                          float (&t00)[3], float (&t01)[3], float (&t10)[3],
+                                                          float (&t11)[3]) {
+    const int o00 = (int)__umul24(__umul24(b.i0, w) + b.j0, 12u);
+    const int o10 = o00 + w * 12;
+    const auto a = __builtin_amdgcn_raw_buffer_load_b96(rs, o00, 0, 0);
+    const auto c = __builtin_amdgcn_raw_buffer_load_b96(rs, o00 + 12, 0, 0);
+    const auto d = __builtin_amdgcn_raw_buffer_load_b96(rs, o10, 0, 0);
+    const auto e = __builtin_amdgcn_raw_buffer_load_b96(rs, o10 + 12, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        t00[k] = __int_as_float(a[k]);
+        t01[k] = __int_as_float(c[k]);
+        t10[k] = __int_as_float(d[k]);
+        t11[k] = __int_as_float(e[k]);
+    }
+}
 template <int CM>
 __device__ __forceinline__ void load_texel_quad(__amdgpu_buffer_rsrc_t rs, const Bilerp& b, int w, int Cn,
                                                 float (&t00)[CM], float (&t01)[CM], float (&t10)[CM],
@@ -666,8 +687,11 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
                     if (GSTEX_ABLATE & 512) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) p00[c] = p01[c] = p10[c] = p11[c] = __int_as_float(b.i0 + c);
-                    } else
-                    load_texel_quad<CM>(rs, b, r.w, Cn, p00, p01, p10, p11);
+                    } else if constexpr (CM == 3) {
+                        load_texel_quad_unclamped(rs, b, r.w, p00, p01, p10, p11);
+                    } else {
+                        load_texel_quad<CM>(rs, b, r.w, Cn, p00, p01, p10, p11);
+                    }
                     pax = b.ax;
                     pay = b.ay;
                     pw = w;
