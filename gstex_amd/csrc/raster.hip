@@ -1204,7 +1204,14 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
                     b = bilerp_coords(tu, tv, r.h, r.w);
-                    if (!(GSTEX_ABLATE & 8)) load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
+                    // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
+                    // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
+                    if (GSTEX_ABLATE & 8) {
+                    } else if constexpr (CM == 3) {
+                        load_texel_quad_unclamped(rs, b, r.w, t00, t01, t10, t11);
+                    } else {
+                        load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
+                    }
                 }
                 float g = (Gimg[0] * r.rgb[0] + Gimg[1] * r.rgb[1]) + Gimg[2] * r.rgb[2];
                 P[P_RGB + 0] = w * Gimg[0];
