@@ -165,12 +165,20 @@ __global__ __launch_bounds__(256) void count_kernel(int n, const float* __restri
         for (int tx = r.x0; tx < r.x1; ++tx) rank[e++] = atomicAdd(&tile_count[ty * tiles_x + tx], 1);
 }
 
-// 1'. the same count + rank with the tile histogram privatised in LDS: each workgroup ranks its
-// 1024 splats' pairs with LDS atomics, then reserves one global range per touched tile (one global
-// atomic per (workgroup, tile) instead of one per pair: the image centre's tiles receive ~2000 pairs
-// each, which serialised on their counters).  Ranks are scattered positions inside a tile's bucket
-// only; the per-tile sort by (depth, id) makes the final order independent of them.
-constexpr int kCountSplatsPerThread = 4;
+// 1'. the same count + rank with the tile histogram privatised in LDS: each workgroup builds the histogram of its
+// 256 * kCountSplatsPerThread splats' pairs with LDS atomics, reserves one global range per touched tile (one global
+// atomic per (workgroup, tile) instead of one per pair: the image centre's tiles receive ~2000 pairs each, which
+// serialised on their counters), then ranks each pair inside its tile's range with a second LDS atomic.  (The
+// earlier form ranked first and added the range start with a global read-modify-write per pair afterwards: a serial
+// chain of global loads per thread, 45 -> 29 us at cfg3 without it.)  Ranks are scattered positions inside a tile's
+// bucket only; the per-tile sort by (depth, id) makes the final order independent of them.
+#ifndef GSTEX_COUNT_SPT
+#define GSTEX_COUNT_SPT 2  // splats per thread (measured at cfg3: 4 -> 2 saves 5 us, 1 is slower: more range reservations)
+#endif
+constexpr int kCountSplatsPerThread = GSTEX_COUNT_SPT;
+#ifndef GSTEX_COUNT_RESERVE
+#define GSTEX_COUNT_RESERVE 1  // histogram, reserve, then rank (no global read-modify-write of the ranks)
+#endif
 constexpr int kCountLdsTiles = 16384;  // 64 KiB histogram
 
 #ifndef GSTEX_WAVE_PAIRS
@@ -225,11 +233,18 @@ __global__ __launch_bounds__(256) void count_lds_kernel(int n, const float* __re
         if (g < n)
             rr[k] = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
                               tiles_y, block);
+#if GSTEX_COUNT_RESERVE
+        // pass 1: the workgroup's tile histogram (no returned values: the LDS adds pipeline)
+        for (int ty = rr[k].y0; ty < rr[k].y1; ++ty)
+            for (int tx = rr[k].x0; tx < rr[k].x1; ++tx) (void)atomicAdd(&s_hist[ty * tiles_x + tx], 1);
+#else
         int e = g < n ? offsets[g] : 0;
         for (int ty = rr[k].y0; ty < rr[k].y1; ++ty)
             for (int tx = rr[k].x0; tx < rr[k].x1; ++tx) rank[e++] = atomicAdd(&s_hist[ty * tiles_x + tx], 1);
+#endif
     }
     __syncthreads();
+    // one global range per touched tile; s_hist[t] becomes the range's start inside the tile's bucket
     for (int t = threadIdx.x; t < n_tiles; t += 256) {
         const int c = s_hist[t];
         if (c > 0) s_hist[t] = atomicAdd(&tile_count[t], c);
@@ -239,8 +254,15 @@ __global__ __launch_bounds__(256) void count_lds_kernel(int n, const float* __re
     for (int k = 0; k < kCountSplatsPerThread; ++k) {
         const int g = g0 + k * 256;
         int e = g < n ? offsets[g] : 0;
+#if GSTEX_COUNT_RESERVE
+        // pass 2: each pair takes the next position of its tile's range -- one LDS atomic and one store per pair,
+        // no global read of the rank back (the serial per-pair global load was the kernel's latency chain)
+        for (int ty = rr[k].y0; ty < rr[k].y1; ++ty)
+            for (int tx = rr[k].x0; tx < rr[k].x1; ++tx) rank[e++] = atomicAdd(&s_hist[ty * tiles_x + tx], 1);
+#else
         for (int ty = rr[k].y0; ty < rr[k].y1; ++ty)
             for (int tx = rr[k].x0; tx < rr[k].x1; ++tx) rank[e++] += s_hist[ty * tiles_x + tx];
+#endif
     }
 }
 

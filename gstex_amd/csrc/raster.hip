@@ -53,7 +53,7 @@ constexpr int kThreads = kTilePixels;  // 256
 #define GSTEX_STATS 0  // diagnostic builds: count backward work (iterations, culled, active lanes)
 #endif
 #if GSTEX_STATS
-__device__ unsigned long long g_stats[8];
+__device__ unsigned long long g_stats[16];  // [0, 8) backward, [8, 13) forward counters
 extern "C" int gstex_debug_stats(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats)) == hipSuccess ? 0 : 2;
 }
@@ -63,11 +63,16 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 }
 #if GSTEX_STATS == 1
 #define GSTEX_STAT(i, v) do { const unsigned long long v_ = (v); if ((threadIdx.x & 63) == 0) atomicAdd(&g_stats[i], v_); } while (0)
+// the same from the first active lane (divergent code)
+#define GSTEX_STATW(i, v) do { const unsigned long long v_ = (v); \
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_stats[i], v_); } while (0)
 #else
 #define GSTEX_STAT(i, v) do { } while (0)
+#define GSTEX_STATW(i, v) do { } while (0)
 #endif
 #else
 #define GSTEX_STAT(i, v) do { } while (0)
+#define GSTEX_STATW(i, v) do { } while (0)
 #endif
 #ifndef GSTEX_FWD_OCC
 #define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower)
@@ -652,6 +657,8 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
         for (int hb = 0; hb < kFwdBatch / 64; ++hb) {
             const int jj = hb * 64 + lane;
             todo[hb] = __ballot(jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa));
+            GSTEX_STAT(8, (unsigned long long)max(0, min(64, nb - hb * 64)));  // cull candidates (wave, splat)
+            GSTEX_STAT(9, __popcll(todo[hb]));                                 // passing the wave's cull
             // hand the cull to the backward, which visits these splats up to the wave's last contributor
             if (visit_masks && lane == 0 && hb * 64 < nb)
                 visit_masks[(vm_base + ((b0 - rng.x) >> 6) + hb) * 4 + wave] = todo[hb];
@@ -667,6 +674,9 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
                                          : read_rec<kFwdBatch>(s_rec, j);
             Hit h;
             const bool ok = eval_hit(r, px, py, aa, h);
+            GSTEX_STATW(10, 1);                                   // visits (the wave evaluates a splat)
+            GSTEX_STATW(11, __ballot(ok) ? 1 : 0);                // ... with a contributing lane
+            GSTEX_STATW(12, __popcll(__ballot(ok && !(T * (1.0f - h.alpha) < kTMin))));  // contributing lanes
             const float test_T = T * (1.0f - h.alpha);
             const bool stop = ok && test_T < kTMin;
             if (!ok) continue;
