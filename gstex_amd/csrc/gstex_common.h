@@ -323,7 +323,8 @@ __device__ __forceinline__ void affine_homog_vjp(f3 Tu, f3 Tv, f3 Tw, f3 dA, f3 
 enum RecField {
     R_A = 0, R_B = 3, R_PZ = 6, R_TW = 7, R_XY = 10, R_OPAC = 12, R_RGB = 13, R_NRM = 16,
     R_TU0 = 19, R_AUU = 20, R_AUV = 21, R_TV0 = 22, R_AVU = 23, R_AVV = 24,
-    R_H = 25, R_W = 26, R_OFF = 27, R_XA = 28, R_YA = 29  // 30, 31 unused
+    R_H = 25, R_W = 26, R_OFF = 27, R_XA = 28, R_YA = 29,
+    R_HF = 30, R_WF = 31  // (float)h, (float)w: exact, saves the per-visit conversions
 };
 
 // Screen box of the projected disc u^2 + v^2 <= c2 (compute_aabb with a general cutoff).
@@ -394,9 +395,9 @@ constexpr int kPartRowGeo = 32;  // with (27 used)
 // (i/h, j/w), matching texture_dims_to_query, jagged_texture.py:23-34; clamp to edge).
 struct Bilerp { int i0, i1, j0, j1; float ax, ay; bool in_u, in_v; };
 
-__device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w) {
+// hf, wf = (float)h, (float)w (exact), passed in where the caller has them precomputed (raster records)
+__device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w, float hf, float wf) {
     Bilerp b;
-    const float hf = (float)h, wf = (float)w;
     float xr = tu * hf, yr = tv * wf;
     float x = fminf(fmaxf(xr, 0.0f), hf - 1.0f);
     float y = fminf(fmaxf(yr, 0.0f), wf - 1.0f);
@@ -405,9 +406,14 @@ __device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w
     b.i0 = (int)x; b.j0 = (int)y;
     b.i1 = min(b.i0 + 1, h - 1);
     b.j1 = min(b.j0 + 1, w - 1);
-    b.ax = x - (float)b.i0;
-    b.ay = y - (float)b.j0;
+    // x, y >= 0: x - floor(x) is exact and < 1, so v_fract_f32 (S0 - floor(S0)) gives x - (float)i0 bit for bit
+    b.ax = __builtin_amdgcn_fractf(x);
+    b.ay = __builtin_amdgcn_fractf(y);
     return b;
+}
+
+__device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w) {
+    return bilerp_coords(tu, tv, h, w, (float)h, (float)w);
 }
 
 __device__ __forceinline__ float bilerp_mix(float v00, float v01, float v10, float v11, float ax,

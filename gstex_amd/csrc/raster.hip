@@ -184,8 +184,8 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
     r[R_XA] = h.xa;
     r[R_YA] = h.ya;
-    r[30] = 0.0f;
-    r[31] = 0.0f;
+    r[R_HF] = (float)tdims[3 * g];
+    r[R_WF] = (float)tdims[3 * g + 1];
     float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
 #pragma unroll
     for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
@@ -202,10 +202,11 @@ struct Rec {
     float tu0, auu, auv, tv0, avu, avv;
     int h, w, off;
     float xa, ya;
+    float hf, wf;  // (float)h, (float)w
 };
 
 // Record planes (gstex_common.h RecField): A B | B Pz Tw | Tw xy | opac rgb | nrm tu0 | auu auv tv0 avu |
-// avv h w off | xa ya
+// avv h w off | xa ya hf wf
 __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, float4 d, float4 e, float4 f, float4 g,
                                                float4 q) {
     Rec r;
@@ -220,6 +221,7 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.tu0 = e.w; r.auu = f.x; r.auv = f.y; r.tv0 = f.z; r.avu = f.w; r.avv = g.x;
     r.h = __float_as_int(g.y); r.w = __float_as_int(g.z); r.off = __float_as_int(g.w);
     r.xa = q.x; r.ya = q.y;
+    r.hf = q.z; r.wf = q.w;
     return r;
 }
 
@@ -488,8 +490,9 @@ __device__ __forceinline__ void load_texel_rs(__amdgpu_buffer_rsrc_t rs, int idx
 __device__ __forceinline__ void load_texel_quad_unclamped(__amdgpu_buffer_rsrc_t rs, const Bilerp& b, int w,
                                                           float (&t00)[3], float (&t01)[3], float (&t10)[3],
                                                           float (&t11)[3]) {
-    const int o00 = (int)__umul24(__umul24(b.i0, w) + b.j0, 12u);
-    const int o10 = o00 + w * 12;
+    const int rowb = w * 12;  // row stride in bytes (wave-uniform: scalar when w is)
+    const int o00 = (int)(__umul24(b.i0, (unsigned)rowb) + __umul24(b.j0, 12u));
+    const int o10 = o00 + rowb;
     const auto a = __builtin_amdgcn_raw_buffer_load_b96(rs, o00, 0, 0);
     const auto c = __builtin_amdgcn_raw_buffer_load_b96(rs, o00 + 12, 0, 0);
     const auto d = __builtin_amdgcn_raw_buffer_load_b96(rs, o10, 0, 0);
@@ -687,20 +690,24 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
             const float w = h.alpha * T;
             // (a block running past the texel store -- corrupt texture_dims -- contributes no texture)
             if (kDefer) {
-                const bool has_tex = r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && !(GSTEX_ABLATE & 4);
+                // the block's dims are wave-uniform (the record was read from LDS into VGPRs): moved to SGPRs, the
+                // block checks and the texel offsets' row steps become scalar arithmetic
+                const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
+                const int boff = __builtin_amdgcn_readfirstlane(r.off);
+                const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels && !(GSTEX_ABLATE & 4);
                 float tu = 0.f, tv = 0.f;
                 if (has_tex) tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
+                const Bilerp b = bilerp_coords(tu, tv, bh, bw, r.hf, r.wf);
                 fold_pending();  // the previous visit's texels (issued one visit ago) before their registers are reused
                 if (has_tex) {
-                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
+                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
                     if (GSTEX_ABLATE & 512) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) p00[c] = p01[c] = p10[c] = p11[c] = __int_as_float(b.i0 + c);
                     } else if constexpr (CM == 3) {
-                        load_texel_quad_unclamped(rs, b, r.w, p00, p01, p10, p11);
+                        load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
                     } else {
-                        load_texel_quad<CM>(rs, b, r.w, Cn, p00, p01, p10, p11);
+                        load_texel_quad<CM>(rs, b, bw, Cn, p00, p01, p10, p11);
                     }
                     pax = b.ax;
                     pay = b.ay;
@@ -1213,7 +1220,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if (has_tex) {
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
-                    b = bilerp_coords(tu, tv, r.h, r.w);
+                    b = bilerp_coords(tu, tv, r.h, r.w);  // (converting h, w here measured faster than r.hf, r.wf)
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
                     // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
                     if (GSTEX_ABLATE & 8) {
@@ -1727,7 +1734,7 @@ __global__ __launch_bounds__(kThreads) void texture_edit_kernel(
             if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && h.z >= dlo && h.z <= dhi) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp bl = bilerp_coords(tu, tv, r.h, r.w);
+                const Bilerp bl = bilerp_coords(tu, tv, r.h, r.w, r.hf, r.wf);
                 const float wc[4] = {(1.0f - bl.ax) * (1.0f - bl.ay), (1.0f - bl.ax) * bl.ay,
                                      bl.ax * (1.0f - bl.ay), bl.ax * bl.ay};
                 const int tc[4] = {bl.i0 * r.w + bl.j0, bl.i0 * r.w + bl.j1, bl.i1 * r.w + bl.j0, bl.i1 * r.w + bl.j1};
