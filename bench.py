@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-sub", action="store_true", help="skip the cfg1/cfg2/eval/rechart sub-records")
+    p.add_argument("--async-texture", action="store_true",
+                   help="texel Adam update on a side stream, overlapping the next step (measured: no net gain)")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="diagnostics only: no HIP events around the raster launches (no roofline figures)")
@@ -253,7 +255,7 @@ def main():
     scene = make_scene(args.n_splats, args.n_texels, seed=args.seed)
     views = [sphere_view(i, H, W, n_views=N_POSES).to(dev) for i in range(N_POSES)]
     # start_step = 3 x sh_degree_interval: SH at its full degree 3 (the regime of 12k of the 15k iterations)
-    trainer = GStexTrainer(scene, dev, start_step=3000)
+    trainer = GStexTrainer(scene, dev, start_step=3000, async_texture=args.async_texture)
     sync = GradSync(trainer, world) if world > 1 else None
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     gts = [torch.rand((H, W, 3), generator=g).to(dev) for _ in range(N_POSES)]
@@ -412,6 +414,9 @@ def main():
             "sh_degree": trainer.sh_degree_now(), "settings": trainer.settings,
             "geometry_outputs": trainer.geometry_outputs,
             "fold_aabb": True, "texture_transform": "SH2RGB on read (0.28209479, 0.5)",
+            "texture_update": ("side stream: the texel Adam update (zeroing its gradient) overlaps the next step's "
+                               "preprocessing and binning; the raster forward waits for it" if trainer.async_texture
+                               else "compute stream"),
         },
         "roofline": roofline,
         "cpu_baseline": cpu,

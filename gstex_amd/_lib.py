@@ -52,6 +52,8 @@ class GstexAdamTensor(ctypes.Structure):
 
 
 ADAM_MAX_TENSORS = 16
+ADAM_ZERO_GRAD = 1  # GSTEX_ADAM_ZERO_GRAD
+ADAM_GRID_SHIFT = 8  # GSTEX_ADAM_GRID_SHIFT
 _P = c_void_p
 _CAM = POINTER(GstexCamera)
 
@@ -112,6 +114,7 @@ SIGNATURES = {
     "gstex_loss_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, POINTER(c_float), c_float, _P, _P,
                                  _P, _P, _P, c_size_t, _P]),
     "gstex_adam_step": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, _P]),
+    "gstex_adam_step_ex": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32, _P]),
 }
 
 _lib = None

@@ -56,8 +56,10 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     p = p + neg_step * (m / denom);
 }
 
-__global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
-    const int64_t b = blockIdx.x;
+// ZERO_GRAD: the gradient is zeroed after it is read (the next backward accumulates into the same buffer: no separate
+// fill launch, and the zeroing rides along with an update that may run on a side stream)
+template <bool ZERO_GRAD>
+__device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
     int k = 0;
     while (k + 1 < a.n && a.block_start[k + 1] <= b) ++k;
     const gstex_adam_tensor& t = a.t[k];
@@ -92,26 +94,38 @@ __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
                 st_stream(reinterpret_cast<float4*>(t.param + i), p[r]);
                 st_stream(reinterpret_cast<float4*>(t.exp_avg + i), m[r]);
                 st_stream(reinterpret_cast<float4*>(t.exp_avg_sq + i), v[r]);
+                if (ZERO_GRAD) st_stream(reinterpret_cast<float4*>(const_cast<float*>(t.grad) + i), make_float4(0.f, 0.f, 0.f, 0.f));
             } else {
-                for (int64_t e = i; e < t.numel; ++e)
+                for (int64_t e = i; e < t.numel; ++e) {
                     adam_elem(t.param[e], t.grad[e], t.exp_avg[e], t.exp_avg_sq[e], a.one_m_beta1, a.beta2,
                               a.one_m_beta2, a.eps, neg_step, bc2s);
+                    if (ZERO_GRAD) const_cast<float*>(t.grad)[e] = 0.0f;
+                }
             }
         }
     } else {
         for (int e = threadIdx.x; e < kAdamPerBlock; e += kAdamThreads) {
             const int64_t i = base + e;
-            if (i < t.numel)
+            if (i < t.numel) {
                 adam_elem(t.param[i], t.grad[i], t.exp_avg[i], t.exp_avg_sq[i], a.one_m_beta1, a.beta2,
                           a.one_m_beta2, a.eps, neg_step, bc2s);
+                if (ZERO_GRAD) const_cast<float*>(t.grad)[i] = 0.0f;
+            }
         }
     }
 }
 
+// grid-stride over the chunks: a capped grid (GSTEX_ADAM_GRID flags) leaves most of every CU to another stream
+template <bool ZERO_GRAD>
+__global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
+    for (int64_t b = blockIdx.x; b < a.block_start[a.n]; b += gridDim.x) adam_chunk<ZERO_GRAD>(a, b);
+}
+
 }  // namespace
 
-extern "C" int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
-                               double eps, void* stream) {
+namespace {
+int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2, double eps,
+                int32_t flags, void* stream) {
     GSTEX_REQUIRE(n_tensors >= 0 && n_tensors <= kAdamMaxTensors,
                   "gstex_adam_step: n_tensors must be in [0, %d] (got %d)", kAdamMaxTensors, n_tensors);
     GSTEX_REQUIRE(n_tensors == 0 || tensors, "gstex_adam_step: null tensor table");
@@ -137,6 +151,24 @@ extern "C" int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tenso
     a.eps = (float)eps;
     a.one_m_beta1 = (float)(1.0 - beta1);
     a.one_m_beta2 = (float)(1.0 - beta2);
-    adam_kernel<<<(unsigned)blocks, kAdamThreads, 0, gstex::as_stream(stream)>>>(a);
+    const int64_t cap = (flags >> GSTEX_ADAM_GRID_SHIFT) & 0xFFFF;
+    const unsigned grid = (unsigned)(cap > 0 && cap < blocks ? cap : blocks);
+    if (flags & GSTEX_ADAM_ZERO_GRAD)
+        adam_kernel<true><<<grid, kAdamThreads, 0, gstex::as_stream(stream)>>>(a);
+    else
+        adam_kernel<false><<<grid, kAdamThreads, 0, gstex::as_stream(stream)>>>(a);
     return gstex::launch_status("gstex_adam_step");
+}
+}  // namespace
+
+extern "C" int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                               double eps, void* stream) {
+    return adam_launch(n_tensors, tensors, beta1, beta2, eps, 0, stream);
+}
+
+extern "C" int gstex_adam_step_ex(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                                  double eps, int32_t flags, void* stream) {
+    GSTEX_REQUIRE((flags & ~(GSTEX_ADAM_ZERO_GRAD | (0xFFFF << GSTEX_ADAM_GRID_SHIFT))) == 0,
+                  "gstex_adam_step_ex: unknown flags 0x%x", flags);
+    return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, stream);
 }

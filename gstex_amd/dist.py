@@ -62,6 +62,8 @@ class GradSync:
         key = self._layout(params)
         if key == self._key and self.flat is not None:
             return False
+        if self.flat is not None and hasattr(self.trainer, "wait_texture"):
+            self.trainer.wait_texture()  # a side-stream texel update may still read the old buffer
         total = sum(p.numel() for p in params)
         dev = params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
@@ -109,8 +111,14 @@ class GradSync:
     def zero(self):
         if self._work is not None:
             raise RuntimeError("GradSync.zero(): the previous backward's all_reduce() was never called")
-        self.rebuild()
-        self.flat.zero_()
+        if self.rebuild():
+            return  # a new buffer is zero
+        if getattr(self.trainer, "async_texture", False):
+            # the texel slice is zeroed by the trainer's side-stream Adam as it reads it (GSTEX_ADAM_ZERO_GRAD);
+            # filling it here would race that update
+            self.flat[:self._tail_off].zero_()
+        else:
+            self.flat.zero_()
 
     def all_reduce(self):
         """Average the flat gradient buffer over all ranks (the tail's collective may already be running)."""

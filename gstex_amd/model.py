@@ -18,6 +18,7 @@ The rechart every 100 steps (gstex.py:890-914) is provided by `recharge()`.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -104,7 +105,8 @@ class GStexTrainer:
     def __init__(self, scene: Scene, device, sh_degree: int = 3, settings: int = DEFAULT_SETTINGS,
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
-                 sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0):
+                 sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
+                 async_texture: bool = False):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -141,7 +143,34 @@ class GStexTrainer:
         self.texture_grad_sink = None
         self.texture_grad_ready = None
         self.test_colors = None  # eval-render test colours (gstex.py:309)
+        # async_texture (not in the reference; fused Adam on a HIP device): the texel parameter's Adam update (73 % of
+        # the parameters at cfg3) runs on a side stream and zeroes its gradient as it reads it; the next step's
+        # preprocessing and binning overlap it, and only its raster forward waits (texture_gaussians texture_ready).
+        # The gradient lives in a persistent buffer the raster backward accumulates into (texture_grad_sink), so
+        # no per-step zero fill remains.  Anything else reading texture_dc after optimizer_step() must call
+        # wait_texture() first (eval_render and recharge in this class do).
+        self.async_texture = bool(async_texture) and fused_adam and self.device.type == "cuda"
+        self._tex_stream = torch.cuda.Stream(device=d) if self.async_texture else None
+        self._tex_ready = None
+        self._tex_grad = None
+        # the side-stream update's workgroup cap (GSTEX_TEX_ADAM_GRID; 0 = full grid).  Measured at cfg3: no cap, 512,
+        # 256, 128, 64 -- none gains over the compute-stream update
+        self._tex_grid = int(os.environ.get("GSTEX_TEX_ADAM_GRID", "0")) if self.async_texture else 0
+        if self.async_texture:
+            self._own_texture_grad()
         self._build_optimizer()
+
+    def _own_texture_grad(self):
+        # the persistent texel-gradient buffer (replaced by a flat-buffer slice when GradSync takes over)
+        self._tex_grad = torch.zeros_like(self.texture_dc)
+        self.texture_dc.grad = self._tex_grad
+        self.texture_grad_sink = self._tex_grad
+
+    def wait_texture(self):
+        """Order the current stream after the pending side-stream texel update (async_texture)."""
+        if self._tex_ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._tex_ready)
+            self._tex_ready = None
 
     # ------------------------------------------------------------------ parameters
     def param_groups(self):
@@ -204,7 +233,8 @@ class GStexTrainer:
             ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs, texture_grad_sink=self.texture_grad_sink,
-            on_texture_grad=self.texture_grad_ready)
+            on_texture_grad=self.texture_grad_ready, texture_ready=self._tex_ready)
+        self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
@@ -216,6 +246,7 @@ class GStexTrainer:
         """The reference's eval render (get_outputs with extra_stuff, gstex.py:1086-1203): a 6-channel texture
         [SH2RGB(texture_dc), 0, 0, 0] and three raster calls -- the image, the test-colour render with
         thresholded opacities (test_img / uv_im) and the settings | 1 << 15 render (edit_img, clean normals)."""
+        self.wait_texture()
         means = self.means
         quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
             means, self.quats, self.scales, self.opacities, self.mappings, view.c2w[:3, 3])
@@ -279,13 +310,38 @@ class GStexTrainer:
         return StepOutput(loss.detach(), rgb.detach())
 
     def optimizer_step(self):
-        self.optimizer.step()
+        if not self.async_texture:
+            self.optimizer.step()
+            self.step += 1
+            return
+        # the texel update on the side stream, after everything enqueued so far (the backward, and a GradSync
+        # all-reduce of the gradient); the other groups on the current stream
+        main = torch.cuda.current_stream(self.device)
+        self.wait_texture()  # (a step without a render in between)
+        tex = {id(self.texture_dc)}
+        self.optimizer.step(skip=tex)
+        # recorded after the other groups' update: that one runs alone at full bandwidth, and the texel update then
+        # overlaps the next step's latency-bound kernels (preprocessing, binning) instead of contending with it
+        grads_ready = torch.cuda.Event()
+        grads_ready.record(main)
+        self._tex_stream.wait_event(grads_ready)
+        with torch.cuda.stream(self._tex_stream):
+            self.optimizer.step(only=tex, zero_grad=True, grid=self._tex_grid)
+            ev = torch.cuda.Event()
+            ev.record(self._tex_stream)
+        self._tex_ready = ev
         self.step += 1
 
     def zero_grad(self, set_to_none: bool = True):
         """Optimizers.zero_grad_all (engine/optimizers.py): torch's default set_to_none=True, so backward
         writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
-        when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead)."""
+        when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead).  With
+        async_texture the texel gradient buffer is kept (the side-stream Adam zeroes it)."""
+        if self.async_texture:
+            keep = self.texture_dc.grad
+            self.optimizer.zero_grad(set_to_none=set_to_none)
+            self.texture_dc.grad = keep
+            return
         self.optimizer.zero_grad(set_to_none=set_to_none)
 
     # ------------------------------------------------------------------ rechart
@@ -298,6 +354,7 @@ class GStexTrainer:
         The texel store is reused in place while the new charts fit its capacity (jagged_texture.py:45-64:
         adjust_texture_size only ever grows it), so the Parameter, its optimizer entry and any flat gradient
         buffer built over it (gstex_amd.dist.GradSync) stay valid; only a growth replaces the Parameter."""
+        self.wait_texture()
         new_dims, mappings, _ = build_charts(self.scales.detach(), self.pixel_num)
         n_new = int((new_dims[:, 0].long() * new_dims[:, 1].long()).sum())
         ids, uv = texture_dims_to_query(new_dims)
@@ -318,6 +375,8 @@ class GStexTrainer:
                     "exp_avg": torch.zeros_like(self.texture_dc),
                     "exp_avg_sq": torch.zeros_like(self.texture_dc),
                 }
+            if self.async_texture:  # a fresh persistent gradient buffer (GradSync, if any, replaces it at rebuild)
+                self._own_texture_grad()
         else:
             st = self.optimizer.state.get(old)
             if st:

@@ -318,7 +318,8 @@ class _TextureGaussians(torch.autograd.Function):
     def forward(ctx, texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                 block_width, settings, background, texture_transform=None, fold_aabb=False,
-                geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None):
+                geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None,
+                texture_ready=None):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -399,6 +400,8 @@ class _TextureGaussians(torch.autograd.Function):
         if needs_bwd:
             nb = int(_lib.load().gstex_raster_aux_bytes(n_isect, tile_ranges.shape[0], C))
             aux = torch.empty((nb,), device=dev, dtype=torch.uint8)
+        if texture_ready is not None:  # the texels (and the gradient buffer) are updated on another stream
+            torch.cuda.current_stream(dev).wait_event(texture_ready)
         _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
              ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), geo_ptrs[0], geo_ptrs[1], ptr(alpha),
@@ -470,13 +473,14 @@ class _TextureGaussians(torch.autograd.Function):
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
-                      fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None):
+                      fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None,
+                      texture_ready=None):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -497,6 +501,10 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     buffer); autograd then receives no gradient for `texture`, and on_texture_grad() (if given) is called once the
     kernel producing it has been enqueued.
 
+    texture_ready (not in the reference API): a torch.cuda.Event the current stream waits on right before the raster
+    forward -- the texel update of the previous optimizer step running on a side stream (GStexTrainer
+    async_texture), so preprocessing and binning overlap it.
+
     Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
     Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
     uv0 and background; umap/vmap are treated as constants (detached by the caller, gstex.py:977-984).
@@ -509,7 +517,7 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
                                    fold_aabb, geometry_outputs, torch.is_grad_enabled(), texture_grad_sink,
-                                   on_texture_grad)
+                                   on_texture_grad, texture_ready)
 
 
 rasterize_gaussians = texture_gaussians  # north_star name

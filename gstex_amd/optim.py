@@ -20,7 +20,12 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, only=None, skip=None, zero_grad=False, grid=0):
+        """The Adam update.  Extensions (not in torch.optim.Adam): `only` / `skip` (sets of id(param)) restrict the
+        update to / exclude a set of parameters (so one group can be launched on another stream), and `zero_grad` writes zeros over each
+        gradient after reading it (gstex_adam_step_ex, GSTEX_ADAM_ZERO_GRAD); `grid` > 0 caps the launch's
+        workgroups (GSTEX_ADAM_GRID: each loops over the chunks), leaving CUs to another stream.  The launch goes to
+        the current stream."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -30,7 +35,7 @@ class FusedAdam(torch.optim.Optimizer):
         for group in self.param_groups:
             b1, b2 = group["betas"]
             for p in group["params"]:
-                if p.grad is None:
+                if p.grad is None or (only is not None and id(p) not in only) or (skip is not None and id(p) in skip):
                     continue
                 g = p.grad
                 if g.is_sparse:
@@ -58,5 +63,9 @@ class FusedAdam(torch.optim.Optimizer):
             for i in range(0, len(items), _lib.ADAM_MAX_TENSORS):
                 chunk = items[i:i + _lib.ADAM_MAX_TENSORS]
                 arr = (_lib.GstexAdamTensor * len(chunk))(*[d for d, _ in chunk])
-                _lib.call("gstex_adam_step", len(chunk), arr, float(b1), float(b2), float(eps), st)
+                if zero_grad or grid:
+                    flags = (_lib.ADAM_ZERO_GRAD if zero_grad else 0) | ((int(grid) & 0xFFFF) << _lib.ADAM_GRID_SHIFT)
+                    _lib.call("gstex_adam_step_ex", len(chunk), arr, float(b1), float(b2), float(eps), flags, st)
+                else:
+                    _lib.call("gstex_adam_step", len(chunk), arr, float(b1), float(b2), float(eps), st)
         return loss

@@ -266,6 +266,17 @@ typedef struct gstex_adam_tensor {
 } gstex_adam_tensor;
 int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                     double eps, void* stream);
+/* gstex_adam_step with flags: GSTEX_ADAM_ZERO_GRAD also writes zeros over each gradient after reading it (so the
+ * next backward can accumulate into the same buffer without a separate fill; the update may then run on a side
+ * stream, overlapped with the next step's preprocessing).  Not in the reference (torch.optim.Adam + zero_grad). */
+#define GSTEX_ADAM_ZERO_GRAD 1
+/* flags bits 8..23: cap on the launch's workgroups (0 = one per 1024 elements), each looping over the chunks; a
+ * capped grid (e.g. one workgroup per CU) still streams at near full HBM bandwidth while leaving most of every CU's
+ * wave slots to kernels of another stream.  GSTEX_ADAM_GRID(n) builds the field. */
+#define GSTEX_ADAM_GRID_SHIFT 8
+#define GSTEX_ADAM_GRID(n) (((n) & 0xFFFF) << GSTEX_ADAM_GRID_SHIFT)
+int gstex_adam_step_ex(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                       double eps, int32_t flags, void* stream);
 
 #ifdef __cplusplus
 }

@@ -60,3 +60,54 @@ def test_synced_step_matches_unsynced_across_rechart():
             assert err < 1e-5, f"{name}: synced step differs ({err:.2e})"
     finally:
         dist.destroy_process_group()
+
+
+def test_async_texture_update_matches_sync_step():
+    """async_texture: the texel Adam update on a side stream (zeroing its gradient buffer), overlapped with the
+    next step's preprocessing; alone and under GradSync (world 1), across an in-place rechart and an eval render,
+    it must train like the plain step."""
+    from gstex_amd.dist import GradSync
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        sc = make_scene(4000, 80_000, seed=5)
+        views = [sphere_view(i, 96, 96).to(dev) for i in range(3)]
+        g = torch.Generator().manual_seed(1)
+        gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(3)]
+        plain = GStexTrainer(sc, dev, start_step=3000)
+        alone = GStexTrainer(sc, dev, start_step=3000, async_texture=True)
+        synced = GStexTrainer(sc, dev, start_step=3000, async_texture=True)
+        assert alone.async_texture and synced.async_texture
+        sync = GradSync(synced, 1)
+        for step in range(5):
+            for tr in (plain, alone):
+                tr.zero_grad()
+                tr.forward_backward(views[step % 3], gts[step % 3])
+                tr.optimizer_step()
+            sync.zero()
+            synced.forward_backward(views[step % 3], gts[step % 3])
+            sync.all_reduce()
+            synced.optimizer_step()
+            if step == 1:
+                for tr in (plain, alone, synced):
+                    tr.recharge()
+            if step == 2:
+                ev = [tr.eval_render(views[0])["rgb"] for tr in (plain, alone)]
+                assert float((ev[0] - ev[1]).abs().max()) < 1e-4
+        for tr in (alone, synced):
+            tr.wait_texture()
+        torch.cuda.synchronize()
+        # the persistent texel-gradient buffers are left zeroed by the side-stream update
+        assert float(alone.texture_dc.grad.abs().max()) == 0.0
+        assert float(sync.flat[sync._tail_off:].abs().max()) == 0.0
+        for other in (alone, synced):
+            for (name, a), b in zip(plain.param_groups().items(), other.param_groups().values()):
+                a, b = a[0].detach().double(), b[0].detach().double()
+                err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-30)
+                assert err < 1e-5, f"{name}: async texel update differs ({err:.2e})"
+    finally:
+        dist.destroy_process_group()
