@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void count_kernel(int n, const float* __restri
 // atomic per (workgroup, tile) instead of one per pair: the image centre's tiles receive ~2000 pairs each, which
 // serialised on their counters), then ranks each pair inside its tile's range with a second LDS atomic.  (The
 // earlier form ranked first and added the range start with a global read-modify-write per pair afterwards: a serial
-// chain of global loads per thread, 45 -> 29 us at cfg3 without it.)  Ranks are scattered positions inside a tile's
+// chain of global loads per thread, 45 -> 28 us at cfg3 without it.)  Ranks are scattered positions inside a tile's
 // bucket only; the per-tile sort by (depth, id) makes the final order independent of them.
 #ifndef GSTEX_COUNT_SPT
 #define GSTEX_COUNT_SPT 2  // splats per thread (measured at cfg3: 4 -> 2 saves 5 us, 1 is slower: more range reservations)
