@@ -321,10 +321,11 @@ __device__ __forceinline__ void affine_homog_vjp(f3 Tu, f3 Tv, f3 Tw, f3 dA, f3 
 
 // Raster record layout (GSTEX_REC_FLOATS = 32 floats = 128 B, one cache line), as 8 float4 planes.
 enum RecField {
-    R_A = 0, R_B = 3, R_PZ = 6, R_TW = 7, R_XY = 10, R_OPAC = 12, R_RGB = 13, R_NRM = 16,
-    R_TU0 = 19, R_AUU = 20, R_AUV = 21, R_TV0 = 22, R_AVU = 23, R_AVV = 24,
-    R_H = 25, R_W = 26, R_OFF = 27, R_XA = 28, R_YA = 29,
-    R_HF = 30, R_WF = 31  // (float)h, (float)w: exact, saves the per-visit conversions
+    // every field the photometric backward reads lies in [0, 27) (one contiguous scalar load run per visit)
+    R_A = 0, R_B = 3, R_PZ = 6, R_TW = 7, R_XY = 10, R_OPAC = 12, R_RGB = 13,
+    R_TU0 = 16, R_AUU = 17, R_AUV = 18, R_TV0 = 19, R_AVU = 20, R_AVV = 21,
+    R_H = 22, R_W = 23, R_OFF = 24, R_XA = 25, R_YA = 26, R_NRM = 27,
+    R_HF = 30, R_WF = 31  // (float)h, (float)w: exact, saves the forward's per-visit conversions
 };
 
 // Screen box of the projected disc u^2 + v^2 <= c2 (compute_aabb with a general cutoff).

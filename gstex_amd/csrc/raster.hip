@@ -205,8 +205,8 @@ struct Rec {
     float hf, wf;  // (float)h, (float)w
 };
 
-// Record planes (gstex_common.h RecField): A B | B Pz Tw | Tw xy | opac rgb | nrm tu0 | auu auv tv0 avu |
-// avv h w off | xa ya hf wf
+// Record planes (gstex_common.h RecField): A B | B Pz Tw | Tw xy | opac rgb | tu0 auu auv tv0 | avu avv h w |
+// off xa ya nrm | nrm hf wf
 __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, float4 d, float4 e, float4 f, float4 g,
                                                float4 q) {
     Rec r;
@@ -217,10 +217,10 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.x = c.z; r.y = c.w;
     r.opac = d.x;
     r.rgb[0] = d.y; r.rgb[1] = d.z; r.rgb[2] = d.w;
-    r.nrm[0] = e.x; r.nrm[1] = e.y; r.nrm[2] = e.z;
-    r.tu0 = e.w; r.auu = f.x; r.auv = f.y; r.tv0 = f.z; r.avu = f.w; r.avv = g.x;
-    r.h = __float_as_int(g.y); r.w = __float_as_int(g.z); r.off = __float_as_int(g.w);
-    r.xa = q.x; r.ya = q.y;
+    r.tu0 = e.x; r.auu = e.y; r.auv = e.z; r.tv0 = e.w; r.avu = f.x; r.avv = f.y;
+    r.h = __float_as_int(f.z); r.w = __float_as_int(f.w); r.off = __float_as_int(g.x);
+    r.xa = g.y; r.ya = g.z;
+    r.nrm[0] = g.w; r.nrm[1] = q.x; r.nrm[2] = q.y;
     r.hf = q.z; r.wf = q.w;
     return r;
 }
@@ -353,7 +353,7 @@ __device__ __forceinline__ bool conic_edge(float ax, float ay, float az, float q
 template <int NB>
 __device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
                                              bool aa) {
-    const float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], d = s[3 * NB + j], q = s[7 * NB + j];
+    const float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], d = s[3 * NB + j], g = s[6 * NB + j];
     const float opac = d.x;
     if (!(opac * 255.0f > 1.0f)) return false;
     const float rm = 2.0f * logf(255.0f * opac) * 1.01f + 1e-2f;
@@ -362,7 +362,7 @@ __device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, 
         const float ex = c.z - fminf(fmaxf(c.z, x0), x1), ey = c.w - fminf(fmaxf(c.w, y0), y1);
         if (2.0f * (ex * ex + ey * ey) <= rm) return true;
     }
-    const float xa = q.x, ya = q.y;
+    const float xa = g.y, ya = g.z;
     if (xa >= x0 && xa <= x1 && ya >= y0 && ya <= y1) return true;
     if (!GSTEX_CONIC_CULL) return true;
     const float Ax = a.x, Ay = a.y, Az = a.z, Bx = a.w, By = b.x, Bz = b.y, Pz = b.z;
