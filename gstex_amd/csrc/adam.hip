@@ -7,8 +7,9 @@
 //   m = lerp(m, g, 1 - beta1)                      m + (1-beta1) * (g - m)
 //   v = v * beta2 + (1 - beta2) * (g * g)
 //   p = p - step_size * m / (sqrt(v) / sqrt(bc2) + eps),  step_size = lr / bc1
-// with bc1 = 1 - beta1^t, bc2 = 1 - beta2^t computed on the host per tensor (each tensor keeps its
-// own step count: the texel store restarts at t = 1 after every rechart, gstex.py:812-815).
+// with bc1 = 1 - beta1^t, bc2 = 1 - beta2^t computed on the host per tensor (each tensor keeps its own step
+// count; a rechart zeroes the texel store's moments m and v and keeps its step count, like the reference's
+// reshape_in_optim, gstex.py:809-815 -- GStexTrainer.recharge).
 // HBM-bound: 16 B read + 12 B written per element, float4 vectorised, one launch for all tensors; one
 // float4 per thread with nontemporal loads/stores (measured at cfg3: 205 us with 4 cached float4 per
 // thread, 178 us like this = 6.5 TB/s).

@@ -75,86 +75,104 @@ __device__ __forceinline__ Camera load_camera(const CamArgs& a) {
     return c;
 }
 
-struct f3 { float x, y, z; };
+// 3-vectors and the per-splat geometry, templated on the arithmetic type: float for the per-pixel work and the
+// preprocessing kernels, double for the raster's per-splat record (setup) and its backward chain (setup_bwd), whose
+// fp32 rounding was measured to dominate the means / quats gradient error (tools/grad_precision.py).
+template <typename T> struct V3 { T x, y, z; };
+using f3 = V3<float>;
+using d3 = V3<double>;
 
 __device__ __forceinline__ f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
-__device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-__device__ __forceinline__ f3 cross3(f3 a, f3 b) {
-    return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+template <typename T> __device__ __forceinline__ T dot3(V3<T> a, V3<T> b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+template <typename T> __device__ __forceinline__ V3<T> cross3(V3<T> a, V3<T> b) {
+    return V3<T>{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-__device__ __forceinline__ f3 scale3(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
-__device__ __forceinline__ f3 add3(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <typename T> __device__ __forceinline__ V3<T> scale3(V3<T> a, T s) { return V3<T>{a.x * s, a.y * s, a.z * s}; }
+template <typename T> __device__ __forceinline__ V3<T> add3(V3<T> a, V3<T> b) { return V3<T>{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ d3 to_d3(f3 a) { return d3{(double)a.x, (double)a.y, (double)a.z}; }
+__device__ __forceinline__ f3 to_f3(d3 a) { return f3{(float)a.x, (float)a.y, (float)a.z}; }
 
 // Normalised wxyz quaternion -> rotation columns (t_u, t_v, t_w).  Matches
 // nerfstudio/utils/rotations.py:43-72 on unit quaternions (wxyz, real part first).
-struct Frame { f3 tu, tv, tw; float qw, qx, qy, qz, qnorm; };
+template <typename T> struct FrameT { V3<T> tu, tv, tw; T qw, qx, qy, qz, qnorm; };
+using Frame = FrameT<float>;
 
-__device__ __forceinline__ Frame quat_frame(const float* q4) {
-    Frame f;
-    float w = q4[0], x = q4[1], y = q4[2], z = q4[3];
-    float nrm = sqrtf(((w * w + x * x) + y * y) + z * z);
+template <typename T>
+__device__ __forceinline__ FrameT<T> quat_frame_t(const float* q4) {
+    FrameT<T> f;
+    T w = q4[0], x = q4[1], y = q4[2], z = q4[3];
+    T nrm = sqrt(((w * w + x * x) + y * y) + z * z);
     w = w / nrm; x = x / nrm; y = y / nrm; z = z / nrm;
     f.qw = w; f.qx = x; f.qy = y; f.qz = z; f.qnorm = nrm;
-    float r00 = 1.0f - 2.0f * (y * y + z * z);
-    float r01 = 2.0f * (x * y - w * z);
-    float r02 = 2.0f * (x * z + w * y);
-    float r10 = 2.0f * (x * y + w * z);
-    float r11 = 1.0f - 2.0f * (x * x + z * z);
-    float r12 = 2.0f * (y * z - w * x);
-    float r20 = 2.0f * (x * z - w * y);
-    float r21 = 2.0f * (y * z + w * x);
-    float r22 = 1.0f - 2.0f * (x * x + y * y);
-    f.tu = f3{r00, r10, r20};
-    f.tv = f3{r01, r11, r21};
-    f.tw = f3{r02, r12, r22};
+    const T one = 1, two = 2;
+    T r00 = one - two * (y * y + z * z);
+    T r01 = two * (x * y - w * z);
+    T r02 = two * (x * z + w * y);
+    T r10 = two * (x * y + w * z);
+    T r11 = one - two * (x * x + z * z);
+    T r12 = two * (y * z - w * x);
+    T r20 = two * (x * z - w * y);
+    T r21 = two * (y * z + w * x);
+    T r22 = one - two * (x * x + y * y);
+    f.tu = V3<T>{r00, r10, r20};
+    f.tv = V3<T>{r01, r11, r21};
+    f.tw = V3<T>{r02, r12, r22};
     return f;
 }
+__device__ __forceinline__ Frame quat_frame(const float* q4) { return quat_frame_t<float>(q4); }
 
 // Row r of the 3x3 rotation part of the view matrix applied to a vector.
-__device__ __forceinline__ float vrow(const Camera& c, int r, f3 a) {
-    return (c.V[4 * r + 0] * a.x + c.V[4 * r + 1] * a.y) + c.V[4 * r + 2] * a.z;
+template <typename T>
+__device__ __forceinline__ T vrow(const Camera& c, int r, V3<T> a) {
+    return ((T)c.V[4 * r + 0] * a.x + (T)c.V[4 * r + 1] * a.y) + (T)c.V[4 * r + 2] * a.z;
 }
 
 // Splat -> pixel homogeneous matrix M = K [R|t] [[su t_u, sv t_v, mu],[0,0,1]] (rows Tu,Tv,Tw).
-struct Homog { f3 Tu, Tv, Tw; };
+template <typename T> struct HomogT { V3<T> Tu, Tv, Tw; };
+using Homog = HomogT<float>;
 
-__device__ __forceinline__ Homog splat_homography(const Camera& c, f3 mu, float su, float sv,
-                                                  const Frame& fr) {
-    f3 a = scale3(fr.tu, su);
-    f3 b = scale3(fr.tv, sv);
-    float W0[3], W1[3], W2[3];
+template <typename T>
+__device__ __forceinline__ HomogT<T> splat_homography(const Camera& c, V3<T> mu, T su, T sv, const FrameT<T>& fr) {
+    V3<T> a = scale3(fr.tu, su);
+    V3<T> b = scale3(fr.tv, sv);
+    T W0[3], W1[3], W2[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         W0[r] = vrow(c, r, a);
         W1[r] = vrow(c, r, b);
-        W2[r] = vrow(c, r, mu) + c.V[4 * r + 3];
+        W2[r] = vrow(c, r, mu) + (T)c.V[4 * r + 3];
     }
-    Homog h;
-    h.Tu = f3{c.fx * W0[0] + c.cx * W0[2], c.fx * W1[0] + c.cx * W1[2], c.fx * W2[0] + c.cx * W2[2]};
-    h.Tv = f3{c.fy * W0[1] + c.cy * W0[2], c.fy * W1[1] + c.cy * W1[2], c.fy * W2[1] + c.cy * W2[2]};
-    h.Tw = f3{W0[2], W1[2], W2[2]};
+    const T fx = c.fx, fy = c.fy, cx = c.cx, cy = c.cy;
+    HomogT<T> h;
+    h.Tu = V3<T>{fx * W0[0] + cx * W0[2], fx * W1[0] + cx * W1[2], fx * W2[0] + cx * W2[2]};
+    h.Tv = V3<T>{fy * W0[1] + cy * W0[2], fy * W1[1] + cy * W1[2], fy * W2[1] + cy * W2[2]};
+    h.Tw = V3<T>{W0[2], W1[2], W2[2]};
     return h;
 }
 
 // dL/dM -> dL/d(mu, su, sv, t_u, t_v)
-struct HomogGrad { f3 dmu; float dsu, dsv; f3 dtu, dtv; };
+template <typename T> struct HomogGradT { V3<T> dmu; T dsu, dsv; V3<T> dtu, dtv; };
+using HomogGrad = HomogGradT<float>;
 
-__device__ __forceinline__ HomogGrad splat_homography_vjp(const Camera& c, float su, float sv,
-                                                          const Frame& fr, f3 dTu, f3 dTv,
-                                                          f3 dTw) {
+// R_cw^T e (the view matrix's rotation transposed)
+template <typename T>
+__device__ __forceinline__ V3<T> view_rt(const Camera& c, T e0, T e1, T e2) {
+    return V3<T>{((T)c.V[0] * e0 + (T)c.V[4] * e1) + (T)c.V[8] * e2, ((T)c.V[1] * e0 + (T)c.V[5] * e1) + (T)c.V[9] * e2,
+                 ((T)c.V[2] * e0 + (T)c.V[6] * e1) + (T)c.V[10] * e2};
+}
+
+template <typename T>
+__device__ __forceinline__ HomogGradT<T> splat_homography_vjp(const Camera& c, T su, T sv, const FrameT<T>& fr,
+                                                              V3<T> dTu, V3<T> dTv, V3<T> dTw) {
     // W rows: dW[0,:] = fx dTu, dW[1,:] = fy dTv, dW[2,:] = cx dTu + cy dTv + dTw
-    f3 dW0r = scale3(dTu, c.fx);
-    f3 dW1r = scale3(dTv, c.fy);
-    f3 dW2r = add3(add3(scale3(dTu, c.cx), scale3(dTv, c.cy)), dTw);
+    V3<T> dW0r = scale3(dTu, (T)c.fx);
+    V3<T> dW1r = scale3(dTv, (T)c.fy);
+    V3<T> dW2r = add3(add3(scale3(dTu, (T)c.cx), scale3(dTv, (T)c.cy)), dTw);
     // columns of dW: col k = (dW0r[k], dW1r[k], dW2r[k]); d(vec) = R_cw^T col
-    auto rt = [&](float e0, float e1, float e2) {
-        return f3{(c.V[0] * e0 + c.V[4] * e1) + c.V[8] * e2, (c.V[1] * e0 + c.V[5] * e1) + c.V[9] * e2,
-                  (c.V[2] * e0 + c.V[6] * e1) + c.V[10] * e2};
-    };
-    f3 da = rt(dW0r.x, dW1r.x, dW2r.x);
-    f3 db = rt(dW0r.y, dW1r.y, dW2r.y);
-    HomogGrad g;
-    g.dmu = rt(dW0r.z, dW1r.z, dW2r.z);
+    V3<T> da = view_rt(c, dW0r.x, dW1r.x, dW2r.x);
+    V3<T> db = view_rt(c, dW0r.y, dW1r.y, dW2r.y);
+    HomogGradT<T> g;
+    g.dmu = view_rt(c, dW0r.z, dW1r.z, dW2r.z);
     g.dsu = dot3(fr.tu, da);
     g.dsv = dot3(fr.tv, db);
     g.dtu = scale3(da, su);
@@ -169,48 +187,45 @@ __device__ __forceinline__ HomogGrad splat_homography_vjp(const Camera& c, float
 //   Tu' = Tu - xa Tw = fx (W0[0] - xn W0[2], W1[0] - xn W1[2], 0),   xn = W2[0] / W2[2]
 //   Tv' = Tv - ya Tw = fy (W0[1] - yn W0[2], W1[1] - yn W1[2], 0),   yn = W2[1] / W2[2]
 //   xa = fx xn + cx,  ya = fy yn + cy
-struct Anchored { f3 Tu, Tv, Tw; float xn, yn, xa, ya; };
+template <typename T> struct AnchoredT { V3<T> Tu, Tv, Tw; T xn, yn, xa, ya; };
 
-__device__ __forceinline__ Anchored splat_anchored(const Camera& c, f3 mu, float su, float sv,
-                                                   const Frame& fr) {
-    f3 a = scale3(fr.tu, su);
-    f3 b = scale3(fr.tv, sv);
-    float W0[3], W1[3], W2[3];
+template <typename T>
+__device__ __forceinline__ AnchoredT<T> splat_anchored(const Camera& c, V3<T> mu, T su, T sv, const FrameT<T>& fr) {
+    V3<T> a = scale3(fr.tu, su);
+    V3<T> b = scale3(fr.tv, sv);
+    T W0[3], W1[3], W2[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         W0[r] = vrow(c, r, a);
         W1[r] = vrow(c, r, b);
-        W2[r] = vrow(c, r, mu) + c.V[4 * r + 3];
+        W2[r] = vrow(c, r, mu) + (T)c.V[4 * r + 3];
     }
-    Anchored h;
+    const T fx = c.fx, fy = c.fy, cx = c.cx, cy = c.cy;
+    AnchoredT<T> h;
     h.xn = W2[0] / W2[2];
     h.yn = W2[1] / W2[2];
-    h.Tu = f3{c.fx * (W0[0] - h.xn * W0[2]), c.fx * (W1[0] - h.xn * W1[2]), 0.0f};
-    h.Tv = f3{c.fy * (W0[1] - h.yn * W0[2]), c.fy * (W1[1] - h.yn * W1[2]), 0.0f};
-    h.Tw = f3{W0[2], W1[2], W2[2]};
-    h.xa = c.fx * h.xn + c.cx;
-    h.ya = c.fy * h.yn + c.cy;
+    h.Tu = V3<T>{fx * (W0[0] - h.xn * W0[2]), fx * (W1[0] - h.xn * W1[2]), (T)0};
+    h.Tv = V3<T>{fy * (W0[1] - h.yn * W0[2]), fy * (W1[1] - h.yn * W1[2]), (T)0};
+    h.Tw = V3<T>{W0[2], W1[2], W2[2]};
+    h.xa = fx * h.xn + cx;
+    h.ya = fy * h.yn + cy;
     return h;
 }
 
 // Gradient of the anchored form w.r.t. (mu, su, sv, t_u, t_v), treating the anchor as a constant
 // (k and l do not depend on it).  A = dL/dTu, B = dL/dTv, Pw = dL/dTw accumulated with the
 // anchored pixel offsets:  dW[0,:] = fx A,  dW[1,:] = fy B,  dW[2,:] = Pw - xn dW[0,:] - yn dW[1,:].
-__device__ __forceinline__ HomogGrad splat_anchored_vjp(const Camera& c, float su, float sv,
-                                                        const Frame& fr, float xn, float yn, f3 A,
-                                                        f3 B, f3 Pw) {
-    f3 dW0r = scale3(A, c.fx);
-    f3 dW1r = scale3(B, c.fy);
-    f3 dW2r = f3{(Pw.x - xn * dW0r.x) - yn * dW1r.x, (Pw.y - xn * dW0r.y) - yn * dW1r.y,
-                 (Pw.z - xn * dW0r.z) - yn * dW1r.z};
-    auto rt = [&](float e0, float e1, float e2) {
-        return f3{(c.V[0] * e0 + c.V[4] * e1) + c.V[8] * e2, (c.V[1] * e0 + c.V[5] * e1) + c.V[9] * e2,
-                  (c.V[2] * e0 + c.V[6] * e1) + c.V[10] * e2};
-    };
-    f3 da = rt(dW0r.x, dW1r.x, dW2r.x);
-    f3 db = rt(dW0r.y, dW1r.y, dW2r.y);
-    HomogGrad g;
-    g.dmu = rt(dW0r.z, dW1r.z, dW2r.z);
+template <typename T>
+__device__ __forceinline__ HomogGradT<T> splat_anchored_vjp(const Camera& c, T su, T sv, const FrameT<T>& fr, T xn,
+                                                            T yn, V3<T> A, V3<T> B, V3<T> Pw) {
+    V3<T> dW0r = scale3(A, (T)c.fx);
+    V3<T> dW1r = scale3(B, (T)c.fy);
+    V3<T> dW2r = V3<T>{(Pw.x - xn * dW0r.x) - yn * dW1r.x, (Pw.y - xn * dW0r.y) - yn * dW1r.y,
+                       (Pw.z - xn * dW0r.z) - yn * dW1r.z};
+    V3<T> da = view_rt(c, dW0r.x, dW1r.x, dW2r.x);
+    V3<T> db = view_rt(c, dW0r.y, dW1r.y, dW2r.y);
+    HomogGradT<T> g;
+    g.dmu = view_rt(c, dW0r.z, dW1r.z, dW2r.z);
     g.dsu = dot3(fr.tu, da);
     g.dsv = dot3(fr.tv, db);
     g.dtu = scale3(da, su);
@@ -219,21 +234,20 @@ __device__ __forceinline__ HomogGrad splat_anchored_vjp(const Camera& c, float s
 }
 
 // dL/d(rotation columns) -> dL/d(raw quaternion), through the normalisation.
-__device__ __forceinline__ void frame_vjp(const Frame& f, f3 dtu, f3 dtv, f3 dtw, float* dq) {
-    const float w = f.qw, x = f.qx, y = f.qy, z = f.qz;
+template <typename T>
+__device__ __forceinline__ void frame_vjp(const FrameT<T>& f, V3<T> dtu, V3<T> dtv, V3<T> dtw, T* dq) {
+    const T w = f.qw, x = f.qx, y = f.qy, z = f.qz;
+    const T two = 2;
     // R[r][c]: column c = (tu, tv, tw)[c], row r = component
-    const float d00 = dtu.x, d10 = dtu.y, d20 = dtu.z;
-    const float d01 = dtv.x, d11 = dtv.y, d21 = dtv.z;
-    const float d02 = dtw.x, d12 = dtw.y, d22 = dtw.z;
-    float gw = 2.0f * (-z * d01 + y * d02 + z * d10 - x * d12 - y * d20 + x * d21);
-    float gx = 2.0f * (y * d01 + z * d02 + y * d10 - 2.0f * x * d11 - w * d12 + z * d20 + w * d21 -
-                       2.0f * x * d22);
-    float gy = 2.0f * (-2.0f * y * d00 + x * d01 + w * d02 + x * d10 + z * d12 - w * d20 + z * d21 -
-                       2.0f * y * d22);
-    float gz = 2.0f * (-2.0f * z * d00 - w * d01 + x * d02 + w * d10 - 2.0f * z * d11 + y * d12 +
-                       x * d20 + y * d21);
-    float proj = ((w * gw + x * gx) + y * gy) + z * gz;
-    float inv = 1.0f / f.qnorm;
+    const T d00 = dtu.x, d10 = dtu.y, d20 = dtu.z;
+    const T d01 = dtv.x, d11 = dtv.y, d21 = dtv.z;
+    const T d02 = dtw.x, d12 = dtw.y, d22 = dtw.z;
+    T gw = two * (-z * d01 + y * d02 + z * d10 - x * d12 - y * d20 + x * d21);
+    T gx = two * (y * d01 + z * d02 + y * d10 - two * x * d11 - w * d12 + z * d20 + w * d21 - two * x * d22);
+    T gy = two * (-two * y * d00 + x * d01 + w * d02 + x * d10 + z * d12 - w * d20 + z * d21 - two * y * d22);
+    T gz = two * (-two * z * d00 - w * d01 + x * d02 + w * d10 - two * z * d11 + y * d12 + x * d20 + y * d21);
+    T proj = ((w * gw + x * gx) + y * gy) + z * gz;
+    T inv = (T)1 / f.qnorm;
     dq[0] = (gw - w * proj) * inv;
     dq[1] = (gx - x * proj) * inv;
     dq[2] = (gy - y * proj) * inv;
@@ -302,18 +316,20 @@ __device__ __forceinline__ Rect tile_rect(float cx, float cy, float ex, float ey
 //   p = d.x A + d.y B + P0,   A = Tv' x Tw,  B = Tw x Tu',  P0 = Tu' x Tv' = (0, 0, Pz)
 // (the d.x d.y Tw x Tw term vanishes).  The raster evaluates p this way: 6 products instead of 2 x 3 + 6, and no
 // per-pixel cancellation of the d.x d.y terms.
-struct AffineHomog { f3 A, B; float Pz; };
-__device__ __forceinline__ AffineHomog affine_homog(f3 Tu, f3 Tv, f3 Tw) {  // Tu.z = Tv.z = 0 (anchored)
-    AffineHomog a;
-    a.A = f3{Tw.z * Tv.y, -(Tw.z * Tv.x), Tw.y * Tv.x - Tw.x * Tv.y};
-    a.B = f3{-(Tu.y * Tw.z), Tu.x * Tw.z, Tu.y * Tw.x - Tu.x * Tw.y};
+template <typename T> struct AffineHomogT { V3<T> A, B; T Pz; };
+template <typename T>
+__device__ __forceinline__ AffineHomogT<T> affine_homog(V3<T> Tu, V3<T> Tv, V3<T> Tw) {  // Tu.z = Tv.z = 0 (anchored)
+    AffineHomogT<T> a;
+    a.A = V3<T>{Tw.z * Tv.y, -(Tw.z * Tv.x), Tw.y * Tv.x - Tw.x * Tv.y};
+    a.B = V3<T>{-(Tu.y * Tw.z), Tu.x * Tw.z, Tu.y * Tw.x - Tu.x * Tw.y};
     a.Pz = Tu.x * Tv.y - Tu.y * Tv.x;
     return a;
 }
 // dL/d(A, B, P0) -> dL/d(Tu', Tv', Tw) (c = a x b: dL/da = b x dL/dc, dL/db = dL/dc x a), including the
 // gradients of the z-components of Tu', Tv' (zero-valued, but the anchored vjp holds the anchor fixed)
-__device__ __forceinline__ void affine_homog_vjp(f3 Tu, f3 Tv, f3 Tw, f3 dA, f3 dB, f3 dP0, f3& dTu, f3& dTv,
-                                                 f3& dTw) {
+template <typename T>
+__device__ __forceinline__ void affine_homog_vjp(V3<T> Tu, V3<T> Tv, V3<T> Tw, V3<T> dA, V3<T> dB, V3<T> dP0,
+                                                 V3<T>& dTu, V3<T>& dTv, V3<T>& dTw) {
     dTu = add3(cross3(dB, Tw), cross3(Tv, dP0));
     dTv = add3(cross3(Tw, dA), cross3(dP0, Tu));
     dTw = add3(cross3(dA, Tv), cross3(Tu, dB));

@@ -155,35 +155,37 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     if (nth[g] <= 0) return;
-    Frame fr = quat_frame(quats + 4 * g);
-    float su = scales[3 * g] * glob, sv = scales[3 * g + 1] * glob;
-    f3 mu = mk3(means[3 * g], means[3 * g + 1], means[3 * g + 2]);
-    Anchored h = splat_anchored(cam, mu, su, sv, fr);
-    f3 dir = f3{cam.campos[0] - mu.x, cam.campos[1] - mu.y, cam.campos[2] - mu.z};
-    float sgn = dot3(fr.tw, dir) < 0.0f ? -1.0f : 1.0f;
-    f3 um = mk3(umap[3 * g], umap[3 * g + 1], umap[3 * g + 2]);
-    f3 vm = mk3(vmap[3 * g], vmap[3 * g + 1], vmap[3 * g + 2]);
+    // the record is evaluated in fp64 and rounded once per value (one thread per splat, ~100 fp64 operations): its
+    // fp32 evaluation was the dominant error of the means / quats gradients (tools/grad_precision.py)
+    const FrameT<double> fr = quat_frame_t<double>(quats + 4 * g);
+    const double su = (double)scales[3 * g] * (double)glob, sv = (double)scales[3 * g + 1] * (double)glob;
+    const d3 mu = d3{(double)means[3 * g], (double)means[3 * g + 1], (double)means[3 * g + 2]};
+    const AnchoredT<double> h = splat_anchored(cam, mu, su, sv, fr);
+    const d3 dir = d3{(double)cam.campos[0] - mu.x, (double)cam.campos[1] - mu.y, (double)cam.campos[2] - mu.z};
+    const double sgn = dot3(fr.tw, dir) < 0.0 ? -1.0 : 1.0;
+    const d3 um = d3{(double)umap[3 * g], (double)umap[3 * g + 1], (double)umap[3 * g + 2]};
+    const d3 vm = d3{(double)vmap[3 * g], (double)vmap[3 * g + 1], (double)vmap[3 * g + 2]};
     float r[GSTEX_REC_FLOATS];
-    const AffineHomog ah = affine_homog(h.Tu, h.Tv, h.Tw);
-    r[R_A + 0] = ah.A.x; r[R_A + 1] = ah.A.y; r[R_A + 2] = ah.A.z;
-    r[R_B + 0] = ah.B.x; r[R_B + 1] = ah.B.y; r[R_B + 2] = ah.B.z;
-    r[R_PZ] = ah.Pz;
-    r[R_TW + 0] = h.Tw.x; r[R_TW + 1] = h.Tw.y; r[R_TW + 2] = h.Tw.z;
+    const AffineHomogT<double> ah = affine_homog(h.Tu, h.Tv, h.Tw);
+    r[R_A + 0] = (float)ah.A.x; r[R_A + 1] = (float)ah.A.y; r[R_A + 2] = (float)ah.A.z;
+    r[R_B + 0] = (float)ah.B.x; r[R_B + 1] = (float)ah.B.y; r[R_B + 2] = (float)ah.B.z;
+    r[R_PZ] = (float)ah.Pz;
+    r[R_TW + 0] = (float)h.Tw.x; r[R_TW + 1] = (float)h.Tw.y; r[R_TW + 2] = (float)h.Tw.z;
     r[R_XY + 0] = centers[2 * g]; r[R_XY + 1] = centers[2 * g + 1];
     r[R_OPAC] = opacities[g];
     r[R_RGB + 0] = rgbs[3 * g]; r[R_RGB + 1] = rgbs[3 * g + 1]; r[R_RGB + 2] = rgbs[3 * g + 2];
-    r[R_NRM + 0] = sgn * fr.tw.x; r[R_NRM + 1] = sgn * fr.tw.y; r[R_NRM + 2] = sgn * fr.tw.z;
+    r[R_NRM + 0] = (float)(sgn * fr.tw.x); r[R_NRM + 1] = (float)(sgn * fr.tw.y); r[R_NRM + 2] = (float)(sgn * fr.tw.z);
     r[R_TU0] = uv0[2 * g];
-    r[R_AUU] = su * dot3(fr.tu, um);
-    r[R_AUV] = sv * dot3(fr.tv, um);
+    r[R_AUU] = (float)(su * dot3(fr.tu, um));
+    r[R_AUV] = (float)(sv * dot3(fr.tv, um));
     r[R_TV0] = uv0[2 * g + 1];
-    r[R_AVU] = su * dot3(fr.tu, vm);
-    r[R_AVV] = sv * dot3(fr.tv, vm);
+    r[R_AVU] = (float)(su * dot3(fr.tu, vm));
+    r[R_AVV] = (float)(sv * dot3(fr.tv, vm));
     r[R_H] = __int_as_float(tdims[3 * g]);
     r[R_W] = __int_as_float(tdims[3 * g + 1]);
     r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
-    r[R_XA] = h.xa;
-    r[R_YA] = h.ya;
+    r[R_XA] = (float)h.xa;
+    r[R_YA] = (float)h.ya;
     r[R_HF] = (float)tdims[3 * g];
     r[R_WF] = (float)tdims[3 * g + 1];
     float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
@@ -524,6 +526,24 @@ __device__ __forceinline__ void load_texel_quad(__amdgpu_buffer_rsrc_t rs, const
             t01[k] = __int_as_float(c[k]);
             t10[k] = __int_as_float(d[k]);
             t11[k] = __int_as_float(e[k]);
+        }
+    } else if constexpr (CM == 6) {
+        // the eval render's 6 channels: two 12-B loads per corner (24 B contiguous per texel) instead of six dwords
+        const int o00 = (int)__umul24(__umul24(b.i0, w) + b.j0, 24u);
+        const int o01 = b.j1 > b.j0 ? o00 + 24 : o00;
+        const int o10 = b.i1 > b.i0 ? o00 + w * 24 : o00;
+        const int o11 = b.j1 > b.j0 ? o10 + 24 : o10;
+        const int off[4] = {o00, o01, o10, o11};
+        float (*dst[4])[CM] = {&t00, &t01, &t10, &t11};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const auto lo = __builtin_amdgcn_raw_buffer_load_b96(rs, off[q], 0, 0);
+            const auto hi = __builtin_amdgcn_raw_buffer_load_b96(rs, off[q] + 12, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                (*dst[q])[k] = __int_as_float(lo[k]);
+                (*dst[q])[3 + k] = __int_as_float(hi[k]);
+            }
         }
     } else {
         load_texel_rs<CM>(rs, b.i0 * w + b.j0, Cn, t00);
@@ -1187,6 +1207,9 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
             GSTEX_STAT(1, 1);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
+            GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
+            GSTEX_STAT(14, __popcll(__ballot(contrib)) <= 16 ? 1 : 0);  // sparse visits
+            GSTEX_STAT(15, __popcll(__ballot(contrib)) >= 48 ? 1 : 0);  // dense visits
             constexpr int NP = GEO ? kPartRowGeo : kPartRow;
             // a spare slot of the row (zero when stored): the texel fixed-point bound
             constexpr int kMBound = GEO ? 27 : P_NRM;
@@ -1620,41 +1643,46 @@ __device__ __forceinline__ void setup_bwd_chain(int g, const float (&S)[kPartRow
         v_quats[4 * g] = v_quats[4 * g + 1] = v_quats[4 * g + 2] = v_quats[4 * g + 3] = 0.f;
         return;
     }
-    Frame fr = quat_frame(quats + 4 * g);
-    const float su = scales[3 * g] * glob, sv = scales[3 * g + 1] * glob;
-    f3 mu = mk3(means[3 * g], means[3 * g + 1], means[3 * g + 2]);
-    const Anchored an = splat_anchored(cam, mu, su, sv, fr);
-    f3 dTu, dTv, dTw;
-    affine_homog_vjp(an.Tu, an.Tv, an.Tw, f3{S[P_A], S[P_A + 1], S[P_A + 2]}, f3{S[P_B], S[P_B + 1], S[P_B + 2]},
-                     f3{S[P_P0], S[P_P0 + 1], S[P_P0 + 2]}, dTu, dTv, dTw);
-    dTw = add3(dTw, f3{S[P_TW], S[P_TW + 1], S[P_TW + 2]});
-    HomogGrad hg = splat_anchored_vjp(cam, su, sv, fr, an.xn, an.yn, dTu, dTv, dTw);
-    const f3 um = mk3(umap[3 * g], umap[3 * g + 1], umap[3 * g + 2]);
-    const f3 vm = mk3(vmap[3 * g], vmap[3 * g + 1], vmap[3 * g + 2]);
-    const float dauu = S[P_AUU], dauv = S[P_AUV], davu = S[P_AVU], davv = S[P_AVV];
-    float dsu = hg.dsu + dauu * dot3(fr.tu, um) + davu * dot3(fr.tu, vm);
-    float dsv = hg.dsv + dauv * dot3(fr.tv, um) + davv * dot3(fr.tv, vm);
-    f3 dtu = add3(hg.dtu, add3(scale3(um, dauu * su), scale3(vm, davu * su)));
-    f3 dtv = add3(hg.dtv, add3(scale3(um, dauv * sv), scale3(vm, davv * sv)));
-    f3 dir = f3{cam.campos[0] - mu.x, cam.campos[1] - mu.y, cam.campos[2] - mu.z};
-    const float sgn = dot3(fr.tw, dir) < 0.0f ? -1.0f : 1.0f;
-    f3 dtw = f3{sgn * S[P_NRM], sgn * S[P_NRM + 1], sgn * S[P_NRM + 2]};
-    float dq[4];
-    frame_vjp(fr, dtu, dtv, dtw, dq);
-    f3 vmu = hg.dmu;
-    float vsu = dsu * glob, vsv = dsv * glob;
+    // fp64 chain (one thread per splat): the record it differentiates was evaluated in fp64 (setup_kernel)
+    const FrameT<double> fr = quat_frame_t<double>(quats + 4 * g);
+    const double su = (double)scales[3 * g] * (double)glob, sv = (double)scales[3 * g + 1] * (double)glob;
+    const d3 mu = d3{(double)means[3 * g], (double)means[3 * g + 1], (double)means[3 * g + 2]};
+    const AnchoredT<double> an = splat_anchored(cam, mu, su, sv, fr);
+    d3 dTu, dTv, dTw;
+    auto sd = [&](int i) { return d3{(double)S[i], (double)S[i + 1], (double)S[i + 2]}; };
+    affine_homog_vjp(an.Tu, an.Tv, an.Tw, sd(P_A), sd(P_B), sd(P_P0), dTu, dTv, dTw);
+    dTw = add3(dTw, sd(P_TW));
+    const HomogGradT<double> hg = splat_anchored_vjp(cam, su, sv, fr, an.xn, an.yn, dTu, dTv, dTw);
+    const d3 um = d3{(double)umap[3 * g], (double)umap[3 * g + 1], (double)umap[3 * g + 2]};
+    const d3 vm = d3{(double)vmap[3 * g], (double)vmap[3 * g + 1], (double)vmap[3 * g + 2]};
+    const double dauu = S[P_AUU], dauv = S[P_AUV], davu = S[P_AVU], davv = S[P_AVV];
+    const double dsu = hg.dsu + dauu * dot3(fr.tu, um) + davu * dot3(fr.tu, vm);
+    const double dsv = hg.dsv + dauv * dot3(fr.tv, um) + davv * dot3(fr.tv, vm);
+    const d3 dtu = add3(hg.dtu, add3(scale3(um, dauu * su), scale3(vm, davu * su)));
+    const d3 dtv = add3(hg.dtv, add3(scale3(um, dauv * sv), scale3(vm, davv * sv)));
+    const d3 dir = d3{(double)cam.campos[0] - mu.x, (double)cam.campos[1] - mu.y, (double)cam.campos[2] - mu.z};
+    const double sgn = dot3(fr.tw, dir) < 0.0 ? -1.0 : 1.0;
+    const d3 dtw = d3{sgn * S[P_NRM], sgn * S[P_NRM + 1], sgn * S[P_NRM + 2]};
+    double dqd[4];
+    frame_vjp(fr, dtu, dtv, dtw, dqd);
+    // rounded to fp32 once; the folded AABB-centre chain below stays fp32 (bit-identical to get_aabb_2d's backward)
+    f3 vmu = to_f3(hg.dmu);
+    float vsu = (float)(dsu * (double)glob), vsv = (float)(dsv * (double)glob);
+    float dq[4] = {(float)dqd[0], (float)dqd[1], (float)dqd[2], (float)dqd[3]};
     if (FOLD_AABB) {
         // aabb_bwd_kernel for this splat (zero when there is no centre gradient or the splat is culled)
         f3 amu = f3{0.f, 0.f, 0.f};
         float asu = 0.f, asv = 0.f, aq[4] = {0.f, 0.f, 0.f, 0.f};
         const float gcx = S[P_XY + 0], gcy = S[P_XY + 1];
         float acx, acy, aex, aey;
-        const Homog ah = splat_homography(cam, mu, su, sv, fr);
+        const Frame frf = quat_frame(quats + 4 * g);
+        const float suf = scales[3 * g] * glob, svf = scales[3 * g + 1] * glob;
+        const Homog ah = splat_homography(cam, mk3(means[3 * g], means[3 * g + 1], means[3 * g + 2]), suf, svf, frf);
         if (!(gcx == 0.0f && gcy == 0.0f) && aabb_from_homog(ah, acx, acy, aex, aey)) {
             f3 dTu, dTv, dTw;
             aabb_centre_vjp(ah, acx, acy, gcx, gcy, dTu, dTv, dTw);
-            const HomogGrad ag = splat_homography_vjp(cam, su, sv, fr, dTu, dTv, dTw);
-            frame_vjp(fr, ag.dtu, ag.dtv, f3{0.0f, 0.0f, 0.0f}, aq);
+            const HomogGrad ag = splat_homography_vjp(cam, suf, svf, frf, dTu, dTv, dTw);
+            frame_vjp(frf, ag.dtu, ag.dtv, f3{0.0f, 0.0f, 0.0f}, aq);
             amu = ag.dmu;
             asu = ag.dsu * glob;
             asv = ag.dsv * glob;

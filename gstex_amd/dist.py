@@ -95,9 +95,12 @@ class GradSync:
 
     def _tail_ready_sink(self):
         # the raster backward has just been enqueued on the compute stream: the collective is stream-ordered
-        # after it and overlaps the rest of the backward
-        if self._work is None:
-            self._start_tail()
+        # after it and overlaps the rest of the backward.  A second backward before all_reduce() would add into the
+        # slice the in-flight collective is reading: refused (one backward per all_reduce(), class docstring)
+        if self._work is not None:
+            raise RuntimeError("GradSync: a second backward before all_reduce() (its texel gradient would race the "
+                               "collective still reading the flat buffer)")
+        self._start_tail()
 
     def _tail_ready(self, param):
         # fires once the texel gradient is final for this backward; the view is still the flat buffer's
@@ -121,17 +124,51 @@ class GradSync:
             self.flat.zero_()
 
     def all_reduce(self):
-        """Average the flat gradient buffer over all ranks (the tail's collective may already be running)."""
+        """Average the flat gradient buffer over all ranks (the tail's collective may already be running).
+
+        Every .grad must still be its view of the buffer: a zero_grad(set_to_none=True) after zero() (trainer or
+        optimizer) lets autograd write fresh tensors, which are folded back into the buffer here (a parameter whose
+        .grad is None took no gradient; the texel store's slice keeps what the raster backward wrote into it)."""
         work, self._work = self._work, None
-        if work is not None and self._layout(self._params()) == self._key:
-            dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
-            work.wait()
-        else:
+        params = self._params()
+        if self._layout(params) != self._key:
             if work is not None:
                 work.wait()
+                raise RuntimeError("GradSync.all_reduce(): the parameters changed between backward and all_reduce() "
+                                   "(call zero() after a rechart, before the backward)")
             self.rebuild_if_detached()
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            # the tail is the texel store: with a running collective its slice is final (written by the kernel)
+            self._reattach(params, skip_tail=work is not None)
+            if work is not None:
+                dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
+                work.wait()
+            else:
+                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
+
+    def _reattach(self, params, skip_tail=False):
+        """Point every .grad back at its slice of `flat`, copying a detached gradient in (None: zero, except the
+        texel store's slice when the raster backward accumulated straight into it -- the sink)."""
+        off = 0
+        last = len(params) - 1
+        for i, p in enumerate(params):
+            n = p.numel()
+            view = self.flat[off:off + n]
+            off += n
+            if p.grad is not None and p.grad.data_ptr() == view.data_ptr():
+                continue
+            g = p.grad
+            p.grad = view.view_as(p)
+            if i == last and (skip_tail or self._sink):
+                if g is not None and g.data_ptr() != view.data_ptr():
+                    p.grad.add_(g)  # an autograd gradient on top of the sink's accumulation (none in GStexTrainer)
+                continue
+            if g is not None:
+                p.grad.copy_(g)
+            else:
+                p.grad.zero_()
 
     def rebuild_if_detached(self):
         # autograd may have replaced a .grad that was not a view of `flat` (e.g. first step after

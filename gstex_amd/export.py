@@ -18,6 +18,8 @@ NPZ_KEYS = ("xyz", "features_rest", "opacity", "scaling", "rotation", "texture_d
 
 
 def export_npz(trainer, path) -> None:
+    if hasattr(trainer, "wait_texture"):  # async_texture: the side-stream texel update must land before the read
+        trainer.wait_texture()
     params = {
         "xyz": trainer.means,
         "features_rest": trainer.features_rest,

@@ -172,6 +172,12 @@ class GStexTrainer:
             torch.cuda.current_stream(self.device).wait_event(self._tex_ready)
             self._tex_ready = None
 
+    def texels(self) -> torch.Tensor:
+        """The texel store (SH-DC values) for readers outside the step (export, average_colors, viewers): waits for a
+        pending side-stream update first (async_texture), so no reader depends on remembering wait_texture()."""
+        self.wait_texture()
+        return self.texture_dc.detach()
+
     # ------------------------------------------------------------------ parameters
     def param_groups(self):
         return {

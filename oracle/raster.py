@@ -297,8 +297,17 @@ class RasterInputs:
     background: torch.Tensor | None = None  # (3,)
 
 
+# raster.hip setup_kernel evaluates the per-splat record in fp64 and rounds each value to fp32 once (and
+# setup_bwd_chain differentiates it in fp64): the fp32 evaluation of the record was measured to dominate the
+# means / quats gradient error (tools/grad_precision.py).  False restores the all-fp32 record
+# (precision analysis only).
+RECORD_FP64 = True
+
+
 def _splat_table(inp: RasterInputs, dtype):
-    """gstex_amd/csrc/raster.hip:setup_kernel — per-splat record in `dtype`."""
+    """gstex_amd/csrc/raster.hip:setup_kernel — per-splat record in `dtype` (fp32: fp64 evaluation, rounded once)."""
+    if dtype == F32 and RECORD_FP64:
+        return {k: (v.to(F32) if v.is_floating_point() else v) for k, v in _splat_table(inp, F64).items()}
     V, campos, fx, fy, cx, cy = inp.cam.cast(dtype)
     Tu, Tv, Tw, xa, ya = splat_anchored(inp.means, inp.scales, inp.glob_scale, inp.quats, inp.cam, dtype)
     tu, tv, tw = quat_frame(inp.quats.to(dtype))
@@ -327,30 +336,35 @@ def _splat_table(inp: RasterInputs, dtype):
     )
 
 
-def rasterize(inp: RasterInputs, grad_dtype=F64, bins=None):
+def rasterize(inp: RasterInputs, grad_dtype=F64, bins=None, table_dtype=None):
     """Forward composite.  Returns (outputs_fp32, outputs_hi, aux) where outputs_* is a dict
     img (H,W,3), depth, reg, alpha (H,W), tex (H,W,C), normal (H,W,3); outputs_fp32 are the values
     the GPU must reproduce, outputs_hi the `grad_dtype` re-evaluation (differentiable w.r.t. the
-    leaf tensors of `inp` that require grad) that shares the fp32 decisions."""
+    leaf tensors of `inp` that require grad) that shares the fp32 decisions.
+    table_dtype (precision analysis, tools/grad_precision.py): evaluate the per-splat table (the chain that
+    raster.hip's setup / setup_bwd implement) in this dtype and only the per-pair part in grad_dtype."""
     cam = inp.cam
     H, W = cam.H, cam.W
     if bins is None:
         bins = bin_and_sort(inp.centers, inp.extents, inp.depths, H, W, cam.block)
     offsets, tile_ranges, sorted_ids, sorted_slots = bins
     dec = _render(inp, F32, tile_ranges, sorted_ids, None)
-    hi = _render(inp, grad_dtype, tile_ranges, sorted_ids, dec["decisions"])
+    hi = _render(inp, grad_dtype, tile_ranges, sorted_ids, dec["decisions"], table_dtype=table_dtype)
     aux = dict(offsets=offsets, tile_ranges=tile_ranges, sorted_ids=sorted_ids, sorted_slots=sorted_slots,
                last=dec["last"], T_final=dec["out"]["T_final"], margin=dec["margin"])
     return dec["out"], hi["out"], aux
 
 
-def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=None):
+def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=None, table_dtype=None):
     cam = inp.cam
     H, W = cam.H, cam.W
     C = inp.texture.shape[1]
     aa = bool(inp.settings & SETTING_AA_BLUR)
     dreg = bool(inp.settings & SETTING_DIST_REG)
-    tab = _splat_table(inp, dtype)
+    if table_dtype is None or table_dtype == dtype:
+        tab = _splat_table(inp, dtype)
+    else:  # mixed precision: table in table_dtype, cast (differentiably) to the per-pair dtype
+        tab = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in _splat_table(inp, table_dtype).items()}
     if decisions is not None:  # orientation sign from the fp32 pass
         tab["nrm"] = (tab["nrm"] * tab["sgn"][:, None]) * decisions["sgn"][:, None]
     tex = inp.texture.to(dtype)

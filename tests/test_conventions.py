@@ -1,0 +1,147 @@
+"""Raster output conventions pinned by the REFERENCE's own code (tests/golden/make_conventions_golden.py).
+
+The GStex_cuda kernels are absent from the reference, so the raster itself is parity-unpinned; these tests pin the
+conventions its consumers fix:
+  * pixel centre (x + 0.5, y + 0.5) and view-space z depth: the reference's depths_to_points (gstex.py:122-149,
+    +0.5 at :138-139, "don't use view depth" at :145-146) puts the rendered depth / alpha of a plane back ON the
+    plane (residual ~1e-6), where integer pixel coordinates would miss it by ~1e-2;
+  * world-space normals facing the camera: the reference's depth_to_normal (gstex.py:151-161), as its normal loss
+    uses it (gstex.py:1218-1220, 1316), agrees with the rendered normal in direction and sign;
+  * the composite (gstex.py:1204-1205) and the loss terms of get_loss_dict (gstex.py:1301-1322).
+CPU tests: the oracle against the golden; -m gpu tests: the HIP path against the same golden.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import raster as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "conventions.npz")
+
+
+@pytest.fixture(scope="module")
+def z():
+    with np.load(GOLD, allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
+def _plane_inputs(z):
+    H, W = (int(v) for v in z["plane_hw"])
+    fx, fy, cx, cy = (float(v) for v in z["plane_intr"])
+    vm = torch.from_numpy(z["plane_viewmat"])
+    c2w = torch.from_numpy(z["plane_c2w"])
+    cam = O.Camera(vm, fx, fy, cx, cy, H, W, 16, c2w[:3, 3])
+    means = torch.from_numpy(z["plane_means"])
+    scales = torch.from_numpy(z["plane_scales"])
+    quats = torch.from_numpy(z["plane_quats"])
+    opac = torch.from_numpy(z["plane_opacities"])
+    n = means.shape[0]
+    centers, extents = O.aabb_2d(means, scales, 1.0, quats, cam)
+    _, depths = O.project_points(means, cam)
+    inp = O.RasterInputs(torch.zeros((n, 3), dtype=torch.int32), centers, extents, depths, torch.full((n, 3), 0.5),
+                         opac, means, scales, 1.0, quats, torch.full((n, 1, 2), 0.5), torch.zeros((n, 1, 3)),
+                         torch.zeros((n, 1, 3)), torch.zeros((0, 3)), cam, settings=int(z["plane_settings"][0]))
+    return inp, (vm, c2w, fx, fy, cx, cy, H, W)
+
+
+def _interior(alpha):
+    from scipy.ndimage import binary_erosion
+
+    m = binary_erosion(alpha > 0.999)
+    m[0, :] = m[-1, :] = m[:, 0] = m[:, -1] = False
+    return m
+
+
+def test_reference_points_lie_on_the_plane(z):
+    """depths_to_points (reference) of depth / alpha: on the plane to ~1e-6, vs >= 1e-2 for integer centres."""
+    inside = z["plane_alpha"] > 0.999
+    assert inside.mean() > 0.5
+    n = z["plane_normal"].astype(np.float64)
+    res = np.abs(z["plane_ref_points"].astype(np.float64) @ n)[inside]
+    ctrl = np.abs(z["plane_ref_points_intcentre"].astype(np.float64) @ n)[inside]
+    assert res.max() < 1e-5, res.max()
+    assert ctrl.min() > 1e-3 and ctrl.min() > 1000 * res.max(), (ctrl.min(), res.max())
+
+
+def test_reference_estimated_normals_match_rendered(z):
+    """depth_to_normal (reference, on the raw depth as gstex.py:1220 calls it) == the rendered normal's direction,
+    same sign (both face the camera, world space).  The raw depth carries the (1 - T) factor (T in [1e-4, 1e-3]),
+    so the agreement is ~1e-4 in cos, not exact."""
+    m = _interior(z["plane_alpha"])
+    assert m.sum() > 1000
+    est = z["plane_ref_est_normal"].astype(np.float64)
+    rn = z["plane_rnormal"].astype(np.float64)
+    rnn = rn / np.linalg.norm(rn, axis=-1, keepdims=True).clip(1e-30)
+    cos = (est * rnn).sum(-1)[m]
+    assert cos.min() > 0.999 and np.median(cos) > 0.99995, (cos.min(), np.median(cos))
+    # the rendered normal is the plane's (world space) oriented toward the camera
+    campos = z["plane_c2w"][:3, 3].astype(np.float64)
+    n = z["plane_normal"].astype(np.float64)
+    assert np.all(np.abs(rnn[m] @ n) > 1 - 1e-6)
+    assert np.all(rnn[m] @ campos > 0)  # the plane passes through the origin: facing the camera
+
+
+def test_oracle_renders_the_golden_plane(z):
+    inp, _ = _plane_inputs(z)
+    o32, _, _ = O.rasterize(inp)
+    for k, g in (("depth", "plane_depth"), ("alpha", "plane_alpha"), ("normal", "plane_rnormal")):
+        np.testing.assert_array_equal(o32[k].numpy(), z[g], err_msg=k)
+
+
+def test_composite_and_loss_terms_match_reference(z):
+    """The composite (gstex.py:1204-1205) as GStexTrainer.render forms it, and the loss combination of
+    get_loss_dict with the golden's stubbed SSIM value."""
+    img, tex, alpha = (torch.from_numpy(z[k]) for k in ("loss_img", "loss_tex", "loss_alpha"))
+    bg, gt = torch.from_numpy(z["loss_bg"]), torch.from_numpy(z["loss_gt"])
+    rgb = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * bg[None, None, :], 0.0, 1.0)  # model.py
+    np.testing.assert_array_equal(rgb.numpy(), z["loss_rgb"])
+    l1 = torch.abs(gt - rgb).mean()
+    assert abs(float(l1) - float(z["loss_l1"][0])) < 1e-7
+    lam_ssim, lam_reg, lam_normal = (float(v) for v in z["loss_lambdas"])
+    main = (1 - lam_ssim) * l1 + lam_ssim * (1 - float(z["loss_ssim_stub"][0]))
+    assert abs(float(main) - float(z["loss_main"][0])) < 1e-7
+    normal, est, reg = (torch.from_numpy(z[k]) for k in ("loss_normal", "loss_est", "loss_reg"))
+    nl = lam_normal * torch.mean(alpha - torch.sum(normal * est, dim=-1))
+    assert abs(float(nl) - float(z["loss_normal_loss"][0])) < 1e-7
+    assert abs(float(lam_reg * reg.mean()) - float(z["loss_reg_loss"][0])) < 1e-7
+
+
+# ------------------------------------------------------------------------------------------ HIP path
+@pytest.mark.gpu
+def test_hip_plane_depth_normal_match_golden(z):
+    """The HIP rasterizer's depth / alpha / normal of the plane: within the forward tolerance of the golden, so the
+    reference's depths_to_points / depth_to_normal see the same geometry from the HIP path."""
+    import gstex_cuda
+
+    from helpers import TOL_ABS, TOL_REL
+
+    inp, (vm, c2w, fx, fy, cx, cy, H, W) = _plane_inputs(z)
+    dev = "cuda"
+    d = lambda t: t.detach().to(dev).contiguous()  # noqa: E731
+    n = inp.means.shape[0]
+    nth = O.num_tiles_hit(inp.centers, inp.extents, H, W)
+    outs = gstex_cuda.texture_gaussians(
+        (n, 1, 3), d(inp.texture_dims), d(inp.centers), d(inp.extents), d(inp.depths), d(nth), d(inp.rgbs),
+        d(inp.opacities), d(inp.means), d(inp.scales), 1.0, d(inp.quats), d(inp.uv0), d(inp.umap), d(inp.vmap),
+        torch.zeros((0, 3), device=dev), d(vm), d(c2w), fx, fy, cx, cy, H, W, 16, inp.settings)
+    got = {"depth": outs[1].cpu(), "alpha": outs[3].cpu(), "normal": outs[5].cpu()}
+    for k, g in (("depth", "plane_depth"), ("alpha", "plane_alpha"), ("normal", "plane_rnormal")):
+        ref = torch.from_numpy(z[g]).double()
+        err = (got[k].double() - ref).abs()
+        assert bool((err <= TOL_ABS + TOL_REL * ref.abs()).all()), f"{k}: max err {float(err.max()):.3e}"
+
+
+@pytest.mark.gpu
+def test_hip_composite_and_l1_match_reference(z):
+    """The fused loss kernel (gstex_amd.loss, ssim_lambda = 0: the loss is L1) against the reference's composite and
+    L1 (gstex.py:1204-1205, 1301)."""
+    from gstex_amd.loss import photometric_loss
+
+    dev = "cuda"
+    img, tex, alpha, bg, gt = (torch.from_numpy(z[k]).to(dev).contiguous()
+                               for k in ("loss_img", "loss_tex", "loss_alpha", "loss_bg", "loss_gt"))
+    loss, rgb = photometric_loss(img, tex, alpha, bg, gt, ssim_lambda=0.0)
+    np.testing.assert_allclose(rgb.cpu().numpy(), z["loss_rgb"], rtol=0, atol=1e-7)
+    assert abs(float(loss) - float(z["loss_l1"][0])) < 1e-6 * max(1.0, float(z["loss_l1"][0]))

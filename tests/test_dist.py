@@ -92,6 +92,13 @@ class _SinkTrainer:
         return [self.means, self.features_dc, self.features_rest, self.opacities, self.scales, self.quats,
                 self.texture_dc]
 
+    def zero_grad(self, set_to_none=True):  # torch.optim.Optimizer.zero_grad semantics (GStexTrainer.zero_grad)
+        for p in self.parameters():
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
     def backward(self, rank):
         w = float(rank + 1)
         loss = w * (self.means.sum() + self.features_rest.sum() + 2 * self.opacities.sum() + self.scales.sum()
@@ -132,7 +139,22 @@ def _trainer_worker(rank, world, port, q):
             tr.backward(rank)
             sync.all_reduce()
             res[f"after_rechart_{step}"] = bool(torch.allclose(tr.texture_dc.grad, mean_w * tr.texture_dc.detach()))
-        # a second backward without all_reduce() in between is refused
+        # zero_grad(set_to_none=True) after zero(): autograd writes detached .grad tensors and the
+        # kernel still fills the sink; all_reduce() must fold them back and reduce everything exactly once
+        for step in range(2):
+            sync.zero()
+            tr.zero_grad()
+            tr.backward(rank)
+            detached = tr.means.grad.data_ptr() != sync.flat.data_ptr()
+            sync.all_reduce()
+            ok = detached and torch.allclose(tr.texture_dc.grad, mean_w * tr.texture_dc.detach())
+            ok = ok and torch.allclose(tr.means.grad, torch.full_like(tr.means, mean_w))
+            ok = ok and torch.allclose(tr.quats.grad, torch.full_like(tr.quats, mean_w))
+            ok = ok and bool(torch.all(tr.features_dc.grad == 0))
+            ok = ok and tr.means.grad.data_ptr() == sync.flat.data_ptr()  # re-attached to the buffer
+            res[f"set_to_none_{step}"] = bool(ok)
+        # a second backward without all_reduce() in between is refused: by zero(), and by the sink's ready callback
+        # (its kernel would add into the slice the running collective reads)
         sync.zero()
         tr.backward(rank)
         try:
@@ -140,6 +162,11 @@ def _trainer_worker(rank, world, port, q):
             res["double_backward_refused"] = False
         except RuntimeError:
             res["double_backward_refused"] = True
+        try:
+            tr.backward(rank)
+            res["double_backward_sink_refused"] = False
+        except RuntimeError:
+            res["double_backward_sink_refused"] = True
         sync.all_reduce()
         q.put((rank, res))
     finally:
@@ -164,3 +191,6 @@ def test_trainer_layout_sink_and_recharts_world2():
         assert not r["rebuilt_0"], "an in-place rechart must keep the flat buffer"
         assert r["rebuilt_1"], "a grown texel store must rebuild the flat buffer"
         assert r["double_backward_refused"]
+        assert r["double_backward_sink_refused"]
+        for step in range(2):
+            assert r[f"set_to_none_{step}"], f"rank {rank}: zero_grad(set_to_none) after zero() mis-reduced (step {step})"

@@ -36,8 +36,7 @@ def test_synced_step_matches_unsynced_across_rechart():
         plain = GStexTrainer(sc, dev, start_step=3000)
         synced = GStexTrainer(sc, dev, start_step=3000)
         sync = GradSync(synced, 1)
-        store = synced.texture_dc
-        for step in range(4):
+        for step in range(5):
             plain.zero_grad()
             plain.forward_backward(views[step % 3], gts[step % 3])
             plain.optimizer_step()
@@ -47,11 +46,19 @@ def test_synced_step_matches_unsynced_across_rechart():
                 sync.flat[sync._tail_off:].data_ptr()
             sync.all_reduce()
             synced.optimizer_step()
-            if step == 1:
-                plain.recharge()
-                synced.recharge()
-        # a rechart that fits the store keeps the Parameter (and the flat buffer); one that needs more grows it
-        assert (synced.texture_dc is store) == (synced.n_texels <= store.shape[0])
+            if step in (1, 2):
+                # step 1: charts for 90 % of the store's rows (fit: the Parameter and the flat buffer are kept);
+                # step 2: 130 % (the store grows: a new Parameter, a new buffer and sink at the next zero())
+                store, flat = synced.texture_dc, sync.flat
+                for tr in (plain, synced):
+                    tr.pixel_num = (0.9 if step == 1 else 1.3) * store.shape[0]
+                    tr.recharge()
+                if step == 1:
+                    assert synced.texture_dc is store and synced.n_texels <= store.shape[0]
+                else:
+                    assert synced.texture_dc is not store and synced.texture_dc.shape[0] > store.shape[0]
+                sync.zero()
+                assert (sync.flat is flat) == (step == 1), "flat buffer kept in place / rebuilt after growth"
         assert synced.texture_dc.shape == plain.texture_dc.shape
         for (name, a), b in zip(plain.param_groups().items(), synced.param_groups().values()):
             a, b = a[0].detach().double(), b[0].detach().double()

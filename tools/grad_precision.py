@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Where does the fp32 error of the means / quats gradients arise?  (VERDICT r02 next #4.)
+
+Runs the CPU oracle's autograd on a window of a bench scene in three precision mixes and reports each
+gradient's norm-wise and max relative error against the all-fp64 evaluation:
+  fp32        per-splat table (the chain raster.hip's setup / setup_bwd implement) and per-pair part in fp32
+              (--fp32-record: the round-2 formulation; default: the record evaluated in fp64 and rounded once, the
+              current raster.hip setup_kernel / setup_bwd_chain) -- its error is the tests' "fp32 floor";
+  pair32      table fp64, per-pair fp32 (a GPU whose setup_bwd chain ran in fp64);
+  table32     table fp32, per-pair fp64;
+With the fp64 record (default) "table32" means the fp64 record rounded to fp32, so pair64/table32 isolates the
+rounding of the stored record: exact arithmetic everywhere else -- the conditioning floor of an fp32 record.
+Test infrastructure only (imports oracle/).  Usage: python tools/grad_precision.py [--win 48] [--cfg 3]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from helpers import DIFF, FLIP_MARGIN, grad_norm_err, grad_rel_err, make_window_case, upstream  # noqa: E402
+from oracle import raster as O  # noqa: E402
+
+F32, F64 = torch.float32, torch.float64
+
+
+def grads(case, pair_dtype, table_dtype, outputs):
+    inp = case.inp
+    leaves = {}
+    for k in DIFF:
+        t = getattr(inp, k).detach().clone().requires_grad_(True)
+        setattr(inp, k, t)
+        leaves[k] = t
+    _, o, aux = O.rasterize(inp, grad_dtype=pair_dtype, table_dtype=table_dtype)
+    up = upstream(inp.cam.H, inp.cam.W, case.C, 5, aux["margin"] < FLIP_MARGIN)
+    loss = sum((o[k] * up[k].to(pair_dtype)).sum() for k in outputs)
+    loss.backward()
+    out = {k: (v.grad.detach().double() if v.grad is not None else torch.zeros_like(v, dtype=F64)) for k, v in leaves.items()}
+    for k in DIFF:
+        setattr(inp, k, getattr(inp, k).detach())
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--win", type=int, default=48)
+    ap.add_argument("--cfg", type=int, default=3)
+    ap.add_argument("--all-outputs", action="store_true")
+    ap.add_argument("--fp32-record", action="store_true", help="all-fp32 per-splat record (round-2 formulation)")
+    args = ap.parse_args()
+    O.RECORD_FP64 = not args.fp32_record
+    n, t = (200_000, 1e7) if args.cfg == 3 else (50_000, 1e6)
+    case = make_window_case(n, t, 800, 800, args.win)
+    outputs = ("img", "depth", "reg", "alpha", "tex", "normal") if args.all_outputs else ("img", "alpha", "tex")
+    ref = grads(case, F64, F64, outputs)
+    mixes = {"fp32": (F32, F32), "pair32/table64": (F32, F64), "pair64/table32": (F64, F32)}
+    print(f"cfg{args.cfg} {args.win}x{args.win} window, {case.inp.means.shape[0]} splats, outputs {outputs}")
+    print(f"{'mix':16s} " + " ".join(f"{k:>18s}" for k in DIFF))
+    for name, (pd, td) in mixes.items():
+        g = grads(case, pd, td, outputs)
+        cells = []
+        for k in DIFF:
+            cells.append(f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}")
+        print(f"{name:16s} " + " ".join(f"{c:>18s}" for c in cells))
+    print("(norm-wise / max-element relative error vs all-fp64)")
+
+
+if __name__ == "__main__":
+    main()

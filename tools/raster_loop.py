@@ -74,7 +74,8 @@ def main():
         lib.gstex_debug_stats(buf)
         n = args.iters + 1
         names = ["units", "visits", "visits_any", "contrib_lanes", "flush_passes", "tail_lanes", "flushed_entries", "tex_visits",
-                 "fwd_candidates", "fwd_cull_pass", "fwd_visits", "fwd_visits_any", "fwd_contrib_lanes"]
+                 "fwd_candidates", "fwd_cull_pass", "fwd_visits", "fwd_visits_any", "fwd_contrib_lanes",
+                 "bwd_alive_lanes", "bwd_visits_le16", "bwd_visits_ge48"]
         if os.environ.get("GSTEX_STATS_PHASES"):  # GSTEX_STATS=2: wave-clock sums per backward phase
             names = ["load+barrier", "place+cull", "visits", "barrier_pre_combine", "combine+flush", "barrier_end",
                      "prologue", "-"]
