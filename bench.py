@@ -274,9 +274,8 @@ def main():
         else:
             trainer.zero_grad()
         trainer.forward_backward(views[pose], gts[pose])
-        if sync is not None:
-            sync.all_reduce()
-        trainer.optimizer_step()
+        # N > 1: the collectives inside the step (texel group updated while the head's collective runs)
+        trainer.optimizer_step(sync=sync)
 
     for _ in range(args.warmup):
         step()

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 REC_FLOATS = 32
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows (24 or 32 used)
 SETTING_AA_BLUR = 1 << 9
@@ -115,6 +115,8 @@ SIGNATURES = {
                                  _P, _P, _P, c_size_t, _P]),
     "gstex_adam_step": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, _P]),
     "gstex_adam_step_ex": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32, _P]),
+    "gstex_adam_step_scaled": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32,
+                                         c_float, _P]),
 }
 
 _lib = None

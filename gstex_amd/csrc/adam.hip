@@ -47,10 +47,13 @@ struct AdamArgs {
     int64_t block_start[kAdamMaxTensors + 1];
     int n;
     float beta1, beta2, eps, one_m_beta1, one_m_beta2;
+    float gscale;  // gradient scale applied on read (gstex_adam_step_scaled: a data-parallel 1 / world), 1 = none
 };
 
+template <bool SCALE>
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1w, float b2,
-                                          float one_m_b2, float eps, float neg_step, float bc2_sqrt) {
+                                          float one_m_b2, float eps, float neg_step, float bc2_sqrt, float gs) {
+    if (SCALE) g = g * gs;  // the same fp32 product as scaling the gradient buffer first
     m = m + b1w * (g - m);
     v = v * b2 + one_m_b2 * (g * g);
     const float denom = sqrtf(v) / bc2_sqrt + eps;
@@ -59,7 +62,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 
 // ZERO_GRAD: the gradient is zeroed after it is read (the next backward accumulates into the same buffer: no separate
 // fill launch, and the zeroing rides along with an update that may run on a side stream)
-template <bool ZERO_GRAD>
+template <bool ZERO_GRAD, bool SCALE>
 __device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
     int k = 0;
     while (k + 1 < a.n && a.block_start[k + 1] <= b) ++k;
@@ -88,18 +91,18 @@ __device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
         for (int r = 0; r < kAdamVec; ++r) {
             const int64_t i = base + 4 * ((int64_t)r * kAdamThreads + threadIdx.x);
             if (full[r]) {
-                adam_elem(p[r].x, g[r].x, m[r].x, v[r].x, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                adam_elem(p[r].y, g[r].y, m[r].y, v[r].y, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                adam_elem(p[r].z, g[r].z, m[r].z, v[r].z, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
-                adam_elem(p[r].w, g[r].w, m[r].w, v[r].w, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem<SCALE>(p[r].x, g[r].x, m[r].x, v[r].x, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s, a.gscale);
+                adam_elem<SCALE>(p[r].y, g[r].y, m[r].y, v[r].y, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s, a.gscale);
+                adam_elem<SCALE>(p[r].z, g[r].z, m[r].z, v[r].z, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s, a.gscale);
+                adam_elem<SCALE>(p[r].w, g[r].w, m[r].w, v[r].w, a.one_m_beta1, a.beta2, a.one_m_beta2, a.eps, neg_step, bc2s, a.gscale);
                 st_stream(reinterpret_cast<float4*>(t.param + i), p[r]);
                 st_stream(reinterpret_cast<float4*>(t.exp_avg + i), m[r]);
                 st_stream(reinterpret_cast<float4*>(t.exp_avg_sq + i), v[r]);
                 if (ZERO_GRAD) st_stream(reinterpret_cast<float4*>(const_cast<float*>(t.grad) + i), make_float4(0.f, 0.f, 0.f, 0.f));
             } else {
                 for (int64_t e = i; e < t.numel; ++e) {
-                    adam_elem(t.param[e], t.grad[e], t.exp_avg[e], t.exp_avg_sq[e], a.one_m_beta1, a.beta2,
-                              a.one_m_beta2, a.eps, neg_step, bc2s);
+                    adam_elem<SCALE>(t.param[e], t.grad[e], t.exp_avg[e], t.exp_avg_sq[e], a.one_m_beta1, a.beta2,
+                                     a.one_m_beta2, a.eps, neg_step, bc2s, a.gscale);
                     if (ZERO_GRAD) const_cast<float*>(t.grad)[e] = 0.0f;
                 }
             }
@@ -108,8 +111,8 @@ __device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
         for (int e = threadIdx.x; e < kAdamPerBlock; e += kAdamThreads) {
             const int64_t i = base + e;
             if (i < t.numel) {
-                adam_elem(t.param[i], t.grad[i], t.exp_avg[i], t.exp_avg_sq[i], a.one_m_beta1, a.beta2,
-                          a.one_m_beta2, a.eps, neg_step, bc2s);
+                adam_elem<SCALE>(t.param[i], t.grad[i], t.exp_avg[i], t.exp_avg_sq[i], a.one_m_beta1, a.beta2,
+                                 a.one_m_beta2, a.eps, neg_step, bc2s, a.gscale);
                 if (ZERO_GRAD) const_cast<float*>(t.grad)[i] = 0.0f;
             }
         }
@@ -117,16 +120,16 @@ __device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
 }
 
 // grid-stride over the chunks: a capped grid (GSTEX_ADAM_GRID flags) leaves most of every CU to another stream
-template <bool ZERO_GRAD>
+template <bool ZERO_GRAD, bool SCALE>
 __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
-    for (int64_t b = blockIdx.x; b < a.block_start[a.n]; b += gridDim.x) adam_chunk<ZERO_GRAD>(a, b);
+    for (int64_t b = blockIdx.x; b < a.block_start[a.n]; b += gridDim.x) adam_chunk<ZERO_GRAD, SCALE>(a, b);
 }
 
 }  // namespace
 
 namespace {
 int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2, double eps,
-                int32_t flags, void* stream) {
+                int32_t flags, float grad_scale, void* stream) {
     GSTEX_REQUIRE(n_tensors >= 0 && n_tensors <= kAdamMaxTensors,
                   "gstex_adam_step: n_tensors must be in [0, %d] (got %d)", kAdamMaxTensors, n_tensors);
     GSTEX_REQUIRE(n_tensors == 0 || tensors, "gstex_adam_step: null tensor table");
@@ -152,24 +155,36 @@ int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta
     a.eps = (float)eps;
     a.one_m_beta1 = (float)(1.0 - beta1);
     a.one_m_beta2 = (float)(1.0 - beta2);
+    a.gscale = grad_scale;
     const int64_t cap = (flags >> GSTEX_ADAM_GRID_SHIFT) & 0xFFFF;
     const unsigned grid = (unsigned)(cap > 0 && cap < blocks ? cap : blocks);
-    if (flags & GSTEX_ADAM_ZERO_GRAD)
-        adam_kernel<true><<<grid, kAdamThreads, 0, gstex::as_stream(stream)>>>(a);
-    else
-        adam_kernel<false><<<grid, kAdamThreads, 0, gstex::as_stream(stream)>>>(a);
+    const hipStream_t st = gstex::as_stream(stream);
+    const bool zg = flags & GSTEX_ADAM_ZERO_GRAD, sc = grad_scale != 1.0f;
+    if (zg && sc) adam_kernel<true, true><<<grid, kAdamThreads, 0, st>>>(a);
+    else if (zg) adam_kernel<true, false><<<grid, kAdamThreads, 0, st>>>(a);
+    else if (sc) adam_kernel<false, true><<<grid, kAdamThreads, 0, st>>>(a);
+    else adam_kernel<false, false><<<grid, kAdamThreads, 0, st>>>(a);
     return gstex::launch_status("gstex_adam_step");
 }
 }  // namespace
 
 extern "C" int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                                double eps, void* stream) {
-    return adam_launch(n_tensors, tensors, beta1, beta2, eps, 0, stream);
+    return adam_launch(n_tensors, tensors, beta1, beta2, eps, 0, 1.0f, stream);
 }
 
 extern "C" int gstex_adam_step_ex(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                                   double eps, int32_t flags, void* stream) {
     GSTEX_REQUIRE((flags & ~(GSTEX_ADAM_ZERO_GRAD | (0xFFFF << GSTEX_ADAM_GRID_SHIFT))) == 0,
                   "gstex_adam_step_ex: unknown flags 0x%x", flags);
-    return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, stream);
+    return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, 1.0f, stream);
+}
+
+extern "C" int gstex_adam_step_scaled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                                      double eps, int32_t flags, float grad_scale, void* stream) {
+    GSTEX_REQUIRE((flags & ~(GSTEX_ADAM_ZERO_GRAD | (0xFFFF << GSTEX_ADAM_GRID_SHIFT))) == 0,
+                  "gstex_adam_step_scaled: unknown flags 0x%x", flags);
+    GSTEX_REQUIRE(grad_scale == grad_scale && grad_scale > 0.0f && grad_scale <= 1.0f,
+                  "gstex_adam_step_scaled: grad_scale must be in (0, 1] (got %g)", (double)grad_scale);
+    return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, grad_scale, stream);
 }

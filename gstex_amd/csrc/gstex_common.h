@@ -337,12 +337,15 @@ __device__ __forceinline__ void affine_homog_vjp(V3<T> Tu, V3<T> Tv, V3<T> Tw, V
 
 // Raster record layout (GSTEX_REC_FLOATS = 32 floats = 128 B, one cache line), as 8 float4 planes.
 enum RecField {
-    // every field the photometric backward reads lies in [0, 27) (one contiguous scalar load run per visit)
-    R_A = 0, R_B = 3, R_PZ = 6, R_TW = 7, R_XY = 10, R_OPAC = 12, R_RGB = 13,
-    R_TU0 = 16, R_AUU = 17, R_AUV = 18, R_TV0 = 19, R_AVU = 20, R_AVV = 21,
-    R_H = 22, R_W = 23, R_OFF = 24, R_XA = 25, R_YA = 26, R_NRM = 27,
+    // dwords [0, 12) (planes 0-2): everything the per-wave cull reads (raster.hip wave_may_hit), so a candidate costs
+    // three 16-B loads; every field the photometric backward reads lies in [0, 27) (one contiguous scalar load run
+    // per visit)
+    R_A = 0, R_B = 3, R_PZ = 6, R_XA = 7, R_YA = 8, R_XY = 9, R_OPAC = 11,
+    R_TW = 12, R_RGB = 15, R_TU0 = 18, R_AUU = 19, R_AUV = 20, R_TV0 = 21, R_AVU = 22, R_AVV = 23,
+    R_H = 24, R_W = 25, R_OFF = 26, R_NRM = 27,
     R_HF = 30, R_WF = 31  // (float)h, (float)w: exact, saves the forward's per-visit conversions
 };
+constexpr int kCullPlanes = 3;  // record planes holding the cull fields
 
 // Screen box of the projected disc u^2 + v^2 <= c2 (compute_aabb with a general cutoff).
 // Returns false when the disc reaches the camera plane (unbounded projection).

@@ -131,7 +131,7 @@ constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
                         // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
-                        // (backward ablations skip work: timing experiments only)
+                        // 256 = no partial-row / flag stores (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kRowStride = GSTEX_PARTIAL_FLOATS;  // 32 floats between partial rows
@@ -207,23 +207,24 @@ struct Rec {
     float hf, wf;  // (float)h, (float)w
 };
 
-// Record planes (gstex_common.h RecField): A B | B Pz Tw | Tw xy | opac rgb | tu0 auu auv tv0 | avu avv h w |
-// off xa ya nrm | nrm hf wf
+// Record fields from its 8 float4 planes (gstex_common.h RecField)
 __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, float4 d, float4 e, float4 f, float4 g,
                                                float4 q) {
+    const float v[GSTEX_REC_FLOATS] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w,
+                                       e.x, e.y, e.z, e.w, f.x, f.y, f.z, f.w, g.x, g.y, g.z, g.w, q.x, q.y, q.z, q.w};
     Rec r;
-    r.A = f3{a.x, a.y, a.z};
-    r.B = f3{a.w, b.x, b.y};
-    r.Pz = b.z;
-    r.Tw = f3{b.w, c.x, c.y};
-    r.x = c.z; r.y = c.w;
-    r.opac = d.x;
-    r.rgb[0] = d.y; r.rgb[1] = d.z; r.rgb[2] = d.w;
-    r.tu0 = e.x; r.auu = e.y; r.auv = e.z; r.tv0 = e.w; r.avu = f.x; r.avv = f.y;
-    r.h = __float_as_int(f.z); r.w = __float_as_int(f.w); r.off = __float_as_int(g.x);
-    r.xa = g.y; r.ya = g.z;
-    r.nrm[0] = g.w; r.nrm[1] = q.x; r.nrm[2] = q.y;
-    r.hf = q.z; r.wf = q.w;
+    r.A = f3{v[R_A], v[R_A + 1], v[R_A + 2]};
+    r.B = f3{v[R_B], v[R_B + 1], v[R_B + 2]};
+    r.Pz = v[R_PZ];
+    r.Tw = f3{v[R_TW], v[R_TW + 1], v[R_TW + 2]};
+    r.x = v[R_XY]; r.y = v[R_XY + 1];
+    r.opac = v[R_OPAC];
+    r.rgb[0] = v[R_RGB]; r.rgb[1] = v[R_RGB + 1]; r.rgb[2] = v[R_RGB + 2];
+    r.tu0 = v[R_TU0]; r.auu = v[R_AUU]; r.auv = v[R_AUV]; r.tv0 = v[R_TV0]; r.avu = v[R_AVU]; r.avv = v[R_AVV];
+    r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = __float_as_int(v[R_OFF]);
+    r.xa = v[R_XA]; r.ya = v[R_YA];
+    r.nrm[0] = v[R_NRM]; r.nrm[1] = v[R_NRM + 1]; r.nrm[2] = v[R_NRM + 2];
+    r.hf = v[R_HF]; r.wf = v[R_WF];
     return r;
 }
 
@@ -352,27 +353,34 @@ __device__ __forceinline__ bool conic_edge(float ax, float ay, float az, float q
 // upstream), tested exactly against the rectangle -- anchor inside, or an edge meeting it -- with a 1 %
 // threshold margin and a 0.05 px larger rectangle, so the fp32 evaluation can never accept a pair the test
 // rejected.
-template <int NB>
-__device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
-                                             bool aa) {
-    const float4 a = s[0 * NB + j], b = s[1 * NB + j], c = s[2 * NB + j], d = s[3 * NB + j], g = s[6 * NB + j];
-    const float opac = d.x;
+// (the cull fields are record dwords [0, 12): planes 0-2, RecField)
+__device__ __forceinline__ bool may_hit_planes(float4 p0, float4 p1, float4 p2, float wx0, float wx1, float wy0,
+                                               float wy1, bool aa) {
+    const float v[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
+    const float opac = v[R_OPAC];
     if (!(opac * 255.0f > 1.0f)) return false;
     const float rm = 2.0f * logf(255.0f * opac) * 1.01f + 1e-2f;
     const float x0 = wx0 - 0.05f, x1 = wx1 + 0.05f, y0 = wy0 - 0.05f, y1 = wy1 + 0.05f;
+    const float cx = v[R_XY], cy = v[R_XY + 1];
     if (aa) {
-        const float ex = c.z - fminf(fmaxf(c.z, x0), x1), ey = c.w - fminf(fmaxf(c.w, y0), y1);
+        const float ex = cx - fminf(fmaxf(cx, x0), x1), ey = cy - fminf(fmaxf(cy, y0), y1);
         if (2.0f * (ex * ex + ey * ey) <= rm) return true;
     }
-    const float xa = g.y, ya = g.z;
+    const float xa = v[R_XA], ya = v[R_YA];
     if (xa >= x0 && xa <= x1 && ya >= y0 && ya <= y1) return true;
     if (!GSTEX_CONIC_CULL) return true;
-    const float Ax = a.x, Ay = a.y, Az = a.z, Bx = a.w, By = b.x, Bz = b.y, Pz = b.z;
+    const float Ax = v[R_A], Ay = v[R_A + 1], Az = v[R_A + 2], Bx = v[R_B], By = v[R_B + 1], Bz = v[R_B + 2];
+    const float Pz = v[R_PZ];
     const float dx0 = x0 - xa, dx1 = x1 - xa, dy0 = y0 - ya, dy1 = y1 - ya;
     return conic_edge(Ax, Ay, Az, dy0 * Bx, dy0 * By, Pz + dy0 * Bz, rm, dx0, dx1) ||
            conic_edge(Ax, Ay, Az, dy1 * Bx, dy1 * By, Pz + dy1 * Bz, rm, dx0, dx1) ||
            conic_edge(Bx, By, Bz, dx0 * Ax, dx0 * Ay, Pz + dx0 * Az, rm, dy0, dy1) ||
            conic_edge(Bx, By, Bz, dx1 * Ax, dx1 * Ay, Pz + dx1 * Az, rm, dy0, dy1);
+}
+template <int NB>
+__device__ __forceinline__ bool wave_may_hit(const float4* s, int j, float wx0, float wx1, float wy0, float wy1,
+                                             bool aa) {
+    return may_hit_planes(s[0 * NB + j], s[1 * NB + j], s[2 * NB + j], wx0, wx1, wy0, wy1, aa);
 }
 
 struct Hit {
@@ -572,23 +580,46 @@ __device__ __forceinline__ float tex_accum(float acc, float v00, float v01, floa
 }
 // GEOF = false: depth / distortion / normal not produced (their outputs are NULL: a caller whose loss does
 // not use them, e.g. the photometric training step); every other output is computed unchanged.
-template <int C, bool GEOF>
-__global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster_fwd_kernel(
+// ONE = true (the default, GSTEX_FWD_WAVE): one wave64 workgroup per (tile, 8x8 quadrant) -- no barriers, no record
+// staging shared between the quadrants; each wave culls a 64-position word of the tile list at a time (lane k tests
+// position k from the record's first three planes, the cull fields) and reads each visited record with scalar loads
+// (as the backward does).  ONE = false: the round-2 form, one 256-thread workgroup per tile whose four quadrant waves
+// share 128-record batches staged in LDS (barrier per batch).
+template <bool ONE> struct FwdShape;
+template <> struct FwdShape<false> { static constexpr int kThr = kThreads, kStep = kFwdBatch; };
+template <> struct FwdShape<true> { static constexpr int kThr = 64, kStep = 64; };
+#ifndef GSTEX_FWD_WAVE
+#define GSTEX_FWD_WAVE 1
+#endif
+#ifndef GSTEX_FWD1_OCC
+#define GSTEX_FWD1_OCC 8  // single-wave forward: waves per SIMD the register allocation targets
+#endif
+
+template <int C, bool GEOF, bool ONE>
+__global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, int n_texels, float tex_scale,
     float tex_bias, float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
-    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state, AuxPtrs aux) {
+    float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state, AuxPtrs aux,
+    int n_tiles) {
     const Camera cam = load_camera(cam_args);
     unsigned long long* __restrict__ visit_masks = aux.masks;
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
-    __shared__ float4 s_rec[kRecF4 * kFwdBatch];
-    __shared__ int s_gid[kFwdBatch];
-    const int tile = tile_order ? tile_order[blockIdx.x] : (int)blockIdx.x;  // largest-first when given
+    constexpr int kThr = FwdShape<ONE>::kThr, kStep = FwdShape<ONE>::kStep, kWords = kStep / 64;
+    __shared__ float4 s_rec[ONE ? 1 : kRecF4 * kFwdBatch];
+    __shared__ int s_gid[ONE ? 1 : kFwdBatch];
+    // ONE: tile i of the largest-first order takes blocks 32 (i / 8) + 8 q + i % 8, q = quadrant, so the four quadrants
+    // of a tile are dispatched to one XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2
+    const int bidx = (int)blockIdx.x;
+    const int ti = ONE ? (bidx >> 5) * 8 + (bidx & 7) : bidx;
+    const int tq = ONE ? (bidx >> 3) & 3 : 0;
+    if (ti >= n_tiles) return;  // ONE: the grid is rounded up to whole groups of 8 tiles
+    const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int tid = threadIdx.x;
+    const int tid = ONE ? tq * 64 + (int)threadIdx.x : (int)threadIdx.x;
     const WaveBlock wb = wave_block(tx, ty, tid);
     const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
@@ -629,8 +660,8 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
     // XCD group of the tile's backward units: its GSTEX_XCD_MB x GSTEX_XCD_MB-tile macro-block
     const int xgroup = GSTEX_XCD_GROUPS
         ? (((tx / GSTEX_XCD_MB) + (ty / GSTEX_XCD_MB) * ((tiles_x + GSTEX_XCD_MB - 1) / GSTEX_XCD_MB)) & 7) << 24 : 0;
-    if (aux.slot_tile)
-        for (int k = tid; k * kSegLen < rng.y - rng.x; k += kThreads) aux.slot_tile[sbase + k] = tile;
+    if (aux.slot_tile && (!ONE || tq == 0))
+        for (int k = (int)threadIdx.x; k * kSegLen < rng.y - rng.x; k += kThr) aux.slot_tile[sbase + k] = tile;
     // one checkpoint record: field f of the wave's lane at ckpt[((slot * 4 + wave) * F + f) * 64 + lane]
     auto write_ck = [&](int slot) {
         float* ck = aux.ckpt + ((size_t)slot * 4 + wave) * aux.F * 64 + lane;
@@ -652,7 +683,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
         }
     };
 
-    for (int b0 = rng.x; b0 < rng.y; b0 += kFwdBatch) {
+    for (int b0 = rng.x; b0 < rng.y; b0 += kStep) {
         if (aux.cost && b0 > rng.x && (b0 - rng.x) % kSegLen == 0) {
             // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
             const int cnt = wave_max_i(seg_visits);  // lanes leave the visit loop as they finish: the wave's count
@@ -666,35 +697,52 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster
             seg_visits = 0;
             ++cur_seg;
         }
-        if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
-        for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
-            const int j = q / kRecF4, k = q % kRecF4;
-            if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+        const int nb = min(kStep, rng.y - b0);
+        int my_gid = 0;  // ONE: lane k <-> position b0 + k
+        if constexpr (ONE) {
+            if (__all(done)) break;
+            if (lane < nb) my_gid = sorted_ids[b0 + lane];
+        } else {
+            if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
+            for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
+                const int j = q / kRecF4, k = q % kRecF4;
+                if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+            }
+            if (GSTEX_FWD_SLOAD && tid < kFwdBatch && b0 + tid < rng.y) s_gid[tid] = sorted_ids[b0 + tid];
+            __syncthreads();
         }
-        if (GSTEX_FWD_SLOAD && tid < kFwdBatch && b0 + tid < rng.y) s_gid[tid] = sorted_ids[b0 + tid];
-        __syncthreads();
-        const int nb = min(kFwdBatch, rng.y - b0);
-        // the batch splats whose contribution box meets this wave's 16x4 block, tested all at once
-        unsigned long long todo[kFwdBatch / 64];
+        // the batch splats whose contribution region meets this wave's 8x8 block, tested all at once
+        unsigned long long todo[kWords];
 #pragma unroll
-        for (int hb = 0; hb < kFwdBatch / 64; ++hb) {
+        for (int hb = 0; hb < kWords; ++hb) {
             const int jj = hb * 64 + lane;
-            todo[hb] = __ballot(jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa));
+            bool hit = false;
+            if constexpr (ONE) {
+                if (jj < nb) {
+                    const float4* rc = records + (size_t)my_gid * kRecF4;
+                    hit = may_hit_planes(rc[0], rc[1], rc[2], wx0, wx1, wy0, wy1, aa);
+                }
+            } else {
+                hit = jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa);
+            }
+            todo[hb] = __ballot(hit);
             GSTEX_STAT(8, (unsigned long long)max(0, min(64, nb - hb * 64)));  // cull candidates (wave, splat)
             GSTEX_STAT(9, __popcll(todo[hb]));                                 // passing the wave's cull
             // hand the cull to the backward, which visits these splats up to the wave's last contributor
             if (visit_masks && lane == 0 && hb * 64 < nb)
                 visit_masks[(vm_base + ((b0 - rng.x) >> 6) + hb) * 4 + wave] = todo[hb];
         }
-        for (int hb = 0; hb < kFwdBatch / 64 && !done; ++hb) {
+        for (int hb = 0; hb < kWords && !done; ++hb) {
           unsigned long long m = todo[hb];
           while (m) {
             if (done) break;
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
             ++seg_visits;
-            const Rec r = GSTEX_FWD_SLOAD ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
-                                         : read_rec<kFwdBatch>(s_rec, j);
+            Rec r;
+            if constexpr (ONE) r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(my_gid, j) * kRecF4);
+            else r = GSTEX_FWD_SLOAD ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
+                                     : read_rec<kFwdBatch>(s_rec, j);
             Hit h;
             const bool ok = eval_hit(r, px, py, aa, h);
             GSTEX_STATW(10, 1);                                   // visits (the wave evaluates a splat)
@@ -1356,7 +1404,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // the (pair, quadrant) row: lanes 8k hold NP / 8 consecutive values each; the flag (1: 24-value
                 // row, 2: 32-value row) marks it written
                 const int slot = __builtin_amdgcn_readlane(my_slot, j);
-                if ((lane & 7) == 0) {
+                if ((lane & 7) == 0 && !(GSTEX_ABLATE & 256)) {
                     constexpr int E = NP / 8;
                     const int base = (NP / 2) * ((lane >> 5) & 1) + (NP / 4) * ((lane >> 4) & 1) + E * ((lane >> 3) & 1);
                     float* dst = partials + ((size_t)slot * 4 + quad) * kRowStride + base;
@@ -1368,7 +1416,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                         dst[2] = P[2];
                     }
                 }
-                if (lane == 0) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
+                if (lane == 0 && !(GSTEX_ABLATE & 256)) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
             }
             if (__any(tkey >= 0)) {
                 // fixed point for this visit: every staged entry receives at most vis_M in value units (bilinear
@@ -1840,12 +1888,18 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
     if (aux && hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
         return launch_status("gstex_raster_fwd (aux)");
 #define GSTEX_FWD(CC, GG)                                                                                      \
-    raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(dc, tiles_x, settings, background, channels,      \
-                                                     (const float4*)records, (const int2*)tile_ranges,        \
-                                                     tile_order, sorted_ids, texture, (int)n_texels, tex_scale,        \
-                                                     tex_bias, out_img,                                                   \
-                                                     out_depth, out_reg,                                                  \
-                                                     out_alpha, out_tex, out_normal, (float4*)state, ap)
+    do {                                                                                                       \
+        if (GSTEX_FWD_WAVE)                                                                                    \
+            raster_fwd_kernel<CC, GG, true><<<(unsigned)(((nblk + 7) / 8) * 32), 64, 0, st>>>(                \
+                dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, \
+                tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth,       \
+                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk);                            \
+        else                                                                                                   \
+            raster_fwd_kernel<CC, GG, false><<<nblk, kThreads, 0, st>>>(                                      \
+                dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, \
+                tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth,       \
+                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk);                            \
+    } while (0)
     if (channels == 3 && geo) GSTEX_FWD(3, true);
     else if (channels == 3) GSTEX_FWD(3, false);
     else if (channels == 6 && geo) GSTEX_FWD(6, true);

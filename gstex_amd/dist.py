@@ -148,6 +148,33 @@ class GradSync:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
 
+    def all_reduce_and_step(self, step_tail, step_head):
+        """A data-parallel optimizer step with the collectives overlapped (the trainer's optimizer_step(sync=...)).
+
+        The tail collective (the texel store, started from the raster backward) is followed on the wire by the head's;
+        step_tail(scale) runs as soon as the tail is reduced, so the texel group's update (73 % of the parameters)
+        overlaps the head collective, then step_head(scale) after it.  Both get scale = 1 / world to apply to the
+        SUMMED gradients (FusedAdam grad_scale: the same fp32 product as averaging first, without the separate pass
+        over the buffer), so after this call the buffer holds sums, not averages.  Without a running tail collective
+        (overlap_tail=False, or no backward hook fired) this is all_reduce() followed by both steps at scale 1."""
+        work, self._work = self._work, None
+        params = self._params()
+        if work is None or self._layout(params) != self._key:
+            if work is not None:
+                work.wait()
+                raise RuntimeError("GradSync.all_reduce_and_step(): the parameters changed between backward and the "
+                                   "step (call zero() after a rechart, before the backward)")
+            self.all_reduce()
+            step_tail(1.0)
+            step_head(1.0)
+            return
+        self._reattach(params, skip_tail=True)
+        head = dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        work.wait()
+        step_tail(1.0 / self.world)
+        head.wait()
+        step_head(1.0 / self.world)
+
     def _reattach(self, params, skip_tail=False):
         """Point every .grad back at its slice of `flat`, copying a detached gradient in (None: zero, except the
         texel store's slice when the raster backward accumulated straight into it -- the sink)."""

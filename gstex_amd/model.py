@@ -315,7 +315,19 @@ class GStexTrainer:
         loss.backward()
         return StepOutput(loss.detach(), rgb.detach())
 
-    def optimizer_step(self):
+    def optimizer_step(self, sync=None):
+        """The Adam step.  With a gstex_amd.dist.GradSync `sync` (data-parallel training) the gradient exchange is part
+        of the step: the texel group is updated as soon as its collective lands, overlapping the head's collective,
+        and the 1 / world averaging rides in the fused update (GradSync.all_reduce_and_step); otherwise call
+        sync.all_reduce() before this."""
+        if sync is not None and self.fused_adam and not self.async_texture:
+            tex = {id(self.texture_dc)}
+            sync.all_reduce_and_step(lambda s: self.optimizer.step(only=tex, grad_scale=s),
+                                     lambda s: self.optimizer.step(skip=tex, grad_scale=s))
+            self.step += 1
+            return
+        if sync is not None:
+            sync.all_reduce()
         if not self.async_texture:
             self.optimizer.step()
             self.step += 1

@@ -20,12 +20,13 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
 
     @torch.no_grad()
-    def step(self, closure=None, only=None, skip=None, zero_grad=False, grid=0):
+    def step(self, closure=None, only=None, skip=None, zero_grad=False, grid=0, grad_scale=1.0):
         """The Adam update.  Extensions (not in torch.optim.Adam): `only` / `skip` (sets of id(param)) restrict the
         update to / exclude a set of parameters (so one group can be launched on another stream), and `zero_grad` writes zeros over each
         gradient after reading it (gstex_adam_step_ex, GSTEX_ADAM_ZERO_GRAD); `grid` > 0 caps the launch's
-        workgroups (GSTEX_ADAM_GRID: each loops over the chunks), leaving CUs to another stream.  The launch goes to
-        the current stream."""
+        workgroups (GSTEX_ADAM_GRID: each loops over the chunks), leaving CUs to another stream; `grad_scale` in (0, 1]
+        multiplies every gradient as it is read (gstex_adam_step_scaled: a data-parallel step's 1 / world, applied to the
+        all-reduced sums -- bit-identical to averaging the buffer first).  The launch goes to the current stream."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -63,8 +64,11 @@ class FusedAdam(torch.optim.Optimizer):
             for i in range(0, len(items), _lib.ADAM_MAX_TENSORS):
                 chunk = items[i:i + _lib.ADAM_MAX_TENSORS]
                 arr = (_lib.GstexAdamTensor * len(chunk))(*[d for d, _ in chunk])
-                if zero_grad or grid:
-                    flags = (_lib.ADAM_ZERO_GRAD if zero_grad else 0) | ((int(grid) & 0xFFFF) << _lib.ADAM_GRID_SHIFT)
+                flags = (_lib.ADAM_ZERO_GRAD if zero_grad else 0) | ((int(grid) & 0xFFFF) << _lib.ADAM_GRID_SHIFT)
+                if grad_scale != 1.0:
+                    _lib.call("gstex_adam_step_scaled", len(chunk), arr, float(b1), float(b2), float(eps), flags,
+                              float(grad_scale), st)
+                elif flags:
                     _lib.call("gstex_adam_step_ex", len(chunk), arr, float(b1), float(b2), float(eps), flags, st)
                 else:
                     _lib.call("gstex_adam_step", len(chunk), arr, float(b1), float(b2), float(eps), st)

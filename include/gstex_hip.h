@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 6
+#define GSTEX_ABI_VERSION 7
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -277,6 +277,12 @@ int gstex_adam_step(int32_t n_tensors, const gstex_adam_tensor* tensors, double 
 #define GSTEX_ADAM_GRID(n) (((n) & 0xFFFF) << GSTEX_ADAM_GRID_SHIFT)
 int gstex_adam_step_ex(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                        double eps, int32_t flags, void* stream);
+/* gstex_adam_step_ex with every gradient read as grad * grad_scale, grad_scale in (0, 1] (ABI 7): a data-parallel
+ * step passes 1 / world_size and skips the separate averaging pass over the all-reduced gradient buffer (the same
+ * fp32 product, so the update is bit-identical).  Replaces, with GStex's GradSync, the 1 / world averaging of the
+ * reference's DDP (pipelines/base_pipeline.py:281-283). */
+int gstex_adam_step_scaled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                           double eps, int32_t flags, float grad_scale, void* stream);
 
 #ifdef __cplusplus
 }

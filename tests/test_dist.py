@@ -153,6 +153,20 @@ def _trainer_worker(rank, world, port, q):
             ok = ok and bool(torch.all(tr.features_dc.grad == 0))
             ok = ok and tr.means.grad.data_ptr() == sync.flat.data_ptr()  # re-attached to the buffer
             res[f"set_to_none_{step}"] = bool(ok)
+        # the overlapped exchange inside the optimizer step (GStexTrainer.optimizer_step(sync=...)): the texel step
+        # runs once the tail collective has landed, the head step after the head collective; both see SUMS and the
+        # scale 1 / world
+        sync.zero()
+        tr.backward(rank)
+        calls = []
+        sync.all_reduce_and_step(lambda sc: calls.append(("tail", sc, tr.texture_dc.grad.clone())),
+                                 lambda sc: calls.append(("head", sc, tr.means.grad.clone(), tr.features_dc.grad.clone())))
+        sum_w = mean_w * world
+        res["overlap_order"] = [c[0] for c in calls] == ["tail", "head"]
+        res["overlap_scale"] = all(abs(c[1] - 1.0 / world) < 1e-15 for c in calls)
+        res["overlap_sums"] = bool(torch.allclose(calls[0][2], sum_w * tr.texture_dc.detach())
+                                   and torch.allclose(calls[1][2], torch.full_like(tr.means, sum_w))
+                                   and torch.all(calls[1][3] == 0))
         # a second backward without all_reduce() in between is refused: by zero(), and by the sink's ready callback
         # (its kernel would add into the slice the running collective reads)
         sync.zero()
@@ -192,5 +206,6 @@ def test_trainer_layout_sink_and_recharts_world2():
         assert r["rebuilt_1"], "a grown texel store must rebuild the flat buffer"
         assert r["double_backward_refused"]
         assert r["double_backward_sink_refused"]
+        assert r["overlap_order"] and r["overlap_scale"] and r["overlap_sums"], r
         for step in range(2):
             assert r[f"set_to_none_{step}"], f"rank {rank}: zero_grad(set_to_none) after zero() mis-reduced (step {step})"

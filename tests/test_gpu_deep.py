@@ -5,7 +5,10 @@ tolerances of test_gpu_parity.py, on windows of the bench scenes themselves.
   the forward's batch loop runs >10 batches and the backward's reverse walk >100, with transmittance
   saturation (early termination) inside the lists;
 * cfg2 (50k splats, 1e6 texels, 800x800): the 128x128 centre window;
-* cfg1 exactly (1k splats, 0 texels = 2DGS mode, 256x256): the whole image.
+* cfg1 exactly (1k splats, 0 texels = 2DGS mode, 256x256): the whole image;
+* cfg5's per-GPU raster (DTU-like stand-in: 200k splats, 1e7 texels, 1600x1200; the COLMAP init is absent): a
+  48x48 window at the image centre with every output (depth, distortion, normal) and their gradients (the GEO
+  backward), ~2,500 splats per tile.
 """
 import numpy as np
 import pytest
@@ -60,6 +63,11 @@ def test_cfg3_centre_window_deep_tiles():
 def test_cfg3_centre_window_all_outputs():
     case = make_window_case(200_000, 1e7, 800, 800, 48)
     _check("cfg3 48x48 all outputs", case, min_depth=1500)
+
+
+def test_cfg5_window_all_outputs():
+    case = make_window_case(200_000, 1e7, 1200, 1600, 48, seed=24)
+    _check("cfg5 48x48 all outputs", case, min_depth=1500)
 
 
 def test_cfg2_centre_window():

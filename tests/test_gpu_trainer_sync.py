@@ -44,8 +44,11 @@ def test_synced_step_matches_unsynced_across_rechart():
             synced.forward_backward(views[step % 3], gts[step % 3])
             assert synced.texture_grad_sink is not None and synced.texture_dc.grad.data_ptr() == \
                 sync.flat[sync._tail_off:].data_ptr()
-            sync.all_reduce()
-            synced.optimizer_step()
+            if step % 2 == 0:
+                sync.all_reduce()
+                synced.optimizer_step()
+            else:  # the exchange inside the step: texel group first, head after its collective (RCCL, world 1)
+                synced.optimizer_step(sync=sync)
             if step in (1, 2):
                 # step 1: charts for 90 % of the store's rows (fit: the Parameter and the flat buffer are kept);
                 # step 2: 130 % (the store grows: a new Parameter, a new buffer and sink at the next zero())

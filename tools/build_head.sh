@@ -1,10 +1,11 @@
 #!/bin/bash
-# Builds the library from the committed HEAD sources into scratch/prev/ (A/B baseline for tools/gpu_ablate.sh).
+# The committed HEAD as a whole tree in scratch/head (sources + its own python + built library): tools/gpu_check.sh
+# times it beside the working tree (A/B across ABI changes, since each tree loads its own library).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-rm -rf "$ROOT/scratch/prev_csrc" "$ROOT/scratch/prev"
-mkdir -p "$ROOT/scratch/prev_csrc"
+rm -rf "$ROOT/scratch/head"
+mkdir -p "$ROOT/scratch/head"
 cd "$ROOT"
-for f in $(git ls-files gstex_amd/csrc); do git show HEAD:$f > scratch/prev_csrc/$(basename $f); done
-make -s -C scratch/prev_csrc -j8 OBJDIR="$ROOT/scratch/prev/obj" OUT="$ROOT/scratch/prev/libgstex_hip.so"
-echo "built scratch/prev (HEAD)"
+git archive HEAD | tar -x -C scratch/head
+make -s -C scratch/head/gstex_amd/csrc -j8
+echo "built scratch/head (HEAD $(git rev-parse --short HEAD))"

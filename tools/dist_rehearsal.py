@@ -11,7 +11,8 @@ and step, scripts/train.py:97, full_images_datamanager.py:320, DDP averaging pip
 Exercised, per step:
   * the raster backward accumulating the texel gradient into the flat buffer's slice (the sink) and the tail
     collective started from on_texture_grad (asserted: GradSync._work is set before all_reduce());
-  * the head all-reduce, 1/world averaging, the 7-group FusedAdam;
+  * the head all-reduce, 1/world averaging, the 7-group FusedAdam; from step 1 on the overlapped exchange inside
+    GStexTrainer.optimizer_step(sync=...) (texel group updated while the head collective runs, 1/world in the update);
   * step 1: trainer.zero_grad() (set_to_none) AFTER sync.zero() -- autograd then writes detached .grad tensors,
     which all_reduce() must fold back into the buffer (ADVICE r02 medium);
   * after step 1: a rechart that GROWS the texel store (new Parameter, new flat buffer and sink at the next zero()).
@@ -74,8 +75,11 @@ def main():
             tr.zero_grad()  # set_to_none after zero(): detached autograd .grad tensors, folded back by all_reduce()
         tr.forward_backward(views[pose], gts[pose])
         started = sync._work is not None
-        sync.all_reduce()
-        tr.optimizer_step()
+        if step == 0:  # the plain exchange: averaged gradient buffer, then the step
+            sync.all_reduce()
+            tr.optimizer_step()
+        else:  # the overlapped exchange inside the step (texel update during the head collective, 1/world in Adam)
+            tr.optimizer_step(sync=sync)
         flags = torch.tensor([1.0 if started else 0.0], device=dev)
         dist.all_reduce(flags, op=dist.ReduceOp.MIN)
         say(f"step {step}: poses {[(r + step * world) % N_POSES for r in range(world)]}, tail collective started "
