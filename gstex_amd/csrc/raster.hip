@@ -580,16 +580,17 @@ __device__ __forceinline__ float tex_accum(float acc, float v00, float v01, floa
 }
 // GEOF = false: depth / distortion / normal not produced (their outputs are NULL: a caller whose loss does
 // not use them, e.g. the photometric training step); every other output is computed unchanged.
-// ONE = true (the default, GSTEX_FWD_WAVE): one wave64 workgroup per (tile, 8x8 quadrant) -- no barriers, no record
+// ONE = true (GSTEX_FWD_WAVE=1, an experiment): one wave64 workgroup per (tile, 8x8 quadrant) -- no barriers, no record
 // staging shared between the quadrants; each wave culls a 64-position word of the tile list at a time (lane k tests
 // position k from the record's first three planes, the cull fields) and reads each visited record with scalar loads
-// (as the backward does).  ONE = false: the round-2 form, one 256-thread workgroup per tile whose four quadrant waves
-// share 128-record batches staged in LDS (barrier per batch).
+// (as the backward does).  ONE = false (the default): one 256-thread workgroup per tile whose four quadrant waves share
+// 128-record batches staged in LDS (barrier per batch) -- 12 % faster: the shared staging reads each record once per
+// tile instead of once per quadrant and the quadrants' culls read LDS instead of gathering 48 B per candidate.
 template <bool ONE> struct FwdShape;
 template <> struct FwdShape<false> { static constexpr int kThr = kThreads, kStep = kFwdBatch; };
 template <> struct FwdShape<true> { static constexpr int kThr = 64, kStep = 64; };
 #ifndef GSTEX_FWD_WAVE
-#define GSTEX_FWD_WAVE 1
+#define GSTEX_FWD_WAVE 0  // measured at cfg3 (round 3): single-wave 0.666 ms (6 waves/SIMD), 0.677 (7), 0.752 (8) vs 0.592
 #endif
 #ifndef GSTEX_FWD1_OCC
 #define GSTEX_FWD1_OCC 8  // single-wave forward: waves per SIMD the register allocation targets
