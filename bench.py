@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_TAG = "r02"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+PROFILE_TAG = "r03"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
 N_POSES = 8
 
 
@@ -332,7 +332,13 @@ def main():
                     fwd_bwd_frac=round((ab["fwd"] + ab["bwd"]) / ((f_ms + b_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
     prow = pmc_row(dom)
     if prow is not None:
+        # 2 FETCH + WRITE: the gfx950 x2 FETCH_SIZE correction holds for vector loads of every width the kernels use
+        # but scalar loads count x1 (profiles/r03_fetch_calibration.json), so with the backward's scalar record reads
+        # this is an upper bound; FETCH + WRITE (all loads scalar) is the lower bound
         roofline["traffic"] = int(prow["hbm_bytes_per_launch"])
+        if prow.get("fetch_kib") is not None and prow.get("write_kib") is not None:
+            roofline["traffic_lower_bound"] = int((prow["fetch_kib"] + prow["write_kib"]) * 1024)
+            roofline["traffic_calibration"] = "profiles/r03_fetch_calibration.json"
         if prow.get("valu_insts"):
             # the kernel is VALU-issue/latency bound, not HBM bound: its issue roofline, live time
             roofline["valu_insts_per_launch"] = int(prow["valu_insts"])

@@ -1423,10 +1423,16 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // fixed point for this visit: every staged entry receives at most vis_M in value units (bilinear
                 // weights <= 1), so at scale 2^S, S = 30 - e (vis_M < 2^e), the tails (each < 2^30) and their int32
                 // sums stay in range; resolution 2^-30 of the visit's total
-                int e_m = 0;
-                if (kTexFixed && vis_M > 0.f) (void)frexpf(vis_M, &e_m);
-                const int tex_S = kTexFixed ? kTexFixBits - e_m : 0;
-                const float twq = kTexFixed ? tw * __builtin_ldexpf(1.0f, tex_S) : tw;
+                // S = 30 - e with vis_M = m 2^e, m in [0.5, 1) (frexp), from the float's exponent field on the scalar
+                // unit (vis_M is wave-uniform); 2^S and 2^-S are built as float bit patterns, so the scalings below
+                // are exact multiplies (what ldexp computed); S is clamped to [-126, 126] (denormal / zero bounds)
+                const uint32_t mbits = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(vis_M));
+                const int biased = (int)((mbits >> 23) & 0xFFu);
+                const int e_m = (kTexFixed && biased > 0) ? biased - 126 : 0;
+                const int tex_S = kTexFixed ? min(max(kTexFixBits - e_m, -126), 126) : 0;
+                const float pow_S = __uint_as_float((uint32_t)(tex_S + 127) << 23);     // 2^S
+                const float pow_mS = __uint_as_float((uint32_t)(127 - tex_S) << 23);    // 2^-S
+                const float twq = kTexFixed ? tw * pow_S : tw;
                 float tg[4 * CM];
                 {
 #pragma clang fp contract(fast)
@@ -1466,8 +1472,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     } else {
                         // block larger than the staging area: straight to global, back in value units
                         float* base = v_texture + (size_t)r.off * Cn;
-                        const int uS = -tex_S;
-                        auto val = [&](float y) { return kTexFixed ? __builtin_ldexpf(y, uS) : y; };
+                        auto val = [&](float y) { return kTexFixed ? y * pow_mS : y; };
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
@@ -1495,7 +1500,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                             GSTEX_STAT(6, __popcll(__ballot(v[k] != 0)));
                             if (v[k] == 0) continue;
                             s_texq[e0 + 64 * k] = 0;
-                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, kTexFixed ? __builtin_ldexpf((float)v[k], -tex_S) : (float)v[k]);
+                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, kTexFixed ? (float)v[k] * pow_mS : (float)v[k]);
                         }
                     }
                 }

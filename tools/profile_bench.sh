@@ -5,7 +5,7 @@
 #   4. --pmc SQ_INSTS_VALU SQ_WAVES (wave-level VALU instructions per launch: the issue roofline)
 # Output: gpurun_out/prof_<tag>/...; summarise locally with tools/summarize_profiles.py <tag>.
 set -e
-TAG=${1:-r01}
+TAG=${1:-r03}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
