@@ -259,14 +259,13 @@ def main():
     sync = GradSync(trainer, world) if world > 1 else None
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     gts = [torch.rand((H, W, 3), generator=g).to(dev) for _ in range(N_POSES)]
-    geom = [trainer.means, trainer.scales, trainer.quats, trainer.opacities]
-    geom0 = [p.detach().clone() for p in geom]
+    geom0 = trainer.geometry_flat.detach().clone()  # means / log-scales / quats / opacity logits, one allocation
     setup_s = time.perf_counter() - t_scene
     step_no = [0]
 
     def step():
-        with torch.no_grad():  # stationary workload: same geometry every step (8.8 MB copy, timed, one launch)
-            torch._foreach_copy_(geom, geom0)
+        with torch.no_grad():  # stationary workload: same geometry every step (8.8 MB, one copy, timed)
+            trainer.geometry_flat.copy_(geom0)
         pose = (rank + step_no[0] * world) % N_POSES
         step_no[0] += 1
         if sync is not None:

@@ -16,9 +16,10 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 REC_FLOATS = 32
-PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows (24 or 32 used)
+PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
+PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
 SETTING_AA_BLUR = 1 << 9
 SETTING_DIST_REG = 1 << 10
 SETTING_EDIT = 1 << 13
@@ -73,6 +74,10 @@ SIGNATURES = {
         c_int32,
         [c_int32, c_int64, _P, _P, _P, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, c_size_t, _P],
     ),
+    "gstex_bin_sort_ordered": (
+        c_int32,
+        [c_int32, c_int64, _P, _P, _P, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_size_t, _P],
+    ),
     "gstex_tile_order": (c_int32, [c_int32, _P, _P, _P]),
     "gstex_raster_setup": (
         c_int32,
@@ -93,11 +98,11 @@ SIGNATURES = {
     ),
     "gstex_raster_setup_bwd": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_setup_bwd_aabb": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_sh_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),

@@ -597,11 +597,13 @@ extern "C" size_t gstex_bin_workspace_size(int32_t n, int64_t n_isect, int32_t n
     return bin_layout(n_tiles, n_isect, nullptr, nullptr);
 }
 
-extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float* extents,
-                              const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
-                              int32_t H, int32_t W, int32_t block, int32_t* tile_ranges, int32_t* sorted_ids,
-                              int32_t* sorted_slots, void* workspace, size_t workspace_bytes, void* stream) {
-    (void)num_tiles_hit;
+namespace {
+// tile_order_out (nullable): the largest-first launch order the tile sort used, identical to what
+// gstex_tile_order computes from tile_ranges (both rank the same bucket sizes), so the forward reuses it
+int bin_sort_impl(int32_t n, int64_t n_isect, const float* centers, const float* extents, const float* depths,
+                  const int32_t* offsets, int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
+                  int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order_out, void* workspace,
+                  size_t workspace_bytes, void* stream) {
     GSTEX_REQUIRE(n >= 0 && n_isect >= 0 && n_isect < (1ll << 31) && H > 0 && W > 0 && block > 0,
                   "gstex_bin_sort: invalid sizes (n=%d, n_isect=%lld, H=%d, W=%d, block=%d)", n,
                   (long long)n_isect, H, W, block);
@@ -615,6 +617,7 @@ extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, 
     hipStream_t st = as_stream(stream);
     if (n_isect == 0) {
         (void)hipMemsetAsync(tile_ranges, 0, (size_t)n_tiles * 2 * sizeof(int32_t), st);
+        if (tile_order_out) iota_kernel<<<div_up(n_tiles, 256), 256, 0, st>>>(n_tiles, tile_order_out);
         return launch_status("gstex_bin_sort(empty)");
     }
     GSTEX_REQUIRE(centers && extents && depths && offsets && sorted_ids && sorted_slots,
@@ -633,12 +636,36 @@ extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, 
     place_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, depths, offsets, tiles_x, tiles_y, block,
                                                   ws.tile_start, ws.rank, ws.keys, ws.slot_gid);
     const bool ranked = n_tiles <= kOrderCap;
+    int32_t* order = tile_order_out ? tile_order_out : ws.order;
     if (ranked)
-        tile_rank_kernel<1><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, st>>>(n_tiles, ws.tile_start, ws.order);
-    tile_sort_kernel<<<n_tiles, kSortThreads, 0, st>>>(n_tiles, ranked ? ws.order : nullptr, ws.tile_start, ws.keys,
+        tile_rank_kernel<1><<<div_up(n_tiles, kRankTiles), kRankThreads, 0, st>>>(n_tiles, ws.tile_start, order);
+    else if (tile_order_out)  // beyond the ranking's budget: row-major, as gstex_tile_order
+        iota_kernel<<<div_up(n_tiles, 256), 256, 0, st>>>(n_tiles, tile_order_out);
+    tile_sort_kernel<<<n_tiles, kSortThreads, 0, st>>>(n_tiles, ranked ? order : nullptr, ws.tile_start, ws.keys,
                                                        ws.scratch, ws.slot_gid, tile_ranges, sorted_ids,
                                                        sorted_slots);
     return launch_status("gstex_bin_sort");
+}
+}  // namespace
+
+extern "C" int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float* extents,
+                              const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                              int32_t H, int32_t W, int32_t block, int32_t* tile_ranges, int32_t* sorted_ids,
+                              int32_t* sorted_slots, void* workspace, size_t workspace_bytes, void* stream) {
+    (void)num_tiles_hit;
+    return bin_sort_impl(n, n_isect, centers, extents, depths, offsets, H, W, block, tile_ranges, sorted_ids,
+                         sorted_slots, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gstex_bin_sort_ordered(int32_t n, int64_t n_isect, const float* centers, const float* extents,
+                                      const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                                      int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
+                                      int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+    (void)num_tiles_hit;
+    GSTEX_REQUIRE(tile_order, "gstex_bin_sort_ordered: null tile_order");
+    return bin_sort_impl(n, n_isect, centers, extents, depths, offsets, H, W, block, tile_ranges, sorted_ids,
+                         sorted_slots, tile_order, workspace, workspace_bytes, stream);
 }
 
 extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int32_t* tile_order, void* stream) {

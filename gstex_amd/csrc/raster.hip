@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if ((lane & 7) == 0 && !(GSTEX_ABLATE & 256)) {
                     constexpr int E = NP / 8;
                     const int base = (NP / 2) * ((lane >> 5) & 1) + (NP / 4) * ((lane >> 4) & 1) + E * ((lane >> 3) & 1);
-                    float* dst = partials + ((size_t)slot * 4 + quad) * kRowStride + base;
+                    float* dst = partials + ((size_t)slot * 4 + quad) * NP + base;  // rows NP floats apart
                     if constexpr (E == 4) {
                         *reinterpret_cast<float4*>(dst) = make_float4(P[0], P[1], P[2], P[3]);
                     } else {
@@ -1541,10 +1541,13 @@ constexpr int kSumSlots = GSTEX_SUM_SLOTS;  // slots whose rows one lane group h
 // 32 lanes per splat: lane 8 q + m reads float4 m (columns 4m .. 4m+3) of the quadrant-q rows, kSumSlots slots at a
 // time, and sums them in slot order; the 4 quadrant sums are then combined (q0 + q1) + (q2 + q3) across lanes.
 // Deterministic (fixed order), like the fused kernel's slot-major quadrant-minor order it replaces.
+// rs = floats between rows: kPartRow (24) when the backward had no depth / normal / distortion gradient, else
+// kPartRowGeo (32).  The sums (32 values, the last 8 zero for 24-value rows) go over the splat's first row; with rs =
+// 24 they reach into its second row, which only this splat's lanes read, before (program order) the store.
 __global__ __launch_bounds__(256) void setup_bwd_sum_kernel(int n, const int32_t* __restrict__ nth,
                                                            const int32_t* __restrict__ offsets,
                                                            float* __restrict__ partials,
-                                                           const uint32_t* __restrict__ row_flags) {
+                                                           const uint32_t* __restrict__ row_flags, int rs) {
     const int l = threadIdx.x & 31, q = l >> 3, m = l & 7;
     const int g = blockIdx.x * 8 + (threadIdx.x >> 5);
     const bool live = g < n;
@@ -1552,7 +1555,7 @@ __global__ __launch_bounds__(256) void setup_bwd_sum_kernel(int n, const int32_t
     const size_t s0 = live ? (size_t)offsets[g] : 0;
     // columns 24.. exist only in 32-value rows (flag 2: backward with depth / normal gradients)
     const uint32_t need = m < kPartRow / 4 ? 0xFFu : 0x02u;
-    const float4* rows = reinterpret_cast<const float4*>(partials + s0 * 4 * kRowStride) + q * (kRowStride / 4) + m;
+    const float4* rows = reinterpret_cast<const float4*>(partials + s0 * 4 * rs) + q * (rs / 4) + m;
     const uint32_t* fl = row_flags + s0;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int e = 0; e < cnt; e += kSumSlots) {
@@ -1562,7 +1565,7 @@ __global__ __launch_bounds__(256) void setup_bwd_sum_kernel(int n, const int32_t
         float4 r[kSumSlots];
 #pragma unroll
         for (int u = 0; u < kSumSlots; ++u)
-            r[u] = (f[u] >> (8 * q)) & need ? rows[(size_t)(e + u) * (4 * kRowStride / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+            r[u] = (f[u] >> (8 * q)) & need ? rows[(size_t)(e + u) * rs] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int u = 0; u < kSumSlots; ++u) {
             if ((f[u] >> (8 * q)) & need) {
@@ -1582,7 +1585,7 @@ __global__ __launch_bounds__(256) void setup_bwd_sum_kernel(int n, const int32_t
     acc = xadd(acc, 16);
     // the sums over the splat's first row, whose values every lane has read above: no other splat reads it
     if (live && cnt > 0 && q == 0)
-        reinterpret_cast<float4*>(partials + s0 * 4 * kRowStride)[m] = acc;
+        reinterpret_cast<float4*>(partials + s0 * 4 * rs)[m] = acc;
 }
 
 template <bool FOLD_AABB>
@@ -1596,7 +1599,7 @@ template <bool FOLD_AABB>
 __global__ __launch_bounds__(256) void setup_bwd_chain_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
-    const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials,
+    const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials, int rs,
     CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
     float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers, float* __restrict__ v_uv0) {
     const int g = blockIdx.x * 256 + threadIdx.x;
@@ -1605,7 +1608,7 @@ __global__ __launch_bounds__(256) void setup_bwd_chain_kernel(
     const int cnt = nth[g];
     float S[kPartRowGeo];
     if (cnt > 0) {
-        const float4* src = reinterpret_cast<const float4*>(partials + (size_t)offsets[g] * 4 * kRowStride);
+        const float4* src = reinterpret_cast<const float4*>(partials + (size_t)offsets[g] * 4 * rs);
 #pragma unroll
         for (int i = 0; i < kPartRowGeo / 4; ++i) {
             const float4 v = src[i];
@@ -1624,7 +1627,7 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
     const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials,
-    const uint32_t* __restrict__ row_flags, CamArgs cam_args, float* __restrict__ v_means,
+    const uint32_t* __restrict__ row_flags, int rs, CamArgs cam_args, float* __restrict__ v_means,
     float* __restrict__ v_scales, float* __restrict__ v_quats, float* __restrict__ v_rgbs, float* __restrict__ v_opac,
     float* __restrict__ v_centers, float* __restrict__ v_uv0) {
     // phase 1: 32 lanes per splat, lane c sums column c of the splat's flagged (slot, quadrant) rows in slot-major,
@@ -1642,7 +1645,7 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
             if (g0 + j < n) {
                 const int cnt = nth[g0 + j];
                 const size_t s0 = (size_t)offsets[g0 + j];
-                const float* src = partials + s0 * 4 * kRowStride + c;
+                const float* src = partials + s0 * 4 * rs + c;
                 const uint32_t* fl = row_flags + s0;
                 // groups of kSetupBwdInflight slots: their flag words, then every flagged row of the group, are
                 // loaded before any is summed (most splats hit fewer tiles than one group holds)
@@ -1655,7 +1658,7 @@ __global__ __launch_bounds__(256) void setup_bwd_kernel(
                     for (int u = 0; u < kSetupBwdInflight; ++u)
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
-                            r[4 * u + q] = (f[u] >> (8 * q)) & need ? src[((size_t)(e + u) * 4 + q) * kRowStride] : 0.f;
+                            r[4 * u + q] = (f[u] >> (8 * q)) & need ? src[((size_t)(e + u) * 4 + q) * rs] : 0.f;
 #pragma unroll
                     for (int u = 0; u < kSetupBwdInflight; ++u)
 #pragma unroll
@@ -1972,17 +1975,17 @@ extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32
 template <bool FOLD_AABB>
 int setup_bwd_launch(int32_t n, const float* means, const float* scales, float glob_scale, const float* quats,
                      const float* umap, const float* vmap, const int32_t* nth, const int32_t* offsets,
-                     float* partials, const uint32_t* row_flags, const gstex_camera* cam, float* v_means,
+                     float* partials, const uint32_t* row_flags, int32_t rs, const gstex_camera* cam, float* v_means,
                      float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                      float* v_uv0, hipStream_t st, const char* name) {
     if (GSTEX_SETUP_SPLIT) {
-        setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags);
+        setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags, rs);
         setup_bwd_chain_kernel<FOLD_AABB><<<div_up(n, 256), 256, 0, st>>>(
-            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, to_device_camera(*cam), v_means,
+            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, rs, to_device_camera(*cam), v_means,
             v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     } else {
         setup_bwd_kernel<FOLD_AABB><<<div_up(n, kSetupBwdSplats), 256, 0, st>>>(
-            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, row_flags,
+            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, row_flags, rs,
             to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     }
     return launch_status(name);
@@ -1991,7 +1994,8 @@ int setup_bwd_launch(int32_t n, const float* means, const float* scales, float g
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                                       const float* quats, const float* opacities, const float* umap,
                                       const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      float* partials, const uint32_t* row_flags, const gstex_camera* cam,
+                                      float* partials, const uint32_t* row_flags, int32_t row_floats,
+                                      const gstex_camera* cam,
                                       float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
                                       float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
@@ -2000,15 +2004,18 @@ extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float
     GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd: null pointer");
+    GSTEX_REQUIRE(row_floats == kPartRow || row_floats == kPartRowGeo,
+                  "gstex_raster_setup_bwd: row_floats must be %d or %d (got %d)", kPartRow, kPartRowGeo, row_floats);
     return setup_bwd_launch<false>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
-                                   row_flags, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
+                                   row_flags, row_floats, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
                                    as_stream(stream), "gstex_raster_setup_bwd");
 }
 
 extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
                                       const float* quats, const float* opacities, const float* umap,
                                       const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      float* partials, const uint32_t* row_flags, const gstex_camera* cam,
+                                      float* partials, const uint32_t* row_flags, int32_t row_floats,
+                                      const gstex_camera* cam,
                                       float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
                                       float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
@@ -2017,8 +2024,10 @@ extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const 
     GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
                       v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
                   "gstex_raster_setup_bwd_aabb: null pointer");
+    GSTEX_REQUIRE(row_floats == kPartRow || row_floats == kPartRowGeo,
+                  "gstex_raster_setup_bwd_aabb: row_floats must be %d or %d (got %d)", kPartRow, kPartRowGeo, row_floats);
     return setup_bwd_launch<true>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
-                                   row_flags, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
+                                   row_flags, row_floats, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
                                    as_stream(stream), "gstex_raster_setup_bwd_aabb");
 }
 

@@ -110,10 +110,18 @@ class GStexTrainer:
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
-        self.means = P(scene.means)
-        self.scales = P(scene.log_scales)
-        self.quats = P(scene.quats)
-        self.opacities = P(scene.opacity_logits)
+        # the geometry parameters (what decides which (pixel, splat) pairs exist) share one allocation, each segment
+        # 16-B aligned (the fused Adam's float4 path): `geometry_flat` snapshots / restores all four in one copy
+        geo = [scene.means, scene.log_scales, scene.quats, scene.opacity_logits]
+        sizes = [int(t.numel()) for t in geo]
+        self.geometry_flat = torch.zeros(sum((n + 3) // 4 * 4 for n in sizes), device=d, dtype=torch.float32)
+        views, off = [], 0
+        for t, n in zip(geo, sizes):
+            v = self.geometry_flat[off:off + n].view(t.shape)
+            v.copy_(t.detach().to(d))
+            views.append(torch.nn.Parameter(v))
+            off += (n + 3) // 4 * 4
+        self.means, self.scales, self.quats, self.opacities = views
         self.features_dc = P(scene.features_dc)
         self.features_rest = P(scene.features_rest)
         # the texel parameter stores the SH-DC value; the raster reads SH2RGB of it (gstex.py:1119).  Like the

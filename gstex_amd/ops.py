@@ -13,7 +13,7 @@ from typing import Tuple
 import torch
 
 from . import _lib
-from ._lib import PARTIAL_FLOATS, REC_FLOATS, call, ptr
+from ._lib import PARTIAL_FLOATS, PARTIAL_FLOATS_PHOTO, REC_FLOATS, call, ptr
 
 BLOCK_WIDTH = 16
 
@@ -263,8 +263,10 @@ def bin_begin(num_tiles_hit):
     return nth, offsets, pending
 
 
-def bin_finish(begun, centers, extents, depths, H: int, W: int, block_width: int = BLOCK_WIDTH):
-    """Second half of bin_and_sort: wait for the pair count, size the pair buffers, bin and sort."""
+def bin_finish(begun, centers, extents, depths, H: int, W: int, block_width: int = BLOCK_WIDTH,
+               with_order: bool = False):
+    """Second half of bin_and_sort: wait for the pair count, size the pair buffers, bin and sort.  with_order:
+    also return the largest-first tile order the sort ranked (gstex_bin_sort_ordered; == tile_order(ranges))."""
     nth, offsets, pending = begun
     n = nth.shape[0]
     dev = nth.device
@@ -278,10 +280,15 @@ def bin_finish(begun, centers, extents, depths, H: int, W: int, block_width: int
     sorted_slots = torch.empty((n_isect,), device=dev, dtype=torch.int32)
     wsb = int(_lib.load().gstex_bin_workspace_size(n, n_isect, n_tiles))
     bws = torch.empty((max(wsb, 1),), device=dev, dtype=torch.uint8)
-    _launch("gstex_bin_sort", n, n_isect, ptr(centers.detach().contiguous()), ptr(extents.detach().contiguous()),
-         ptr(depths.detach().contiguous()), ptr(nth), ptr(offsets), int(H), int(W), int(block_width),
-         ptr(tile_ranges), ptr(sorted_ids), ptr(sorted_slots), ptr(bws), bws.numel(), st)
-    return offsets, tile_ranges, sorted_ids, sorted_slots
+    keep = [t.detach().contiguous() for t in (centers, extents, depths)]  # alive until the launch returns
+    geo = (ptr(keep[0]), ptr(keep[1]), ptr(keep[2]), ptr(nth), ptr(offsets), int(H), int(W), int(block_width),
+           ptr(tile_ranges), ptr(sorted_ids), ptr(sorted_slots))
+    if not with_order:
+        _launch("gstex_bin_sort", n, n_isect, *geo, ptr(bws), bws.numel(), st)
+        return offsets, tile_ranges, sorted_ids, sorted_slots
+    order = torch.empty((n_tiles,), device=dev, dtype=torch.int32)
+    _launch("gstex_bin_sort_ordered", n, n_isect, *geo, ptr(order), ptr(bws), bws.numel(), st)
+    return offsets, tile_ranges, sorted_ids, sorted_slots, order
 
 
 def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_width: int = BLOCK_WIDTH):
@@ -370,9 +377,8 @@ class _TextureGaussians(torch.autograd.Function):
                 ctx.v_texture = texture_grad_sink
             else:
                 ctx.v_texture = torch.zeros_like(texture)
-        offsets, tile_ranges, sorted_ids, sorted_slots = bin_finish(begun, centers_c.detach(), extents_c, depths_c,
-                                                                    H, W, BLOCK_WIDTH)
-        order = tile_order(tile_ranges)
+        offsets, tile_ranges, sorted_ids, sorted_slots, order = bin_finish(
+            begun, centers_c.detach(), extents_c, depths_c, H, W, BLOCK_WIDTH, with_order=True)
         ctx_scale, ctx_bias = (1.0, 0.0) if texture_transform is None else (float(texture_transform[0]),
                                                                              float(texture_transform[1]))
         f = dict(device=dev, dtype=torch.float32)
@@ -441,8 +447,11 @@ class _TextureGaussians(torch.autograd.Function):
         v_tex = g(v_tex, (H, W, C))
         v_normal = g(v_normal, (H, W, 3))
         n_isect = sorted_ids.shape[0]
-        # one partial row per (pair, 8x8 quadrant), written only where the quadrant contributes (row_flags)
-        partials = torch.empty((n_isect, 4, PARTIAL_FLOATS), device=dev, dtype=torch.float32)
+        # one partial row per (pair, 8x8 quadrant), written only where the quadrant contributes (row_flags); rows of 24
+        # floats without depth / normal / distortion gradients (gstex_raster_bwd), 32 with
+        geo = v_depth is not None or v_normal is not None or (v_reg is not None and bool(settings & (1 << 10)))
+        row_floats = PARTIAL_FLOATS if geo else PARTIAL_FLOATS_PHOTO
+        partials = torch.empty((n_isect, 4, row_floats), device=dev, dtype=torch.float32)
         row_flags = torch.empty((n_isect,), device=dev, dtype=torch.int32)
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
@@ -464,7 +473,7 @@ class _TextureGaussians(torch.autograd.Function):
         v_uv0 = torch.empty((n, 1, 2), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup_bwd_aabb" if ctx.fold_aabb else "gstex_raster_setup_bwd", n, ptr(means),
                 ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap), ptr(vmap), ptr(nth), ptr(offsets), ptr(partials),
-                ptr(row_flags), cam,
+                ptr(row_flags), row_floats, cam,
                 ptr(v_means), ptr(v_scales), ptr(v_quats), ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
         v_bg = None
         if ctx.needs_input_grad[26]:

@@ -38,12 +38,13 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 7
+#define GSTEX_ABI_VERSION 8
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
 /* Per-(tile, splat, quadrant) gradient partial row written by gstex_raster_bwd (floats). */
 #define GSTEX_PARTIAL_FLOATS 32
+#define GSTEX_PARTIAL_FLOATS_PHOTO 24
 
 /* settings bitfield (GStexModelConfig.settings, gstex.py:194-197) */
 #define GSTEX_SETTING_AA_BLUR (1 << 9)   /* 2DGS screen-space low-pass */
@@ -105,6 +106,15 @@ int gstex_bin_sort(int32_t n, int64_t n_isect, const float* centers, const float
                    int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
                    int32_t* sorted_ids, int32_t* sorted_slots, void* workspace,
                    size_t workspace_bytes, void* stream);
+/* gstex_bin_sort that also writes tile_order[n_tiles] (non-NULL), the largest-first launch order
+ * gstex_tile_order would compute from the resulting tile_ranges (same keys, same ranking): the
+ * tile sort already ranks the buckets, so the raster forward reuses that order instead of a
+ * second ranking launch.  ABI 8. */
+int gstex_bin_sort_ordered(int32_t n, int64_t n_isect, const float* centers, const float* extents,
+                           const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                           int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
+                           int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* Largest-first launch order of the tiles: tile_order[n_tiles] lists the tiles by descending
  * pair count (ties by tile index).  Pass it to gstex_raster_fwd / gstex_texture_edit, whose
@@ -154,9 +164,11 @@ size_t gstex_unit_order_scratch_words(void);
  * launch order into it).  Any of v_img ... v_normal may be NULL (that output's gradient is zero).  Texel blocks
  * that run past n_texels (corrupt texture_dims) are neither read nor written.  One wave per backward unit (tile,
  * 8x8 pixel quadrant q, segment): for every pair (emission slot s) the quadrant contributes to, writes the row
- * partials[(4 s + q) * GSTEX_PARTIAL_FLOATS ...] (n_isect * 4 rows allocated; rows of pairs a quadrant does not
- * reach are never written) and sets byte q of row_flags[s] (n_isect uint32 words, zeroed by this call on the
- * stream); accumulates (+=) texel gradients into v_texture[n_texels][C]. */
+ * partials[(4 s + q) * R ...] (n_isect * 4 rows of R floats allocated; rows of pairs a quadrant does not reach are
+ * never written) and sets byte q of row_flags[s] (n_isect uint32 words, zeroed by this call on the stream);
+ * accumulates (+=) texel gradients into v_texture[n_texels][C].  R = GSTEX_PARTIAL_FLOATS_PHOTO (24) when neither
+ * v_depth nor v_normal is given and v_reg is NULL or distortion (settings bit 10) is off -- the photometric training
+ * step -- else GSTEX_PARTIAL_FLOATS (32); pass the same R to gstex_raster_setup_bwd(_aabb) as row_floats. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
@@ -171,7 +183,7 @@ int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, f
                            const float* quats, const float* opacities, const float* umap,
                            const float* vmap, const int32_t* num_tiles_hit,
                            const int32_t* offsets, float* partials, const uint32_t* row_flags,
-                           const gstex_camera* cam, float* v_means, float* v_scales,
+                           int32_t row_floats, const gstex_camera* cam, float* v_means, float* v_scales,
                            float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                            float* v_uv0, void* stream);
 /* gstex_raster_setup_bwd with gstex_aabb_2d_bwd folded in: for callers whose centres came from
@@ -182,7 +194,7 @@ int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scal
                                 const float* quats, const float* opacities, const float* umap,
                                 const float* vmap, const int32_t* num_tiles_hit,
                                 const int32_t* offsets, float* partials, const uint32_t* row_flags,
-                                const gstex_camera* cam, float* v_means, float* v_scales,
+                                int32_t row_floats, const gstex_camera* cam, float* v_means, float* v_scales,
                                 float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                                 float* v_uv0, void* stream);
 

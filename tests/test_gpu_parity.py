@@ -257,13 +257,36 @@ def test_unit_order(n_units, groups):
         assert np.all(got[:len(placed)] >= 0) and np.all(np.diff(c[placed]) <= 0)
 
 
+@pytest.mark.parametrize("H,W,n", [(80, 96, 400), (64, 64, 0), (2064, 2064, 3000)])  # 16641 tiles: row-major
+def test_bin_sort_ordered_matches_tile_order(H, W, n):
+    """gstex_bin_sort_ordered: the binning as gstex_bin_sort, plus the launch order gstex_tile_order computes
+    from the resulting tile ranges (the forward reuses it instead of ranking the tiles twice)."""
+    from gstex_amd import ops
+
+    g = torch.Generator().manual_seed(n + H)
+    centers = (torch.rand((n, 2), generator=g) * torch.tensor([W, H])).to(DEV)
+    extents = (torch.rand((n, 2), generator=g) * 40 + 1).to(DEV)
+    depths = (torch.rand((n,), generator=g) + 0.5).to(DEV)
+    nth = ops.get_num_tiles_hit_2d(centers, extents, H, W, 16)
+    a = ops.bin_and_sort(centers, extents, depths, nth, H, W)
+    b = ops.bin_finish(ops.bin_begin(nth), centers, extents, depths, H, W, with_order=True)
+    for x, y in zip(a, b[:4]):
+        assert torch.equal(x, y)
+    assert torch.equal(b[4], ops.tile_order(b[1]))
+
+
 def test_outputs_independent_of_launch_order(monkeypatch):
     from gstex_amd import ops
 
     case = make_case(n=400, n_texels=20000, H=80, W=96, seed=13)
     f1, g1 = gpu_run(case, grads=True)
-    monkeypatch.setattr(ops, "tile_order",
-                        lambda tr: torch.arange(tr.shape[0], device=tr.device, dtype=torch.int32).flip(0))
+    finish = ops.bin_finish
+
+    def reversed_order(*a, **k):  # the forward takes its launch order from the binning: reverse it
+        out = finish(*a, **k)
+        return out[:4] + (out[4].flip(0).contiguous(),) if k.get("with_order") else out
+
+    monkeypatch.setattr(ops, "bin_finish", reversed_order)
     f2, g2 = gpu_run(case, grads=True)
     for k in f1:
         assert torch.equal(f1[k], f2[k]), k
