@@ -53,7 +53,7 @@ constexpr int kThreads = kTilePixels;  // 256
 #define GSTEX_STATS 0  // diagnostic builds: count backward work (iterations, culled, active lanes)
 #endif
 #if GSTEX_STATS
-__device__ unsigned long long g_stats[16];  // [0, 8) backward, [8, 13) forward counters
+__device__ unsigned long long g_stats[24];  // [0, 8) backward, [8, 13) forward counters, [13, 20) backward
 extern "C" int gstex_debug_stats(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats)) == hipSuccess ? 0 : 2;
 }
@@ -656,6 +656,11 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     };
     const int lane = tid & 63, wave = tid >> 6;
     const size_t vm_base = visit_mask_base(rng.x, tile);
+#if GSTEX_STATS == 1  // packing counters: runs of consecutive visits whose contributing lane sets are disjoint
+    unsigned long long st_acc = 0, st_acc2 = 0, st_acc4 = 0;
+    int st_n2 = 0, st_n4 = 0;
+    long long st_lanes = 0;
+#endif
     const int sbase = seg_base(rng.x, tile);
     int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
     // XCD group of the tile's backward units: its GSTEX_XCD_MB x GSTEX_XCD_MB-tile macro-block
@@ -1231,6 +1236,11 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     for (int c = 0; c < CM; ++c) gabs = fmaxf(gabs, fabsf(Gtex[c]));
     for (int i = lane; i < kTexStage; i += 64) s_texq[i] = 0;
     const size_t vm_base = visit_mask_base(rng.x, tile);
+#if GSTEX_STATS == 1  // packing counters: runs of consecutive visits whose contributing lane sets are disjoint
+    unsigned long long st_acc = 0, st_acc2 = 0, st_acc4 = 0;
+    int st_n2 = 0, st_n4 = 0;
+    long long st_lanes = 0;
+#endif
 
     for (int wd = hi >> 6; wd >= (lo >> 6); --wd) {
         const int pos0 = wd << 6;
@@ -1259,6 +1269,19 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
             GSTEX_STAT(14, __popcll(__ballot(contrib)) <= 16 ? 1 : 0);  // sparse visits
             GSTEX_STAT(15, __popcll(__ballot(contrib)) >= 48 ? 1 : 0);  // dense visits
+#if GSTEX_STATS == 1
+            {
+                const unsigned long long m = __ballot(contrib);
+                if (m) {
+                    if (st_acc == 0 || (m & st_acc)) { GSTEX_STAT(16, 1); st_acc = m; } else { st_acc |= m; }
+                    if (st_n2 == 0 || st_n2 == 2 || (m & st_acc2)) { GSTEX_STAT(17, 1); st_acc2 = m; st_n2 = 1; }
+                    else { st_acc2 |= m; st_n2 = 2; }
+                    if (st_n4 == 0 || st_n4 == 4 || (m & st_acc4)) { GSTEX_STAT(18, 1); st_acc4 = m; st_n4 = 1; }
+                    else { st_acc4 |= m; ++st_n4; }
+                    st_lanes += __popcll(m);
+                }
+            }
+#endif
             constexpr int NP = GEO ? kPartRowGeo : kPartRow;
             // a spare slot of the row (zero when stored): the texel fixed-point bound
             constexpr int kMBound = GEO ? 27 : P_NRM;
@@ -1507,6 +1530,9 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             }
         }
     }
+#if GSTEX_STATS == 1
+    GSTEX_STAT(19, (st_lanes + 63) / 64);  // passes if this unit's contributing pairs were packed densely
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
