@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 REC_FLOATS = 32
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)

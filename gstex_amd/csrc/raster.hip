@@ -1260,7 +1260,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             const int j = 63 - __builtin_clzll(todo);
             todo &= ~(1ull << j);
             const int rel = pos0 + j;
-            const Rec r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(my_gid, j) * kRecF4);
+            const int gid = __builtin_amdgcn_readlane(my_gid, j);
+            const Rec r = read_rec_global(records + (size_t)gid * kRecF4);
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
@@ -1425,22 +1426,40 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
                     if (lane == kML) P[kMI] = 0.0f;
                 }
-                // the (pair, quadrant) row: lanes 8k hold NP / 8 consecutive values each; the flag (1: 24-value
-                // row, 2: 32-value row) marks it written
-                const int slot = __builtin_amdgcn_readlane(my_slot, j);
-                if ((lane & 7) == 0 && !(GSTEX_ABLATE & 256)) {
-                    constexpr int E = NP / 8;
-                    const int base = (NP / 2) * ((lane >> 5) & 1) + (NP / 4) * ((lane >> 4) & 1) + E * ((lane >> 3) & 1);
-                    float* dst = partials + ((size_t)slot * 4 + quad) * NP + base;  // rows NP floats apart
-                    if constexpr (E == 4) {
-                        *reinterpret_cast<float4*>(dst) = make_float4(P[0], P[1], P[2], P[3]);
-                    } else {
-                        dst[0] = P[0];
-                        dst[1] = P[1];
-                        dst[2] = P[2];
+                // lanes 8k hold NP / 8 consecutive values each.  Deterministic mode (row_flags given): the
+                // (pair, quadrant) row, whose flag (1: 24-value row, 2: 32-value row) marks it written, summed by
+                // setup_bwd in a fixed order.  Otherwise: added with float atomics into the splat's NP-value
+                // accumulator row (zeroed by the caller): no row traffic, no summing pass, order-dependent rounding
+                constexpr int E = NP / 8;
+                const int base = (NP / 2) * ((lane >> 5) & 1) + (NP / 4) * ((lane >> 4) & 1) + E * ((lane >> 3) & 1);
+                if (row_flags) {
+                    const int slot = __builtin_amdgcn_readlane(my_slot, j);
+                    if ((lane & 7) == 0 && !(GSTEX_ABLATE & 256)) {
+                        float* dst = partials + ((size_t)slot * 4 + quad) * NP + base;  // rows NP floats apart
+                        if constexpr (E == 4) {
+                            *reinterpret_cast<float4*>(dst) = make_float4(P[0], P[1], P[2], P[3]);
+                        } else {
+                            dst[0] = P[0];
+                            dst[1] = P[1];
+                            dst[2] = P[2];
+                        }
                     }
+                    if (lane == 0 && !(GSTEX_ABLATE & 256)) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
+                } else if (!(GSTEX_ABLATE & 256)) {
+                    float* dst = partials + (size_t)gid * NP + base;
+                    // lane 8k + e takes value e of lane 8k (DPP row shifts): one atomic instruction covers the NP
+                    // contiguous floats (2 cache-line requests; E atomics from each lane 8k measured +0.2 ms)
+                    const int e = lane & 7;
+                    float v = P[0];
+                    const float s1 = dpp_shr_f<1>(P[1]), s2 = dpp_shr_f<2>(P[2]);
+                    v = e == 1 ? s1 : v;
+                    v = e == 2 ? s2 : v;
+                    if constexpr (E == 4) {
+                        const float s3 = dpp_shr_f<3>(P[3]);
+                        v = e == 3 ? s3 : v;
+                    }
+                    if (e < E) atomicAdd(dst + e, v);
                 }
-                if (lane == 0 && !(GSTEX_ABLATE & 256)) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
             }
             if (__any(tkey >= 0)) {
                 // fixed point for this visit: every staged entry receives at most vis_M in value units (bilinear
@@ -1626,18 +1645,23 @@ __global__ __launch_bounds__(256) void setup_bwd_chain_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
     const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials, int rs,
-    CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales, float* __restrict__ v_quats,
-    float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers, float* __restrict__ v_uv0) {
+    bool per_splat, CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales,
+    float* __restrict__ v_quats, float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers,
+    float* __restrict__ v_uv0) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     const Camera cam = load_camera(cam_args);
     const int cnt = nth[g];
     float S[kPartRowGeo];
     if (cnt > 0) {
-        const float4* src = reinterpret_cast<const float4*>(partials + (size_t)offsets[g] * 4 * rs);
+        // per_splat: the backward's (N, rs) accumulator rows; else the sums setup_bwd_sum wrote over the splat's first
+        // partial row (32 values, the last 8 zero for 24-value rows)
+        const float4* src = reinterpret_cast<const float4*>(per_splat ? partials + (size_t)g * rs
+                                                                       : partials + (size_t)offsets[g] * 4 * rs);
+        const int n4 = per_splat ? rs / 4 : kPartRowGeo / 4;
 #pragma unroll
         for (int i = 0; i < kPartRowGeo / 4; ++i) {
-            const float4 v = src[i];
+            const float4 v = i < n4 ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
             S[4 * i] = v.x; S[4 * i + 1] = v.y; S[4 * i + 2] = v.z; S[4 * i + 3] = v.w;
         }
     } else {
@@ -1960,8 +1984,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && state && aux, "gstex_raster_bwd: null pointer (tile_ranges, state and the forward's aux)");
     GSTEX_REQUIRE(n_isect >= 0 && n_isect < (int64_t)INT32_MAX, "gstex_raster_bwd: n_isect out of range");
-    GSTEX_REQUIRE(n_isect == 0 || (partials && row_flags && sorted_ids && sorted_slots),
-                  "gstex_raster_bwd: null pair buffer");
+    GSTEX_REQUIRE(n_isect == 0 || (partials && sorted_ids && sorted_slots), "gstex_raster_bwd: null pair buffer");
     GSTEX_REQUIRE(n_texels >= 0 && n_texels * channels < (int64_t)INT32_MAX, "gstex_raster_bwd: n_texels out of range");
     GSTEX_REQUIRE(n_texels == 0 || (texture && v_texture), "gstex_raster_bwd: null texture");
     GSTEX_REQUIRE(!(settings & GSTEX_SETTING_EVAL_NORMAL) || !v_normal,
@@ -1971,7 +1994,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     hipStream_t st = as_stream(stream);
     const AuxLayout al = aux_layout(n_isect, tiles_x * tiles_y, channels);
     const AuxPtrs ap = aux_ptrs(aux, al);
-    if (n_isect > 0 && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
+    if (n_isect > 0 && row_flags && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
     // costliest units first, from the histogram the forward built (order entries are unit + 1)
     rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
@@ -2004,11 +2027,13 @@ int setup_bwd_launch(int32_t n, const float* means, const float* scales, float g
                      float* partials, const uint32_t* row_flags, int32_t rs, const gstex_camera* cam, float* v_means,
                      float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                      float* v_uv0, hipStream_t st, const char* name) {
-    if (GSTEX_SETUP_SPLIT) {
-        setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags, rs);
+    if (GSTEX_SETUP_SPLIT || !row_flags) {
+        // no row_flags: the backward accumulated per splat (atomic mode), nothing to sum
+        if (row_flags)
+            setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags, rs);
         setup_bwd_chain_kernel<FOLD_AABB><<<div_up(n, 256), 256, 0, st>>>(
-            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, rs, to_device_camera(*cam), v_means,
-            v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, rs, row_flags == nullptr,
+            to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
     } else {
         setup_bwd_kernel<FOLD_AABB><<<div_up(n, kSetupBwdSplats), 256, 0, st>>>(
             n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, row_flags, rs,

@@ -447,12 +447,18 @@ class _TextureGaussians(torch.autograd.Function):
         v_tex = g(v_tex, (H, W, C))
         v_normal = g(v_normal, (H, W, 3))
         n_isect = sorted_ids.shape[0]
-        # one partial row per (pair, 8x8 quadrant), written only where the quadrant contributes (row_flags); rows of 24
-        # floats without depth / normal / distortion gradients (gstex_raster_bwd), 32 with
+        # 24 values per (pair, quadrant) sum without depth / normal / distortion gradients (gstex_raster_bwd), 32 with.
+        # Default: float-atomic accumulation per splat (like the texel gradients).  Under
+        # torch.use_deterministic_algorithms(True): one row per (pair, 8x8 quadrant), written only where the quadrant
+        # contributes (row_flags), summed in a fixed order by setup_bwd -- bitwise reproducible splat gradients
         geo = v_depth is not None or v_normal is not None or (v_reg is not None and bool(settings & (1 << 10)))
         row_floats = PARTIAL_FLOATS if geo else PARTIAL_FLOATS_PHOTO
-        partials = torch.empty((n_isect, 4, row_floats), device=dev, dtype=torch.float32)
-        row_flags = torch.empty((n_isect,), device=dev, dtype=torch.int32)
+        if torch.are_deterministic_algorithms_enabled():
+            partials = torch.empty((n_isect, 4, row_floats), device=dev, dtype=torch.float32)
+            row_flags = torch.empty((n_isect,), device=dev, dtype=torch.int32)
+        else:
+            partials = torch.zeros((n, row_floats), device=dev, dtype=torch.float32)
+            row_flags = None
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
         _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 8
+#define GSTEX_ABI_VERSION 9
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -168,7 +168,11 @@ size_t gstex_unit_order_scratch_words(void);
  * never written) and sets byte q of row_flags[s] (n_isect uint32 words, zeroed by this call on the stream);
  * accumulates (+=) texel gradients into v_texture[n_texels][C].  R = GSTEX_PARTIAL_FLOATS_PHOTO (24) when neither
  * v_depth nor v_normal is given and v_reg is NULL or distortion (settings bit 10) is off -- the photometric training
- * step -- else GSTEX_PARTIAL_FLOATS (32); pass the same R to gstex_raster_setup_bwd(_aabb) as row_floats. */
+ * step -- else GSTEX_PARTIAL_FLOATS (32); pass the same R to gstex_raster_setup_bwd(_aabb) as row_floats.
+ * row_flags == NULL (ABI 9, the fast mode): instead of rows, every (pair, quadrant) sum is added with float
+ * atomics into partials[g * R ...], an (n_splats, R) accumulator the caller has zeroed -- no per-pair rows, no
+ * summing pass in setup_bwd; the splat gradients then depend on the atomics' order in their last bits (as the
+ * texel gradients always do).  With row_flags the splat gradients are bitwise reproducible. */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const int32_t* tile_ranges,
                      const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
@@ -178,7 +182,8 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      uint32_t* row_flags, float* v_texture, void* aux, void* stream);
 /* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
  * them to the splat parameters. Outputs are overwritten.  partials is consumed: each splat's sums are written
- * over its first row (the rows are backward scratch, not read again). */
+ * over its first row (the rows are backward scratch, not read again).  row_flags == NULL: partials is the
+ * backward's (n, row_floats) per-splat accumulator (gstex_raster_bwd without row_flags), chained directly. */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                            const float* quats, const float* opacities, const float* umap,
                            const float* vmap, const int32_t* num_tiles_hit,

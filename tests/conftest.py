@@ -22,3 +22,17 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture
+def deterministic():
+    """torch.use_deterministic_algorithms(True) for one test: the raster backward then sums its splat gradients in a
+    fixed order (per-pair rows) instead of float atomics -- the mode the bitwise-reproducibility tests check."""
+    import torch
+
+    prev, prev_warn = torch.are_deterministic_algorithms_enabled(), torch.is_deterministic_algorithms_warn_only_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        yield
+    finally:
+        torch.use_deterministic_algorithms(prev, warn_only=prev_warn)

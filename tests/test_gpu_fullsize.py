@@ -105,7 +105,7 @@ def test_cfg3_forward_backward_checksums(cfg3):
     assert torch.allclose(lhs, rhs, rtol=1e-4, atol=1e-6), (lhs, rhs)
 
 
-def test_cfg3_splat_gradients_bitwise_reproducible(cfg3):
+def test_cfg3_splat_gradients_bitwise_reproducible(cfg3, deterministic):
     g1, _, o1 = _render(cfg3)
     torch.autograd.backward(list(o1), [torch.ones_like(o) * 1e-3 for o in o1])
     g2, _, o2 = _render(cfg3)

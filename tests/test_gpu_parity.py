@@ -200,12 +200,29 @@ def test_empty_and_offscreen():
         assert torch.all(gg[k] == 0), k
 
 
-def test_backward_is_deterministic():
+def test_backward_is_deterministic(deterministic):
     case = make_case(n=300, n_texels=20000, H=64, W=64, seed=11)
     _, g1 = gpu_run(case, grads=True)
     _, g2 = gpu_run(case, grads=True)
     for k in ["rgbs", "opacities", "means", "scales", "quats", "centers"]:
         assert torch.equal(g1[k], g2[k]), f"{k} gradient not bitwise reproducible"
+
+
+@pytest.mark.parametrize("geo", [False, True])
+def test_atomic_splat_sums_match_rows(geo):
+    """Default mode (per-splat float-atomic accumulators, no rows, no summing pass) against the deterministic
+    per-pair rows: the same sums up to summation order, for 24-value (photometric) and 32-value rows."""
+    case = make_case(n=700, n_texels=30000, H=80, W=96, seed=29)
+    outs = None if geo else ("img", "alpha", "tex")
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        _, g_rows = gpu_run(case, grads=True, outputs=outs)
+    finally:
+        torch.use_deterministic_algorithms(False)
+    _, g_atom = gpu_run(case, grads=True, outputs=outs)
+    for k in ["rgbs", "opacities", "means", "scales", "quats", "centers", "uv0", "texture"]:
+        assert grad_norm_err(g_atom[k], g_rows[k]) < 1e-6, k
+        assert float(g_rows[k].abs().max()) > 0, k
 
 
 
@@ -275,7 +292,7 @@ def test_bin_sort_ordered_matches_tile_order(H, W, n):
     assert torch.equal(b[4], ops.tile_order(b[1]))
 
 
-def test_outputs_independent_of_launch_order(monkeypatch):
+def test_outputs_independent_of_launch_order(monkeypatch, deterministic):
     from gstex_amd import ops
 
     case = make_case(n=400, n_texels=20000, H=80, W=96, seed=13)
@@ -573,7 +590,7 @@ def test_fused_activations_match_eager_trainer():
 
 
 # ---------------------------------------------------------------- folded AABB-centre chain (training path)
-def test_fold_aabb_gradients_bit_identical():
+def test_fold_aabb_gradients_bit_identical(deterministic):
     """texture_gaussians(fold_aabb=True) chains the centre gradient through get_aabb_2d inside the raster's
     setup backward: means / scales / quats gradients are bit-identical to the separate get_aabb_2d backward
     plus autograd's accumulation."""
@@ -607,7 +624,7 @@ def test_fold_aabb_gradients_bit_identical():
     assert float(res[0]["means"].abs().max()) > 0
 
 
-def test_geometry_outputs_off_matches():
+def test_geometry_outputs_off_matches(deterministic):
     """geometry_outputs=False (photometric training path): img / alpha / tex and every gradient of a
     photometric upstream are bit-identical to the full render; depth / reg / normal come back as zeros."""
     case = make_case(n=500, n_texels=25000, H=64, W=80, seed=23)
