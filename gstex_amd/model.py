@@ -259,7 +259,9 @@ class GStexTrainer:
     def eval_render(self, view: View, edit_texture: torch.Tensor | None = None):
         """The reference's eval render (get_outputs with extra_stuff, gstex.py:1086-1203): a 6-channel texture
         [SH2RGB(texture_dc), 0, 0, 0] and three raster calls -- the image, the test-colour render with
-        thresholded opacities (test_img / uv_im) and the settings | 1 << 15 render (edit_img, clean normals)."""
+        thresholded opacities (test_img / uv_im) and the settings | 1 << 15 render (edit_img, clean normals).
+        Same outputs (tests/test_gpu_eval.py checks them against those three 6-channel calls), computed with one
+        binning and the 3-channel raster (below)."""
         self.wait_texture()
         means = self.means
         quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
@@ -273,34 +275,36 @@ class GStexTrainer:
         n = means.shape[0]
         rgbs = (sh_rest(self.sh_degree_now(), viewdirs, self.features_rest) if self.sh_degree > 0
                 else torch.sigmoid(self.features_dc))
-        tex6 = torch.zeros((self.texture_dc.shape[0], 6), device=means.device)
-        tex6[:, 0:3] = SH2RGB(self.texture_dc)
         if self.test_colors is None or self.test_colors.shape[0] != n:
             g = torch.Generator(device="cpu").manual_seed(0)
             self.test_colors = torch.rand((n, 3), generator=g).to(means.device)  # gstex.py:309
         bgz = torch.zeros_like(self.background)
+        # the three calls share one geometry: binned and sorted once.  The reference's 6-channel texture is
+        # [SH2RGB(texture_dc), 0, 0, 0] for the first call and [edit_texture or 0, 0, 0, 0] for the other two; a
+        # zero texel contributes exactly 0, so each call runs the 3-channel raster (SH2RGB as texture_transform,
+        # the all-zero texture as transform (0, 0)) and channels 3..5 of its texture output are zeros -- the same
+        # outputs without materialising two 6-channel copies of the texel store
+        bins = ops.bin_gaussians(centers, extents, depths, nth, view.H, view.W)
 
-        def tg(cr, ct, co, st):
+        def tg(cr, tex, transform, co, st):
             return ops.texture_gaussians(
-                (n, 1, 6), self.texture_dims, centers, extents, depths, nth, cr, co, means, scales, 1, quats, uv0,
-                umap, vmap, ct, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
-                ops.BLOCK_WIDTH, st, background=bgz)
+                (n, 1, 3), self.texture_dims, centers, extents, depths, nth, cr, co, means, scales, 1, quats, uv0,
+                umap, vmap, tex, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
+                ops.BLOCK_WIDTH, st, background=bgz, texture_transform=transform, binning=bins)
 
-        img, depth, reg, alpha, tex, normal = tg(rgbs, tex6, opacities, self.settings)
-        upd = torch.zeros_like(tex6)
-        upd[:, 3:] = tex6[:, 3:]
-        if edit_texture is not None:
-            upd[:, :3] = edit_texture
+        img, depth, reg, alpha, tex, normal = tg(rgbs, self.texture_dc, (SH_C0, 0.5), opacities, self.settings)
+        upd, upd_tf = (edit_texture, None) if edit_texture is not None else (self.texture_dc, (0.0, 0.0))
         test_op = opacities.clone()
         test_op[test_op <= 0.5] = 0.0
         test_op[test_op > 0.2] = 1.0
-        t_out = tg(self.test_colors, upd, test_op, self.settings)
-        n_out = tg(self.test_colors, upd, opacities, self.settings | (1 << 15))
+        t_out = tg(self.test_colors, upd, upd_tf, test_op, self.settings)
+        n_out = tg(self.test_colors, upd, upd_tf, opacities, self.settings | (1 << 15))
+        zeros3 = torch.zeros_like(img)  # texture channels 3..5 of every call
         bg = self.background[None, None, :]
         rgb = torch.clamp(img + tex[..., 0:3] + (1 - alpha[..., None]) * bg, 0.0, 1.0)
         return dict(rgb=rgb, depth=depth, alpha=alpha, normal=normal,
                     test_img=t_out[0] + (1 - t_out[3][..., None]) * bg,
-                    uv_im=torch.clamp(t_out[4][..., 3:6] + (1 - t_out[3][..., None]) * bg, 0.0, 1.0),
+                    uv_im=torch.clamp(zeros3 + (1 - t_out[3][..., None]) * bg, 0.0, 1.0),
                     edit_img=torch.clamp(img + n_out[4][..., :3] + (1 - alpha[..., None]) * bg, 0.0, 1.0),
                     clean_normal_img=torch.clamp(0.5 * (n_out[5] + 1) + (1 - alpha[..., None]) * bg, 0.0, 1.0))
 

@@ -8,7 +8,7 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 from __future__ import annotations
 
 import time
-from typing import Tuple
+from typing import NamedTuple, Tuple
 
 import torch
 
@@ -326,7 +326,7 @@ class _TextureGaussians(torch.autograd.Function):
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                 block_width, settings, background, texture_transform=None, fold_aabb=False,
                 geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None,
-                texture_ready=None):
+                texture_ready=None, binning=None):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -358,7 +358,7 @@ class _TextureGaussians(torch.autograd.Function):
         # the pair count is read to the host once; work that does not depend on the tile lists is queued
         # between the copy and the wait, so the device runs it while the host waits and sizes the pair
         # buffers: the splat records and the zeroed texel-gradient buffer of the backward
-        begun = bin_begin(nth)
+        begun = bin_begin(nth) if binning is None else None
         records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
              ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
@@ -377,8 +377,15 @@ class _TextureGaussians(torch.autograd.Function):
                 ctx.v_texture = texture_grad_sink
             else:
                 ctx.v_texture = torch.zeros_like(texture)
-        offsets, tile_ranges, sorted_ids, sorted_slots, order = bin_finish(
-            begun, centers_c.detach(), extents_c, depths_c, H, W, BLOCK_WIDTH, with_order=True)
+        if binning is None:
+            offsets, tile_ranges, sorted_ids, sorted_slots, order = bin_finish(
+                begun, centers_c.detach(), extents_c, depths_c, H, W, BLOCK_WIDTH, with_order=True)
+        else:  # a previous call's binning of the same centres / extents / depths / num_tiles_hit (bin_gaussians)
+            _check(binning.n == n and binning.H == H and binning.W == W and binning.nth.data_ptr() == nth.data_ptr(),
+                   "binning was computed for other splats / image size / num_tiles_hit")
+            offsets, tile_ranges, sorted_ids, sorted_slots, order = (binning.offsets, binning.tile_ranges,
+                                                                     binning.sorted_ids, binning.sorted_slots,
+                                                                     binning.order)
         ctx_scale, ctx_bias = (1.0, 0.0) if texture_transform is None else (float(texture_transform[0]),
                                                                              float(texture_transform[1]))
         f = dict(device=dev, dtype=torch.float32)
@@ -488,14 +495,14 @@ class _TextureGaussians(torch.autograd.Function):
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
                       fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None,
-                      texture_ready=None):
+                      texture_ready=None, binning=None):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -520,6 +527,10 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     forward -- the texel update of the previous optimizer step running on a side stream (GStexTrainer
     async_texture), so preprocessing and binning overlap it.
 
+    binning (not in the reference API): a Binning from bin_gaussians() on the same centers / extents / depths /
+    num_tiles_hit tensors -- several renders of one geometry (the eval render's three calls, gstex.py:1165-1200)
+    bin and sort once.
+
     Returns (img (H,W,3), depth (H,W), reg (H,W), alpha (H,W), tex_img (H,W,C), normal (H,W,3)).
     Gradients flow to rgbs, opacities, means, scales, quats, texture, centers (-> get_aabb_2d),
     uv0 and background; umap/vmap are treated as constants (detached by the caller, gstex.py:977-984).
@@ -532,7 +543,31 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
                                    fold_aabb, geometry_outputs, torch.is_grad_enabled(), texture_grad_sink,
-                                   on_texture_grad, texture_ready)
+                                   on_texture_grad, texture_ready, binning)
+
+
+class Binning(NamedTuple):
+    """bin_gaussians() output, reusable by texture_gaussians(binning=...) calls on the same geometry."""
+    n: int
+    H: int
+    W: int
+    nth: torch.Tensor
+    offsets: torch.Tensor
+    tile_ranges: torch.Tensor
+    sorted_ids: torch.Tensor
+    sorted_slots: torch.Tensor
+    order: torch.Tensor
+
+
+def bin_gaussians(centers, extents, depths, num_tiles_hit, H: int, W: int) -> Binning:
+    """Tile binning + depth sort + largest-first tile order of one geometry, for several texture_gaussians calls."""
+    n = centers.shape[0]
+    nth = _i32(num_tiles_hit, "num_tiles_hit", (n,))
+    c = _f32(centers.detach(), "centers", (n, 2))
+    e = _f32(extents.detach(), "extents", (n, 2))
+    d = _f32(depths.detach(), "depths", (n,))
+    out = bin_finish(bin_begin(nth), c, e, d, int(H), int(W), BLOCK_WIDTH, with_order=True)
+    return Binning(n, int(H), int(W), nth, *out)
 
 
 rasterize_gaussians = texture_gaussians  # north_star name
