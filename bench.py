@@ -294,6 +294,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    base_mb = torch.cuda.memory_allocated(dev) / 2**20  # parameters, Adam state, scene, views, targets
+    torch.cuda.reset_peak_memory_stats(dev)
     ops.set_kernel_timing(not args.no_kernel_timing)
     step_ev = []
     t0 = time.perf_counter()
@@ -308,6 +310,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20
     kt = ops.kernel_times()
     ops.set_kernel_timing(False)
     step_ms = _events_ms(step_ev)
@@ -346,6 +349,10 @@ def main():
     sub = None
     if rank == 0 and world == 1 and not args.no_sub:
         sub = {}
+        # HBM footprint of the timed steps (torch allocator): resident state, and the peak including the step's
+        # transient buffers (pair lists, records, per-pixel state, forward aux / checkpoints, gradients)
+        sub["hbm_mb"] = dict(resident=round(base_mb, 1), step_peak=round(peak_mb, 1),
+                             step_transient=round(peak_mb - base_mb, 1))
         try:
             # the full-output forward (depth / distortion / normal produced: the reference kernel's contract)
             trainer.geometry_outputs = True

@@ -85,9 +85,6 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #else
 #define GSTEX_FWD_ATTR
 #endif
-#ifndef GSTEX_FWD_SLOAD
-#define GSTEX_FWD_SLOAD 0  // 1: forward reads each visited record through scalar loads (SGPRs) instead of LDS
-#endif
 #ifndef GSTEX_CONIC_CULL
 #define GSTEX_CONIC_CULL 1  // per-wave ellipse-vs-rectangle cull on top of the contribution box
 #endif
@@ -611,7 +608,6 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     const int Cn = (C > 0) ? C : Cdyn;
     constexpr int kThr = FwdShape<ONE>::kThr, kStep = FwdShape<ONE>::kStep, kWords = kStep / 64;
     __shared__ float4 s_rec[ONE ? 1 : kRecF4 * kFwdBatch];
-    __shared__ int s_gid[ONE ? 1 : kFwdBatch];
     // ONE: tile i of the largest-first order takes blocks 32 (i / 8) + 8 q + i % 8, q = quadrant, so the four quadrants
     // of a tile are dispatched to one XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2
     const int bidx = (int)blockIdx.x;
@@ -638,20 +634,24 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     for (int c = 0; c < CM; ++c) tex[c] = 0.f;
     float D = 0.f, M1 = 0.f, M2 = 0.f, reg = 0.f;
     int last = -1;
-    bool done = !inside;
+    // per-lane "still running" as a float, not a bool: a bool carried around the visit loop becomes an SGPR lane
+    // mask that the compiler re-merges with exec at every join (three SALU per join; measured: the forward with the
+    // divergent per-lane loop exits and bool lane state 0.595 ms, with this loop 0.550 ms)
+    float alive = inside ? 1.0f : 0.0f;
+#define GSTEX_FWD_DONE (alive == 0.0f)
     // Deferred texel accumulation (kFwdDefer): a visit's four texel gathers are issued into the pending registers
     // and folded into tex[] at the lane's next contributing visit (or at a checkpoint / the end), so their latency
     // overlaps the next visit's record read and pair evaluation.  Same values, same order of accumulation.
     constexpr bool kDefer = kFwdDefer && C == 3;
-    bool pend = false;
+    float pend = 0.0f;  // (a float: see `alive`)
     float p00[CM], p01[CM], p10[CM], p11[CM], pax = 0.f, pay = 0.f, pw = 0.f;
     auto fold_pending = [&]() {
-        if (kDefer && pend) {
+        if (kDefer && pend != 0.0f) {
 #pragma unroll
             for (int c = 0; c < CM; ++c) {
                 if (c < Cn) tex[c] = tex_accum(tex[c], p00[c], p01[c], p10[c], p11[c], pax, pay, tex_scale, tex_bias, pw);
             }
-            pend = false;
+            pend = 0.0f;
         }
     };
     const int lane = tid & 63, wave = tid >> 6;
@@ -699,22 +699,21 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
                 atomicAdd(&aux.order_ws[unit_bin(key)], 1);  // the backward's unit-order histogram
             }
             fold_pending();
-            if (__any(!done)) write_ck(sbase + cur_seg);
+            if (__any(!GSTEX_FWD_DONE)) write_ck(sbase + cur_seg);
             seg_visits = 0;
             ++cur_seg;
         }
         const int nb = min(kStep, rng.y - b0);
         int my_gid = 0;  // ONE: lane k <-> position b0 + k
         if constexpr (ONE) {
-            if (__all(done)) break;
+            if (__all(GSTEX_FWD_DONE)) break;
             if (lane < nb) my_gid = sorted_ids[b0 + lane];
         } else {
-            if (__syncthreads_count(done ? 1 : 0) == kThreads) break;
+            if (__syncthreads_count(GSTEX_FWD_DONE ? 1 : 0) == kThreads) break;
             for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
                 const int j = q / kRecF4, k = q % kRecF4;
                 if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
             }
-            if (GSTEX_FWD_SLOAD && tid < kFwdBatch && b0 + tid < rng.y) s_gid[tid] = sorted_ids[b0 + tid];
             __syncthreads();
         }
         // the batch splats whose contribution region meets this wave's 8x8 block, tested all at once
@@ -738,87 +737,80 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
             if (visit_masks && lane == 0 && hb * 64 < nb)
                 visit_masks[(vm_base + ((b0 - rng.x) >> 6) + hb) * 4 + wave] = todo[hb];
         }
-        for (int hb = 0; hb < kWords && !done; ++hb) {
+        // wave-uniform visit loop: finished lanes stay in it with their updates predicated off (no divergent exits:
+        // the loop control is a scalar bit scan, not exec-mask bookkeeping); it ends when the batch's bits run out
+        // or every lane of the wave has finished
+        bool all_done = __all(GSTEX_FWD_DONE);
+        for (int hb = 0; hb < kWords && !all_done; ++hb) {
           unsigned long long m = todo[hb];
           while (m) {
-            if (done) break;
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
             ++seg_visits;
             Rec r;
             if constexpr (ONE) r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(my_gid, j) * kRecF4);
-            else r = GSTEX_FWD_SLOAD ? read_rec_global(records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * kRecF4)
-                                     : read_rec<kFwdBatch>(s_rec, j);
+            else r = read_rec<kFwdBatch>(s_rec, j);
             Hit h;
-            const bool ok = eval_hit(r, px, py, aa, h);
-            GSTEX_STATW(10, 1);                                   // visits (the wave evaluates a splat)
-            GSTEX_STATW(11, __ballot(ok) ? 1 : 0);                // ... with a contributing lane
-            GSTEX_STATW(12, __popcll(__ballot(ok && !(T * (1.0f - h.alpha) < kTMin))));  // contributing lanes
+            const bool ok = eval_hit(r, px, py, aa, h) && alive != 0.0f;
             const float test_T = T * (1.0f - h.alpha);
             const bool stop = ok && test_T < kTMin;
-            if (!ok) continue;
-            if (stop) {
-                done = true;
-                break;
-            }
-            const float w = h.alpha * T;
-            // (a block running past the texel store -- corrupt texture_dims -- contributes no texture)
-            if (kDefer) {
-                // the block's dims are wave-uniform (the record was read from LDS into VGPRs): moved to SGPRs, the
-                // block checks and the texel offsets' row steps become scalar arithmetic
+            GSTEX_STAT(10, 1);                                    // visits (the wave evaluates a splat)
+            GSTEX_STAT(11, __ballot(ok) ? 1 : 0);                 // ... with a contributing lane
+            GSTEX_STAT(12, __popcll(__ballot(ok && !stop)));      // contributing lanes
+            alive = stop ? 0.0f : alive;
+            if (ok && !stop) {
+                const float w = h.alpha * T;
                 const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
                 const int boff = __builtin_amdgcn_readfirstlane(r.off);
                 const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels && !(GSTEX_ABLATE & 4);
-                float tu = 0.f, tv = 0.f;
-                if (has_tex) tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp b = bilerp_coords(tu, tv, bh, bw, r.hf, r.wf);
-                fold_pending();  // the previous visit's texels (issued one visit ago) before their registers are reused
-                if (has_tex) {
-                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
-                    if (GSTEX_ABLATE & 512) {
-#pragma unroll
-                        for (int c = 0; c < CM; ++c) p00[c] = p01[c] = p10[c] = p11[c] = __int_as_float(b.i0 + c);
-                    } else if constexpr (CM == 3) {
-                        load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
-                    } else {
-                        load_texel_quad<CM>(rs, b, bw, Cn, p00, p01, p10, p11);
+                if (kDefer) {
+                    float tu = 0.f, tv = 0.f;
+                    if (has_tex) tex_coords(r, h.u, h.v, tu, tv);
+                    const Bilerp b = bilerp_coords(tu, tv, bh, bw, r.hf, r.wf);
+                    fold_pending();
+                    if (has_tex) {
+                        const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
+                        if constexpr (CM == 3) load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
+                        else load_texel_quad<CM>(rs, b, bw, Cn, p00, p01, p10, p11);
+                        pax = b.ax;
+                        pay = b.ay;
+                        pw = w;
+                        pend = 1.0f;
                     }
-                    pax = b.ax;
-                    pay = b.ay;
-                    pw = w;
-                    pend = true;
-                }
-            } else if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && !(GSTEX_ABLATE & 4)) {
-                float tu, tv;
-                tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
-                const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, r.off, r.h * r.w, Cn);
-                float t00[CM], t01[CM], t10[CM], t11[CM];
-                load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
+                } else if (has_tex) {
+                    float tu, tv;
+                    tex_coords(r, h.u, h.v, tu, tv);
+                    const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
+                    const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
+                    float t00[CM], t01[CM], t10[CM], t11[CM];
+                    load_texel_quad<CM>(rs, b, bw, Cn, t00, t01, t10, t11);
 #pragma unroll
-                for (int c = 0; c < CM; ++c) {
-                    // texel value = tex_scale * stored + tex_bias (affine, so applied after interpolation)
-                    if (c < Cn) tex[c] = tex_accum(tex[c], t00[c], t01[c], t10[c], t11[c], b.ax, b.ay, tex_scale, tex_bias, w);
+                    for (int c = 0; c < CM; ++c)
+                        if (c < Cn) tex[c] = tex_accum(tex[c], t00[c], t01[c], t10[c], t11[c], b.ax, b.ay, tex_scale, tex_bias, w);
                 }
+                img[0] = __builtin_fmaf(r.rgb[0], w, img[0]);
+                img[1] = __builtin_fmaf(r.rgb[1], w, img[1]);
+                img[2] = __builtin_fmaf(r.rgb[2], w, img[2]);
+                if (GEOF) {
+                    D = D + h.z * w;
+                    nrm[0] = nrm[0] + r.nrm[0] * w;
+                    nrm[1] = nrm[1] + r.nrm[1] * w;
+                    nrm[2] = nrm[2] + r.nrm[2] * w;
+                }
+                if (GEOF && dreg) {
+                    const float A = 1.0f - T;
+                    const float mm = kFarRatio * (1.0f - kNear * grad_rcp(h.z));
+                    reg = reg + ((mm * mm * A + M2) - 2.0f * mm * M1) * w;
+                    M1 = M1 + mm * w;
+                    M2 = M2 + mm * mm * w;
+                }
+                T = test_T;
+                last = b0 - rng.x + j;
             }
-            img[0] = __builtin_fmaf(r.rgb[0], w, img[0]);  // accumulations: fused (no decision depends on them)
-            img[1] = __builtin_fmaf(r.rgb[1], w, img[1]);
-            img[2] = __builtin_fmaf(r.rgb[2], w, img[2]);
-            if (GEOF) {
-                D = D + h.z * w;
-                nrm[0] = nrm[0] + r.nrm[0] * w;
-                nrm[1] = nrm[1] + r.nrm[1] * w;
-                nrm[2] = nrm[2] + r.nrm[2] * w;
+            if (__builtin_amdgcn_ballot_w64(alive != 0.0f) == 0) {
+                all_done = true;
+                break;
             }
-            if (GEOF && dreg) {
-                const float A = 1.0f - T;
-                const float m = kFarRatio * (1.0f - kNear * grad_rcp(h.z));
-                reg = reg + ((m * m * A + M2) - 2.0f * m * M1) * w;
-                M1 = M1 + m * w;
-                M2 = M2 + m * m * w;
-            }
-            T = test_T;
-            last = b0 - rng.x + j;
           }
         }
     }
