@@ -656,11 +656,6 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     };
     const int lane = tid & 63, wave = tid >> 6;
     const size_t vm_base = visit_mask_base(rng.x, tile);
-#if GSTEX_STATS == 1  // packing counters: runs of consecutive visits whose contributing lane sets are disjoint
-    unsigned long long st_acc = 0, st_acc2 = 0, st_acc4 = 0;
-    int st_n2 = 0, st_n4 = 0;
-    long long st_lanes = 0;
-#endif
     const int sbase = seg_base(rng.x, tile);
     int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
     // XCD group of the tile's backward units: its GSTEX_XCD_MB x GSTEX_XCD_MB-tile macro-block
