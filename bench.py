@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-sub", action="store_true", help="skip the cfg1/cfg2/eval/rechart sub-records")
+    p.add_argument("--no-defer-texture", action="store_true",
+                   help="run the texel Adam update inside optimizer_step instead of deferring it into the next "
+                        "step's render (GStexTrainer defer_texture)")
     p.add_argument("--async-texture", action="store_true",
                    help="texel Adam update on a side stream, overlapping the next step (measured: no net gain)")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
@@ -255,7 +258,8 @@ def main():
     scene = make_scene(args.n_splats, args.n_texels, seed=args.seed)
     views = [sphere_view(i, H, W, n_views=N_POSES).to(dev) for i in range(N_POSES)]
     # start_step = 3 x sh_degree_interval: SH at its full degree 3 (the regime of 12k of the 15k iterations)
-    trainer = GStexTrainer(scene, dev, start_step=3000, async_texture=args.async_texture)
+    trainer = GStexTrainer(scene, dev, start_step=3000, async_texture=args.async_texture,
+                           defer_texture=not (args.async_texture or args.no_defer_texture))
     sync = GradSync(trainer, world) if world > 1 else None
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     gts = [torch.rand((H, W, 3), generator=g).to(dev) for _ in range(N_POSES)]
@@ -291,6 +295,7 @@ def main():
             abs_.append(algorithmic_bytes(nth.cpu(), trainer.texture_dims.cpu(), H, W))
         ab = {k: sum(a[k] for a in abs_) / len(abs_) for k in abs_[0]}
 
+    trainer.wait_texture()  # the last warmup step's deferred texel update, outside the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -306,6 +311,7 @@ def main():
         step()
         b.record()
         step_ev.append((a, b))
+    trainer.wait_texture()  # the last timed step's deferred texel update, inside: K steps = K texel updates
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -429,6 +435,9 @@ def main():
             "fold_aabb": True, "texture_transform": "SH2RGB on read (0.28209479, 0.5)",
             "texture_update": ("side stream: the texel Adam update (zeroing its gradient) overlaps the next step's "
                                "preprocessing and binning; the raster forward waits for it" if trainer.async_texture
+                               else "deferred: step k's texel Adam update runs in step k+1's render while the host "
+                                    "reads back the pair count (same stream, before the raster forward); the timed "
+                                    "region holds exactly K texel updates" if trainer.defer_texture
                                else "compute stream"),
         },
         "roofline": roofline,

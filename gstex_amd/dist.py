@@ -116,9 +116,9 @@ class GradSync:
             raise RuntimeError("GradSync.zero(): the previous backward's all_reduce() was never called")
         if self.rebuild():
             return  # a new buffer is zero
-        if getattr(self.trainer, "async_texture", False):
-            # the texel slice is zeroed by the trainer's side-stream Adam as it reads it (GSTEX_ADAM_ZERO_GRAD);
-            # filling it here would race that update
+        if getattr(self.trainer, "texture_grad_zeroed_by_update", False):
+            # the texel slice is zeroed by the trainer's texel Adam as it reads it (GSTEX_ADAM_ZERO_GRAD: a side-stream
+            # or deferred update, async_texture / defer_texture); filling it here would race or pre-empt that update
             self.flat[:self._tail_off].zero_()
         else:
             self.flat.zero_()
@@ -148,7 +148,7 @@ class GradSync:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
 
-    def all_reduce_and_step(self, step_tail, step_head):
+    def all_reduce_and_step(self, step_tail, step_head, defer_tail: bool = False):
         """A data-parallel optimizer step with the collectives overlapped (the trainer's optimizer_step(sync=...)).
 
         The tail collective (the texel store, started from the raster backward) is followed on the wire by the head's;
@@ -156,7 +156,9 @@ class GradSync:
         overlaps the head collective, then step_head(scale) after it.  Both get scale = 1 / world to apply to the
         SUMMED gradients (FusedAdam grad_scale: the same fp32 product as averaging first, without the separate pass
         over the buffer), so after this call the buffer holds sums, not averages.  Without a running tail collective
-        (overlap_tail=False, or no backward hook fired) this is all_reduce() followed by both steps at scale 1."""
+        (overlap_tail=False, or no backward hook fired) this is all_reduce() followed by both steps at scale 1.
+        defer_tail: the head is stepped now and the tail's step is returned as a callable instead of run (the trainer's
+        defer_texture: it runs inside the next step's render, after the tail collective has had that much longer)."""
         work, self._work = self._work, None
         params = self._params()
         if work is None or self._layout(params) != self._key:
@@ -165,15 +167,27 @@ class GradSync:
                 raise RuntimeError("GradSync.all_reduce_and_step(): the parameters changed between backward and the "
                                    "step (call zero() after a rechart, before the backward)")
             self.all_reduce()
-            step_tail(1.0)
             step_head(1.0)
-            return
+            if defer_tail:
+                return lambda: step_tail(1.0)
+            step_tail(1.0)
+            return None
         self._reattach(params, skip_tail=True)
         head = dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        scale = 1.0 / self.world
+        if defer_tail:
+            head.wait()
+            step_head(scale)
+
+            def tail():
+                work.wait()
+                step_tail(scale)
+            return tail
         work.wait()
-        step_tail(1.0 / self.world)
+        step_tail(scale)
         head.wait()
-        step_head(1.0 / self.world)
+        step_head(scale)
+        return None
 
     def _reattach(self, params, skip_tail=False):
         """Point every .grad back at its slice of `flat`, copying a detached gradient in (None: zero, except the

@@ -106,7 +106,7 @@ class GStexTrainer:
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
-                 async_texture: bool = False):
+                 async_texture: bool = False, defer_texture: bool = False):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -158,13 +158,21 @@ class GStexTrainer:
         # no per-step zero fill remains.  Anything else reading texture_dc after optimizer_step() must call
         # wait_texture() first (eval_render and recharge in this class do).
         self.async_texture = bool(async_texture) and fused_adam and self.device.type == "cuda"
+        # defer_texture (not in the reference; fused Adam on a HIP device; exclusive with async_texture): the texel
+        # parameter's Adam update of step k runs inside step k+1's render, queued right after the binning's pair count
+        # is read back -- the device runs it while the host waits for that count and sizes the pair buffers (an idle
+        # gap of the device otherwise), and before the raster forward, the first reader of the texels.  Same updates
+        # in the same order on the same stream; the gradient is a persistent buffer the update zeroes as it reads it.
+        # Readers of texture_dc outside the step go through wait_texture() / texels(), which run a pending update.
+        self.defer_texture = bool(defer_texture) and not self.async_texture and fused_adam and self.device.type == "cuda"
+        self._pending_tex = None
         self._tex_stream = torch.cuda.Stream(device=d) if self.async_texture else None
         self._tex_ready = None
         self._tex_grad = None
         # the side-stream update's workgroup cap (GSTEX_TEX_ADAM_GRID; 0 = full grid).  Measured at cfg3: no cap, 512,
         # 256, 128, 64 -- none gains over the compute-stream update
         self._tex_grid = int(os.environ.get("GSTEX_TEX_ADAM_GRID", "0")) if self.async_texture else 0
-        if self.async_texture:
+        if self.async_texture or self.defer_texture:
             self._own_texture_grad()
         self._build_optimizer()
 
@@ -174,8 +182,21 @@ class GStexTrainer:
         self.texture_dc.grad = self._tex_grad
         self.texture_grad_sink = self._tex_grad
 
+    @property
+    def texture_grad_zeroed_by_update(self) -> bool:
+        """The texel Adam update zeroes the texel gradient as it reads it (async_texture / defer_texture): a
+        gradient-buffer owner (gstex_amd.dist.GradSync) must not fill that slice itself."""
+        return self.async_texture or self.defer_texture
+
+    def _run_pending_texture(self):
+        fn, self._pending_tex = self._pending_tex, None
+        if fn is not None:
+            fn()
+
     def wait_texture(self):
-        """Order the current stream after the pending side-stream texel update (async_texture)."""
+        """Order the current stream after the pending texel update: a deferred one (defer_texture) is enqueued now,
+        a side-stream one (async_texture) is waited for."""
+        self._run_pending_texture()
         if self._tex_ready is not None:
             torch.cuda.current_stream(self.device).wait_event(self._tex_ready)
             self._tex_ready = None
@@ -247,7 +268,8 @@ class GStexTrainer:
             ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs, texture_grad_sink=self.texture_grad_sink,
-            on_texture_grad=self.texture_grad_ready, texture_ready=self._tex_ready)
+            on_texture_grad=self.texture_grad_ready, texture_ready=self._tex_ready,
+            before_pair_wait=self._run_pending_texture if self._pending_tex is not None else None)
         self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
@@ -332,6 +354,18 @@ class GStexTrainer:
         of the step: the texel group is updated as soon as its collective lands, overlapping the head's collective,
         and the 1 / world averaging rides in the fused update (GradSync.all_reduce_and_step); otherwise call
         sync.all_reduce() before this."""
+        if self.defer_texture:
+            self._run_pending_texture()  # (two steps without a render in between)
+            tex = {id(self.texture_dc)}
+            if sync is not None:
+                self._pending_tex = sync.all_reduce_and_step(
+                    lambda s: self.optimizer.step(only=tex, zero_grad=True, grad_scale=s),
+                    lambda s: self.optimizer.step(skip=tex, grad_scale=s), defer_tail=True)
+            else:
+                self.optimizer.step(skip=tex)
+                self._pending_tex = lambda: self.optimizer.step(only=tex, zero_grad=True)
+            self.step += 1
+            return
         if sync is not None and self.fused_adam and not self.async_texture:
             tex = {id(self.texture_dc)}
             sync.all_reduce_and_step(lambda s: self.optimizer.step(only=tex, grad_scale=s),
@@ -367,7 +401,7 @@ class GStexTrainer:
         writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
         when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead).  With
         async_texture the texel gradient buffer is kept (the side-stream Adam zeroes it)."""
-        if self.async_texture:
+        if self.async_texture or self.defer_texture:
             keep = self.texture_dc.grad
             self.optimizer.zero_grad(set_to_none=set_to_none)
             self.texture_dc.grad = keep
@@ -405,7 +439,7 @@ class GStexTrainer:
                     "exp_avg": torch.zeros_like(self.texture_dc),
                     "exp_avg_sq": torch.zeros_like(self.texture_dc),
                 }
-            if self.async_texture:  # a fresh persistent gradient buffer (GradSync, if any, replaces it at rebuild)
+            if self.async_texture or self.defer_texture:  # a fresh persistent gradient buffer (GradSync replaces it)
                 self._own_texture_grad()
         else:
             st = self.optimizer.state.get(old)

@@ -326,7 +326,7 @@ class _TextureGaussians(torch.autograd.Function):
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                 block_width, settings, background, texture_transform=None, fold_aabb=False,
                 geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None,
-                texture_ready=None, binning=None):
+                texture_ready=None, binning=None, before_pair_wait=None):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -377,6 +377,8 @@ class _TextureGaussians(torch.autograd.Function):
                 ctx.v_texture = texture_grad_sink
             else:
                 ctx.v_texture = torch.zeros_like(texture)
+        if before_pair_wait is not None:
+            before_pair_wait()  # caller's work for the device while the host waits for the pair count
         if binning is None:
             offsets, tile_ranges, sorted_ids, sorted_slots, order = bin_finish(
                 begun, centers_c.detach(), extents_c, depths_c, H, W, BLOCK_WIDTH, with_order=True)
@@ -495,14 +497,14 @@ class _TextureGaussians(torch.autograd.Function):
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
                       fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None,
-                      texture_ready=None, binning=None):
+                      texture_ready=None, binning=None, before_pair_wait=None):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -527,6 +529,10 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     forward -- the texel update of the previous optimizer step running on a side stream (GStexTrainer
     async_texture), so preprocessing and binning overlap it.
 
+    before_pair_wait (not in the reference API): a callable run after the pair-count read-back has been queued and
+    before the host waits for it -- work it enqueues keeps the device busy through that wait (GStexTrainer
+    defer_texture: the previous step's texel update).
+
     binning (not in the reference API): a Binning from bin_gaussians() on the same centers / extents / depths /
     num_tiles_hit tensors -- several renders of one geometry (the eval render's three calls, gstex.py:1165-1200)
     bin and sort once.
@@ -543,7 +549,7 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
                                    fold_aabb, geometry_outputs, torch.is_grad_enabled(), texture_grad_sink,
-                                   on_texture_grad, texture_ready, binning)
+                                   on_texture_grad, texture_ready, binning, before_pair_wait)
 
 
 class Binning(NamedTuple):

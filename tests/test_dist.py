@@ -167,6 +167,19 @@ def _trainer_worker(rank, world, port, q):
         res["overlap_sums"] = bool(torch.allclose(calls[0][2], sum_w * tr.texture_dc.detach())
                                    and torch.allclose(calls[1][2], torch.full_like(tr.means, sum_w))
                                    and torch.all(calls[1][3] == 0))
+        # deferred tail (GStexTrainer defer_texture): the head is stepped at once, the tail's step comes back as a
+        # callable, run later (in the next step's render) with the same sums and scale
+        sync.zero()
+        tr.backward(rank)
+        calls = []
+        pending = sync.all_reduce_and_step(lambda sc: calls.append(("tail", sc, tr.texture_dc.grad.clone())),
+                                           lambda sc: calls.append(("head", sc, tr.means.grad.clone())),
+                                           defer_tail=True)
+        res["defer_head_first"] = [c[0] for c in calls] == ["head"] and callable(pending)
+        pending()
+        res["defer_tail_later"] = ([c[0] for c in calls] == ["head", "tail"]
+                                   and all(abs(c[1] - 1.0 / world) < 1e-15 for c in calls)
+                                   and bool(torch.allclose(calls[1][2], sum_w * tr.texture_dc.detach())))
         # a second backward without all_reduce() in between is refused: by zero(), and by the sink's ready callback
         # (its kernel would add into the slice the running collective reads)
         sync.zero()
@@ -207,5 +220,6 @@ def test_trainer_layout_sink_and_recharts_world2():
         assert r["double_backward_refused"]
         assert r["double_backward_sink_refused"]
         assert r["overlap_order"] and r["overlap_scale"] and r["overlap_sums"], r
+        assert r["defer_head_first"] and r["defer_tail_later"], r
         for step in range(2):
             assert r[f"set_to_none_{step}"], f"rank {rank}: zero_grad(set_to_none) after zero() mis-reduced (step {step})"

@@ -121,3 +121,56 @@ def test_async_texture_update_matches_sync_step():
                 assert err < 1e-5, f"{name}: async texel update differs ({err:.2e})"
     finally:
         dist.destroy_process_group()
+
+
+def test_deferred_texture_update_matches_plain_step():
+    """defer_texture: step k's texel Adam update runs inside step k+1's render (while the host reads back the pair
+    count); alone and under GradSync (world 1, the overlapped exchange of optimizer_step(sync=...)), across an
+    in-place and a growing rechart and an eval render, it must train like the plain step."""
+    from gstex_amd.dist import GradSync
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        sc = make_scene(4000, 80_000, seed=6)
+        views = [sphere_view(i, 96, 96).to(dev) for i in range(3)]
+        g = torch.Generator().manual_seed(2)
+        gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(3)]
+        plain = GStexTrainer(sc, dev, start_step=3000)
+        alone = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+        synced = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+        assert alone.defer_texture and synced.defer_texture
+        sync = GradSync(synced, 1)
+        for step in range(6):
+            for tr in (plain, alone):
+                tr.zero_grad()
+                tr.forward_backward(views[step % 3], gts[step % 3])
+                tr.optimizer_step()
+            sync.zero()
+            synced.forward_backward(views[step % 3], gts[step % 3])
+            synced.optimizer_step(sync=sync)
+            assert alone._pending_tex is not None and synced._pending_tex is not None
+            if step in (1, 3):
+                for tr in (plain, alone, synced):
+                    tr.pixel_num = (0.9 if step == 1 else 1.3) * tr.texture_dc.shape[0]
+                    tr.recharge()
+            if step == 2:
+                ev = [tr.eval_render(views[0])["rgb"] for tr in (plain, alone)]
+                assert float((ev[0] - ev[1]).abs().max()) < 1e-4
+        for tr in (alone, synced):
+            tr.wait_texture()
+        torch.cuda.synchronize()
+        # the persistent texel-gradient buffers are left zeroed by the deferred update
+        assert float(alone.texture_dc.grad.abs().max()) == 0.0
+        assert float(sync.flat[sync._tail_off:].abs().max()) == 0.0
+        for other in (alone, synced):
+            assert other.texture_dc.shape == plain.texture_dc.shape
+            for (name, a), b in zip(plain.param_groups().items(), other.param_groups().values()):
+                a, b = a[0].detach().double(), b[0].detach().double()
+                err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-30)
+                assert err < 1e-5, f"{name}: deferred texel update differs ({err:.2e})"
+    finally:
+        dist.destroy_process_group()
