@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 REC_FLOATS = 32
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
@@ -67,6 +67,7 @@ SIGNATURES = {
     "gstex_aabb_2d": (c_int32, [c_int32, _P, _P, c_float, _P, _CAM, _P, _P, _P]),
     "gstex_aabb_2d_bwd": (c_int32, [c_int32, _P, _P, c_float, _P, _CAM, _P, _P, _P, _P, _P]),
     "gstex_num_tiles_hit": (c_int32, [c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P]),
+    "gstex_preprocess": (c_int32, [c_int32, _P, _P, c_float, _P, _CAM, _P, _P, _P, _P, _P]),
     "gstex_scan_workspace_size": (c_size_t, [c_int32]),
     "gstex_scan_offsets": (c_int32, [c_int32, _P, _P, _P, c_size_t, _P]),
     "gstex_bin_workspace_size": (c_size_t, [c_int32, c_int64, c_int32]),

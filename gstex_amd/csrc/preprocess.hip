@@ -140,7 +140,48 @@ __global__ __launch_bounds__(kBlock) void num_tiles_kernel(int n, const float* _
     out[i] = (r.x1 - r.x0) * (r.y1 - r.y0);
 }
 
+// The three preprocessing outputs the raster needs, in one pass over the splats (the training path calls them
+// back to back on the same inputs): view depth as project_points_kernel, centre / extent as aabb_kernel and the
+// tile count as num_tiles_kernel compute them -- the same device functions, so bit-identical.
+__global__ __launch_bounds__(kBlock) void preprocess_kernel(int n, const float* __restrict__ means,
+                                                            const float* __restrict__ scales, float glob,
+                                                            const float* __restrict__ quats, CamArgs cam_args,
+                                                            int tiles_x, int tiles_y, int block,
+                                                            float* __restrict__ depths, float* __restrict__ centers,
+                                                            float* __restrict__ extents, int32_t* __restrict__ nth) {
+    const Camera cam = load_camera(cam_args);
+    int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    f3 mu = mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+    depths[i] = vrow(cam, 2, mu) + cam.V[11];
+    Frame fr;
+    float su, sv;
+    Homog h = load_homog(i, means, scales, glob, quats, cam, fr, su, sv);
+    float cx = 0.0f, cy = 0.0f, ex = 0.0f, ey = 0.0f;
+    if (!aabb_from_homog(h, cx, cy, ex, ey)) { cx = cy = ex = ey = 0.0f; }
+    centers[2 * i] = cx;
+    centers[2 * i + 1] = cy;
+    extents[2 * i] = ex;
+    extents[2 * i + 1] = ey;
+    Rect r = tile_rect(cx, cy, ex, ey, tiles_x, tiles_y, block);
+    nth[i] = (r.x1 - r.x0) * (r.y1 - r.y0);
+}
+
 }  // namespace
+
+extern "C" int gstex_preprocess(int32_t n, const float* means, const float* scales, float glob_scale,
+                                const float* quats, const gstex_camera* cam, float* depths, float* centers,
+                                float* extents, int32_t* num_tiles_hit, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && cam && cam->H >= 0 && cam->W >= 0 && cam->block > 0, "gstex_preprocess: invalid arguments");
+    if (n == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(means && scales && quats && depths && centers && extents && num_tiles_hit,
+                  "gstex_preprocess: null pointer");
+    const int tx = (cam->W + cam->block - 1) / cam->block, ty = (cam->H + cam->block - 1) / cam->block;
+    preprocess_kernel<<<div_up(n, kBlock), kBlock, 0, as_stream(stream)>>>(
+        n, means, scales, glob_scale, quats, to_device_camera(*cam), tx, ty, cam->block, depths, centers, extents,
+        num_tiles_hit);
+    return launch_status("gstex_preprocess");
+}
 
 extern "C" int gstex_project_points(int32_t n, const float* means, const gstex_camera* cam, float* xys,
                                     float* depths, void* stream) {

@@ -137,6 +137,9 @@ class GStexTrainer:
         self.settings = settings
         self.pixel_num = pixel_num if pixel_num is not None else float(scene.texture.shape[0])
         self.background = torch.tensor(background, dtype=torch.float32, device=d)
+        # the raster's own background is zero (the composite adds the real one, gstex.py:1204): one cached tensor
+        self._bg_zero = torch.zeros_like(self.background)
+        self._one = torch.ones((), dtype=torch.float32, device=d)
         self.step = start_step
         self.sh_degree_interval = sh_degree_interval  # gstex.py:182
         self.fix_init = fix_init  # gstex.py:209 (DTU configs): SH view directions (x, -z, y), gstex.py:1104-1108
@@ -248,9 +251,9 @@ class GStexTrainer:
         if self.fix_init and self.sh_degree > 0:
             viewdirs = torch.stack([viewdirs[:, 0], -viewdirs[:, 2], viewdirs[:, 1]], -1)
         intr = (view.fx, view.fy, view.cx, view.cy)
-        _, depths = ops.project_points(means, view.viewmat, intr)
-        centers, extents = ops.get_aabb_2d(means, scales, 1, quats, view.viewmat, intr)
-        nth = ops.get_num_tiles_hit_2d(centers, extents, view.H, view.W, ops.BLOCK_WIDTH)
+        # project_points / get_aabb_2d / get_num_tiles_hit_2d (gstex.py:1077-1080) in one launch; the centre
+        # gradient is chained inside the raster backward (fold_aabb below), the depths only order the tile lists
+        depths, centers, extents, nth = ops.preprocess(means, scales, 1, quats, view.viewmat, intr, view.H, view.W)
         n = self.means.shape[0]
         if self.sh_degree > 0:
             if self.fused_activations:  # the zeroed DC term (gstex.py:1100) without the cat
@@ -265,7 +268,7 @@ class GStexTrainer:
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
-            ops.BLOCK_WIDTH, self.settings, background=torch.zeros_like(self.background),
+            ops.BLOCK_WIDTH, self.settings, background=self._bg_zero,
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs, texture_grad_sink=self.texture_grad_sink,
             on_texture_grad=self.texture_grad_ready, texture_ready=self._tex_ready,
@@ -300,7 +303,7 @@ class GStexTrainer:
         if self.test_colors is None or self.test_colors.shape[0] != n:
             g = torch.Generator(device="cpu").manual_seed(0)
             self.test_colors = torch.rand((n, 3), generator=g).to(means.device)  # gstex.py:309
-        bgz = torch.zeros_like(self.background)
+        bgz = self._bg_zero
         # the three calls share one geometry: binned and sorted once.  The reference's 6-channel texture is
         # [SH2RGB(texture_dc), 0, 0, 0] for the first call and [edit_texture or 0, 0, 0, 0] for the other two; a
         # zero texel contributes exactly 0, so each call runs the 3-channel raster (SH2RGB as texture_transform,
@@ -346,7 +349,7 @@ class GStexTrainer:
         else:
             rgb = out["rgb"]
             loss = self.loss(rgb, gt)
-        loss.backward()
+        loss.backward(self._one)  # (a cached seed: no per-step fill launch for the implicit ones_like)
         return StepOutput(loss.detach(), rgb.detach())
 
     def optimizer_step(self, sync=None):

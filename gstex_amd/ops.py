@@ -202,6 +202,28 @@ def get_num_tiles_hit_2d(centers, extents, H: int, W: int, block_width: int) -> 
     return out
 
 
+def preprocess(means, scales, glob_scale, quats, viewmat, intrinsics, H: int, W: int):
+    """project_points' depths, get_aabb_2d and get_num_tiles_hit_2d in one launch (gstex_preprocess) ->
+    (depths (N,), centers (N,2), extents (N,2), num_tiles_hit (N,) int32), bit-identical to the three calls and
+    without autograd: for texture_gaussians(..., fold_aabb=True), whose backward chains the centre gradient itself
+    (the training path; gstex.py:1077-1080)."""
+    fx, fy, cx, cy = [float(v) for v in intrinsics]
+    means = _f32(means.detach(), "means", (None, 3))
+    n = means.shape[0]
+    scales = _f32(scales.detach(), "scales", (n, 3))
+    quats = _f32(quats.detach(), "quats", (n, 4))
+    vm = _viewmat(viewmat)
+    f = dict(device=means.device, dtype=torch.float32)
+    depths = torch.empty((n,), **f)
+    centers = torch.empty((n, 2), **f)
+    extents = torch.empty((n, 2), **f)
+    nth = torch.empty((n,), device=means.device, dtype=torch.int32)
+    cam = _lib.make_camera(vm, None, fx, fy, cx, cy, H, W, BLOCK_WIDTH)
+    call("gstex_preprocess", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), cam, ptr(depths),
+         ptr(centers), ptr(extents), ptr(nth), _stream(means))
+    return depths, centers, extents, nth
+
+
 # ----------------------------------------------------------------------------------------
 # binning
 # ----------------------------------------------------------------------------------------

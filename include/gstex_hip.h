@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 9
+#define GSTEX_ABI_VERSION 10
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -90,6 +90,13 @@ int gstex_aabb_2d_bwd(int32_t n, const float* means, const float* scales, float 
                       float* v_means, float* v_scales, float* v_quats, void* stream);
 int gstex_num_tiles_hit(int32_t n, const float* centers, const float* extents, int32_t H,
                         int32_t W, int32_t block, int32_t* num_tiles_hit, void* stream);
+/* The three preprocessing outputs a render needs, in one pass (ABI 10): depths[n] (the view depth of
+ * gstex_project_points), centers / extents[n][2] (gstex_aabb_2d) and num_tiles_hit[n]
+ * (gstex_num_tiles_hit with cam->H, cam->W, cam->block), bit-identical to the three calls.  No
+ * backward: a caller that needs the centre gradient uses gstex_raster_setup_bwd_aabb (fold). */
+int gstex_preprocess(int32_t n, const float* means, const float* scales, float glob_scale,
+                     const float* quats, const gstex_camera* cam, float* depths, float* centers,
+                     float* extents, int32_t* num_tiles_hit, void* stream);
 
 /* ---- binning + per-tile depth sort ---------------------------------------------------- */
 size_t gstex_scan_workspace_size(int32_t n);

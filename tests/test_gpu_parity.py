@@ -52,6 +52,12 @@ def test_project_points_and_aabb_match_oracle():
     onth = O.num_tiles_hit(oc, oe, 100, 120)
     assert torch.equal(nth.cpu(), onth)
     assert int((nth == 0).sum()) > 0, "case should contain culled / off-screen splats"
+    # the fused launch (gstex_preprocess, the training path): the same three outputs, bit for bit
+    from gstex_amd import ops
+
+    d2, c2, e2, n2 = ops.preprocess(inp.means.to(DEV), inp.scales.to(DEV), 1, inp.quats.to(DEV), v.viewmat.to(DEV),
+                                    intr, 100, 120)
+    assert torch.equal(d2.cpu(), odep) and torch.equal(c2, c) and torch.equal(e2, e) and torch.equal(n2, nth)
 
 
 def test_aabb_and_projection_backward():
