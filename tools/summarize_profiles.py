@@ -64,7 +64,7 @@ def main(tag):
     json.dump({"tag": tag, "kernels": rows}, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary `{tag}`\n\nCommand: `tools/profile_bench.sh {tag}` = rocprofv3 over "
-                 "`python3 bench.py --no-cpu-baseline --no-sub` (the default 20 timed + 5 warmup steps of the bench line, sub-records skipped; cfg3: 200k splats, 1e7 texels, "
+                 "`python3 bench.py --no-cpu-baseline --no-sub` (the default 30 timed + 20 warmup steps of the bench line, sub-records skipped; cfg3: 200k splats, 1e7 texels, "
                  "800x800, full train step).\nTraffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch "
                  "(separate --pmc passes; gfx950 FETCH_SIZE halving corrected).\nVALU issue = SQ_INSTS_VALU "
                  "per launch / (avg duration x 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction).\n\n")
