@@ -282,9 +282,8 @@ def main():
         # N > 1: the collectives inside the step (texel group updated while the head's collective runs)
         trainer.optimizer_step(sync=sync)
 
-    for _ in range(args.warmup):
-        step()
-    # counted quantities for the roofline (every pose of this rank's cycle, current parameters)
+    # counted quantities for the roofline (every pose of this rank's cycle; the geometry is stationary), before the
+    # warmup: host work between the warmup and the timed steps would idle the device and let its clock drop
     with torch.no_grad():
         quats = trainer.quats / trainer.quats.norm(dim=-1, keepdim=True)
         s = torch.exp(trainer.scales[:, :-1])
@@ -297,6 +296,8 @@ def main():
             abs_.append(algorithmic_bytes(nth.cpu(), trainer.texture_dims.cpu(), H, W))
         ab = {k: sum(a[k] for a in abs_) / len(abs_) for k in abs_[0]}
 
+    for _ in range(args.warmup):
+        step()
     trainer.wait_texture()  # the last warmup step's deferred texel update, outside the timed region
     if world > 1:
         dist.barrier()
