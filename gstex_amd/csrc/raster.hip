@@ -1267,6 +1267,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     if (st_n4 == 0 || st_n4 == 4 || (m & st_acc4)) { GSTEX_STAT(18, 1); st_acc4 = m; st_n4 = 1; }
                     else { st_acc4 |= m; ++st_n4; }
                     st_lanes += __popcll(m);
+                    // 8x4 half-blocks (lanes 0-31 = rows 0-3, 32-63 = rows 4-7) with a contributing pixel
+                    GSTEX_STAT(20, (unsigned long long)(((unsigned)m != 0u) + ((unsigned)(m >> 32) != 0u)));
                 }
             }
 #endif
