@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--n-splats", type=int, default=20_000)
     ap.add_argument("--n-texels", type=float, default=4e5)
     ap.add_argument("--size", type=int, default=160)
+    ap.add_argument("--defer-texture", action="store_true",
+                    help="GStexTrainer(defer_texture=True): the texel update of step k runs in step k+1's render")
     args = ap.parse_args()
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
@@ -57,7 +59,7 @@ def main():
     views = [sphere_view(i, S, S, n_views=N_POSES).to(dev) for i in range(N_POSES)]
     g = torch.Generator().manual_seed(2024)
     gts = [torch.rand((S, S, 3), generator=g).to(dev) for _ in range(N_POSES)]
-    tr = GStexTrainer(sc, dev, start_step=3000)
+    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=args.defer_texture)
     sync = GradSync(tr, world)
     ref = GStexTrainer(sc, dev, start_step=3000) if rank == 0 else None
     log = []
@@ -104,6 +106,7 @@ def main():
             say(f"rechart after step 1: texel store {cap} -> {tr.texture_dc.shape[0]} rows "
                 f"(new Parameter: {tr.texture_dc is not old}), n_texels {tr.n_texels}")
             ok &= grew
+    tr.wait_texture()  # a deferred texel update (--defer-texture) still pending after the last step
     torch.cuda.synchronize()
     # every rank equals rank 0; rank 0 equals the single-rank mean-gradient reference
     for name, prm in zip([n for n in tr.param_groups()], tr.parameters()):
@@ -124,7 +127,8 @@ def main():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok &= bool(flag.item() == 1.0)
         say(line + ("" if flag.item() == 1.0 else "   <-- FAIL"))
-    say(f"flat buffer {sync.nbytes / 1e6:.1f} MB, backend {dist.get_backend()}, world {world}, {args.steps} steps")
+    say(f"flat buffer {sync.nbytes / 1e6:.1f} MB, backend {dist.get_backend()}, world {world}, {args.steps} steps, "
+        f"defer_texture {tr.defer_texture}")
     say(("REHEARSAL OK" if ok else "REHEARSAL FAILED") + f" world={world}")
     dist.barrier()
     dist.destroy_process_group()
