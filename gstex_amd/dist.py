@@ -48,6 +48,11 @@ class GradSync:
         self._hooked = None
         self._work = None
         self._sink = hasattr(trainer, "texture_grad_sink")
+        # head first (a trainer that defers its texel update into the next step, GStexTrainer defer_texture): the
+        # tail's collective is not started from the raster backward but queued right behind the head's at the step,
+        # so the head (45 MB) lands first, the next step starts on it, and the tail (120 MB) only has to land by that
+        # step's raster forward
+        self.head_first = bool(getattr(trainer, "defer_texture", False))
         self.rebuild()
 
     def _params(self):
@@ -76,7 +81,8 @@ class GradSync:
         self._tail_off = total - params[-1].numel()
         if self._sink:
             self.trainer.texture_grad_sink = params[-1].grad
-            self.trainer.texture_grad_ready = self._tail_ready_sink if self.overlap_tail else None
+            self.trainer.texture_grad_ready = (self._tail_ready_sink if self.overlap_tail and not self.head_first
+                                               else None)
         else:
             self._install_hook(params[-1])
         return True
@@ -161,6 +167,18 @@ class GradSync:
         defer_texture: it runs inside the next step's render, after the tail collective has had that much longer)."""
         work, self._work = self._work, None
         params = self._params()
+        if defer_tail and self.head_first and work is None and self._layout(params) == self._key:
+            self._reattach(params, skip_tail=self._sink)
+            head = dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            tail = dist.all_reduce(self.flat[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            scale = 1.0 / self.world
+            head.wait()
+            step_head(scale)
+
+            def tail_step():
+                tail.wait()
+                step_tail(scale)
+            return tail_step
         if work is None or self._layout(params) != self._key:
             if work is not None:
                 work.wait()

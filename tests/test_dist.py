@@ -195,6 +195,24 @@ def _trainer_worker(rank, world, port, q):
         except RuntimeError:
             res["double_backward_sink_refused"] = True
         sync.all_reduce()
+        # head first (a trainer that defers its texel update, GStexTrainer defer_texture): the backward starts no
+        # collective; the step queues the head's then the tail's, steps the head, and returns the tail's step
+        tr2 = _SinkTrainer()
+        tr2.defer_texture = True
+        sync2 = GradSync(tr2, world)
+        sync2.zero()
+        tr2.backward(rank)
+        res["head_first_no_early_tail"] = sync2.head_first and sync2._work is None
+        calls = []
+        pending = sync2.all_reduce_and_step(lambda sc: calls.append(("tail", sc, tr2.texture_dc.grad.clone())),
+                                            lambda sc: calls.append(("head", sc, tr2.means.grad.clone())),
+                                            defer_tail=True)
+        first = [c[0] for c in calls] == ["head"]
+        pending()
+        res["head_first_sums"] = (first and [c[0] for c in calls] == ["head", "tail"]
+                                  and all(abs(c[1] - 1.0 / world) < 1e-15 for c in calls)
+                                  and bool(torch.allclose(calls[0][2], torch.full_like(tr2.means, sum_w)))
+                                  and bool(torch.allclose(calls[1][2], sum_w * tr2.texture_dc.detach())))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -221,5 +239,6 @@ def test_trainer_layout_sink_and_recharts_world2():
         assert r["double_backward_sink_refused"]
         assert r["overlap_order"] and r["overlap_scale"] and r["overlap_sums"], r
         assert r["defer_head_first"] and r["defer_tail_later"], r
+        assert r["head_first_no_early_tail"] and r["head_first_sums"], r
         for step in range(2):
             assert r[f"set_to_none_{step}"], f"rank {rank}: zero_grad(set_to_none) after zero() mis-reduced (step {step})"

@@ -20,6 +20,20 @@ def _port():
     return p
 
 
+def _assert_trains_alike(name, a, b, what):
+    """Parameters of two trainers after the same steps.  Gradients are float-atomic sums (texels always, splat sums
+    outside the deterministic mode) whose order varies run to run, and Adam's m / sqrt(v) (eps 1e-15) turns the noise
+    of a near-zero gradient into up to one step of update: every element within one step's learning rate, and the
+    mean difference within 1e-6 of the largest magnitude (a wrong exchange or update moves the mean far more)."""
+    from gstex_amd.model import LRS
+
+    a, b = a.detach().double(), b.detach().double()
+    scale = max(float(a.abs().max()), 1e-30)
+    d = (a - b).abs()
+    err, mean = float(d.max()) / scale, float(d.mean()) / scale
+    assert float(d.max()) <= LRS[name] and mean < 1e-6, f"{name}: {what} differs (max {err:.2e}, mean {mean:.2e})"
+
+
 def test_synced_step_matches_unsynced_across_rechart():
     from gstex_amd.dist import GradSync
     from gstex_amd.model import GStexTrainer
@@ -64,10 +78,7 @@ def test_synced_step_matches_unsynced_across_rechart():
                 assert (sync.flat is flat) == (step == 1), "flat buffer kept in place / rebuilt after growth"
         assert synced.texture_dc.shape == plain.texture_dc.shape
         for (name, a), b in zip(plain.param_groups().items(), synced.param_groups().values()):
-            a, b = a[0].detach().double(), b[0].detach().double()
-            # texel gradients combine tiles with fp32 atomics (summation order): tiny differences, then Adam
-            err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-30)
-            assert err < 1e-5, f"{name}: synced step differs ({err:.2e})"
+            _assert_trains_alike(name, a[0], b[0], "synced step")
     finally:
         dist.destroy_process_group()
 
@@ -116,9 +127,7 @@ def test_async_texture_update_matches_sync_step():
         assert float(sync.flat[sync._tail_off:].abs().max()) == 0.0
         for other in (alone, synced):
             for (name, a), b in zip(plain.param_groups().items(), other.param_groups().values()):
-                a, b = a[0].detach().double(), b[0].detach().double()
-                err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-30)
-                assert err < 1e-5, f"{name}: async texel update differs ({err:.2e})"
+                _assert_trains_alike(name, a[0], b[0], "async texel update")
     finally:
         dist.destroy_process_group()
 
@@ -169,8 +178,6 @@ def test_deferred_texture_update_matches_plain_step():
         for other in (alone, synced):
             assert other.texture_dc.shape == plain.texture_dc.shape
             for (name, a), b in zip(plain.param_groups().items(), other.param_groups().values()):
-                a, b = a[0].detach().double(), b[0].detach().double()
-                err = float((a - b).abs().max()) / max(float(a.abs().max()), 1e-30)
-                assert err < 1e-5, f"{name}: deferred texel update differs ({err:.2e})"
+                _assert_trains_alike(name, a[0], b[0], "deferred texel update")
     finally:
         dist.destroy_process_group()

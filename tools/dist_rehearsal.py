@@ -18,8 +18,9 @@ Exercised, per step:
   * after step 1: a rechart that GROWS the texel store (new Parameter, new flat buffer and sink at the next zero()).
 Checked on rank 0 against a single-rank reference trainer that runs the same `world` views per step, sums their
 gradients by autograd accumulation, scales by 1/world and takes the same Adam step (the mean-gradient step); every
-rank's parameters must equal rank 0's.  Tolerance: 1e-5 of each parameter's max magnitude (texel gradients combine
-tiles with float atomics, whose summation order varies run to run).
+rank's parameters must equal rank 0's.  Tolerance: 1e-5 of each parameter's max magnitude; for the texels (float-
+atomic gradient sums whose order varies run to run, through Adam's m / sqrt(v)) the worst texel within one step's
+learning rate and the mean difference within 1e-6 of the max magnitude.
 Test infrastructure; prints one line per check and `REHEARSAL OK world=N` at the end.
 """
 import argparse
@@ -76,7 +77,9 @@ def main():
         if step == 1:
             tr.zero_grad()  # set_to_none after zero(): detached autograd .grad tensors, folded back by all_reduce()
         tr.forward_backward(views[pose], gts[pose])
-        started = sync._work is not None
+        # the tail's collective starts from the raster backward -- unless the exchange is head first (a deferring
+        # trainer), where the step queues it behind the head's
+        started = (sync._work is not None) != sync.head_first
         if step == 0:  # the plain exchange: averaged gradient buffer, then the step
             sync.all_reduce()
             tr.optimizer_step()
@@ -84,8 +87,9 @@ def main():
             tr.optimizer_step(sync=sync)
         flags = torch.tensor([1.0 if started else 0.0], device=dev)
         dist.all_reduce(flags, op=dist.ReduceOp.MIN)
-        say(f"step {step}: poses {[(r + step * world) % N_POSES for r in range(world)]}, tail collective started "
-            f"from the raster backward on every rank: {bool(flags.item() == 1.0)}")
+        say(f"step {step}: poses {[(r + step * world) % N_POSES for r in range(world)]}, tail collective "
+            + ("queued behind the head's (head first)" if sync.head_first else "started from the raster backward")
+            + f" on every rank: {bool(flags.item() == 1.0)}")
         ok &= bool(flags.item() == 1.0)
         if ref is not None:
             ref.zero_grad()
@@ -122,7 +126,15 @@ def main():
             rp = dict(zip(ref.param_groups(), ref.parameters()))[name].detach()
             d_ref = float((r0 - rp).abs().max()) / scale
             line += f",  |rank0 - mean-gradient reference| / max|p| = {d_ref:.2e}"
-            good &= d_ref < 1e-5
+            if name == "texture_dc":
+                # texel gradients are float-atomic sums (summation order varies run to run) and Adam's m / sqrt(v)
+                # (eps 1e-15) turns a near-zero gradient's noise into up to one step (lr) of update: bound the worst
+                # texel by one step and the mean by 1e-6 of max|p|
+                d_mean = float((r0 - rp).abs().mean()) / scale
+                line += f" (mean {d_mean:.2e})"
+                good &= float((r0 - rp).abs().max()) <= ref.optimizer.param_groups[-1]["lr"] and d_mean < 1e-6
+            else:
+                good &= d_ref < 1e-5
         flag = torch.tensor([1.0 if good else 0.0], device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok &= bool(flag.item() == 1.0)
