@@ -13,7 +13,9 @@
 // backward needs, dS/d mu2, dS/d E[Y^2], dS/d E[XY] (gmaps).  A one-workgroup kernel then reduces
 // the partial sums in a fixed order (deterministic loss).
 // Backward: dS/dY(q) = sum over the windows containing q of w * (G_mu2 + 2 Y(q) G_yy + X(q) G_xy),
-// the transposed separable filter of the gmaps, evaluated the same tiled way.
+// the transposed separable filter of the gmaps, evaluated the same tiled way, channel by channel; the
+// composite's backward (d_img, d_tex, d_alpha) is written by the same workgroup once a pixel's three channels are
+// done (no dL/drgb buffer, no separate scatter launch).
 #include "gstex_common.h"
 #include "gstex_error.h"
 
@@ -192,90 +194,94 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int H, int W, int C, cons
                                                        const float* __restrict__ bg, const float* __restrict__ gt,
                                                        Win win, const float* __restrict__ gmaps,
                                                        const float* __restrict__ grad_loss, float k_l1,
-                                                       float k_ssim, float* __restrict__ d_rgb) {
+                                                       float k_ssim, float* __restrict__ d_img,
+                                                       float* __restrict__ d_tex, float* __restrict__ d_alpha) {
+    // one workgroup per 16x16 tile, the three channels in turn; the composite's backward (d_img, d_tex, d_alpha)
+    // written at the end, once every channel's dL/drgb of the pixel is known
     __shared__ float s_g[3][kReg][kReg + 1];
     __shared__ float s_h[3][kReg][kLT + 1];
     const LossTile lt = loss_tile();
-    const int c = lt.c;
     const int x0 = lt.bx * kLT, y0 = lt.by * kLT;  // output pixels [x0, x0+16)
     const int tid = threadIdx.x;
     const int Hv = H - kHalo, Wv = W - kHalo;
     const size_t plane = (size_t)3 * Hv * Wv;
-    // gmaps over positions [x0 - 10, x0 + 16)
-    for (int i = tid; i < kReg * kReg; i += 256) {
-        const int ry = i / kReg, rx = i % kReg;
-        const int py = y0 - kHalo + ry, px = x0 - kHalo + rx;
-        float g0 = 0.f, g1 = 0.f, g2 = 0.f;
-        if (py >= 0 && px >= 0 && py < Hv && px < Wv) {
-            const size_t o = ((size_t)c * Hv + py) * Wv + px;
-            g0 = gmaps[o];
-            g1 = gmaps[plane + o];
-            g2 = gmaps[2 * plane + o];
-        }
-        s_g[0][ry][rx] = g0;
-        s_g[1][ry][rx] = g1;
-        s_g[2][ry][rx] = g2;
-    }
-    __syncthreads();
-    // transposed rows: for output column cx, sum_k w[k] G(position cx + 10 - k)
-    for (int i = tid; i < kReg * kLT; i += 256) {
-        const int ry = i / kLT, cx = i % kLT;
-        float a = 0.f, b = 0.f, d = 0.f;
-#pragma unroll
-        for (int k = 0; k < kWin; ++k) {
-            a += win.w[k] * s_g[0][ry][cx + kHalo - k];
-            b += win.w[k] * s_g[1][ry][cx + kHalo - k];
-            d += win.w[k] * s_g[2][ry][cx + kHalo - k];
-        }
-        s_h[0][ry][cx] = a;
-        s_h[1][ry][cx] = b;
-        s_h[2][ry][cx] = d;
-    }
-    __syncthreads();
     const int cy = tid >> 4, cx = tid & 15;
     const int qy = y0 + cy, qx = x0 + cx;
-    if (qy >= H || qx >= W) return;
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < kWin; ++k) {
-        t0 += win.w[k] * s_h[0][cy + kHalo - k][cx];
-        t1 += win.w[k] * s_h[1][cy + kHalo - k][cx];
-        t2 += win.w[k] * s_h[2][cy + kHalo - k][cx];
-    }
+    const bool out = qy < H && qx < W;
     const size_t pix = (size_t)qy * W + qx;
-    float pre;
-    const float yv = composite(img, tex, alpha, bg, C, pix, c, pre);
-    const float xv = gt[3 * pix + c];
-    const float dS = (t0 + 2.0f * yv * t1) + xv * t2;
-    const float diff = xv - yv;
-    const float sgn = diff > 0.f ? 1.0f : (diff < 0.f ? -1.0f : 0.0f);
-    // L = w1 * mean|X - Y| + w2 * (1 - mean s): dL/dY = -w1 sign(X - Y) / N1 - w2 dS / Np
-    float g = -(k_l1 * sgn) - k_ssim * dS;
-    g *= grad_loss[0];
-    d_rgb[3 * pix + c] = (pre >= 0.0f && pre <= 1.0f) ? g : 0.0f;
-}
-
-// d_rgb -> d_img, d_tex (channels >= 3 get zero), d_alpha = -sum_c d_rgb_c bg_c
-__global__ __launch_bounds__(256) void loss_scatter_kernel(int HW, int C, const float* __restrict__ bg,
-                                                           const float* __restrict__ d_rgb,
-                                                           float* __restrict__ d_img, float* __restrict__ d_tex,
-                                                           float* __restrict__ d_alpha) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= HW) return;
-    const float g0 = d_rgb[3 * (size_t)p], g1 = d_rgb[3 * (size_t)p + 1], g2 = d_rgb[3 * (size_t)p + 2];
-    d_img[3 * (size_t)p] = g0;
-    d_img[3 * (size_t)p + 1] = g1;
-    d_img[3 * (size_t)p + 2] = g2;
-    for (int c = 0; c < C; ++c) d_tex[(size_t)C * p + c] = c == 0 ? g0 : (c == 1 ? g1 : (c == 2 ? g2 : 0.0f));
-    d_alpha[p] = -((g0 * bg[0] + g1 * bg[1]) + g2 * bg[2]);
+    const float gl = grad_loss[0];
+    float gch[3];
+    for (int c = 0; c < 3; ++c) {
+        if (c > 0) __syncthreads();  // the previous channel's passes are done with s_g / s_h
+        // gmaps over positions [x0 - 10, x0 + 16)
+        for (int i = tid; i < kReg * kReg; i += 256) {
+            const int ry = i / kReg, rx = i % kReg;
+            const int gy = y0 - kHalo + ry, gx = x0 - kHalo + rx;
+            float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+            if (gy >= 0 && gx >= 0 && gy < Hv && gx < Wv) {
+                const size_t o = ((size_t)c * Hv + gy) * Wv + gx;
+                g0 = gmaps[o];
+                g1 = gmaps[plane + o];
+                g2 = gmaps[2 * plane + o];
+            }
+            s_g[0][ry][rx] = g0;
+            s_g[1][ry][rx] = g1;
+            s_g[2][ry][rx] = g2;
+        }
+        __syncthreads();
+        // transposed rows: for output column hx, sum_k w[k] G(position hx + 10 - k)
+        for (int i = tid; i < kReg * kLT; i += 256) {
+            const int ry = i / kLT, hx = i % kLT;
+            float a = 0.f, b = 0.f, d = 0.f;
+#pragma unroll
+            for (int k = 0; k < kWin; ++k) {
+                a += win.w[k] * s_g[0][ry][hx + kHalo - k];
+                b += win.w[k] * s_g[1][ry][hx + kHalo - k];
+                d += win.w[k] * s_g[2][ry][hx + kHalo - k];
+            }
+            s_h[0][ry][hx] = a;
+            s_h[1][ry][hx] = b;
+            s_h[2][ry][hx] = d;
+        }
+        __syncthreads();
+        gch[c] = 0.f;
+        if (out) {
+            float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < kWin; ++k) {
+                t0 += win.w[k] * s_h[0][cy + kHalo - k][cx];
+                t1 += win.w[k] * s_h[1][cy + kHalo - k][cx];
+                t2 += win.w[k] * s_h[2][cy + kHalo - k][cx];
+            }
+            float pre;
+            const float yv = composite(img, tex, alpha, bg, C, pix, c, pre);
+            const float xv = gt[3 * pix + c];
+            const float dS = (t0 + 2.0f * yv * t1) + xv * t2;
+            const float diff = xv - yv;
+            const float sgn = diff > 0.f ? 1.0f : (diff < 0.f ? -1.0f : 0.0f);
+            // L = w1 * mean|X - Y| + w2 * (1 - mean s): dL/dY = -w1 sign(X - Y) / N1 - w2 dS / Np
+            float g = -(k_l1 * sgn) - k_ssim * dS;
+            g *= gl;
+            gch[c] = (pre >= 0.0f && pre <= 1.0f) ? g : 0.0f;
+        }
+    }
+    if (!out) return;
+    // rgb = clamp((img + tex) + (1 - alpha) bg): d_img = d_tex[0..2] = dL/drgb, channels >= 3 get zero,
+    // d_alpha = -sum_c dL/drgb_c bg_c
+    d_img[3 * pix] = gch[0];
+    d_img[3 * pix + 1] = gch[1];
+    d_img[3 * pix + 2] = gch[2];
+    for (int c = 0; c < C; ++c) d_tex[(size_t)C * pix + c] = c == 0 ? gch[0] : (c == 1 ? gch[1] : (c == 2 ? gch[2] : 0.0f));
+    d_alpha[pix] = -((gch[0] * bg[0] + gch[1] * bg[1]) + gch[2] * bg[2]);
 }
 
 }  // namespace
 
 using namespace gstex;
 
-static int loss_grid(int H, int W, dim3& grid) {
-    grid = dim3((unsigned)((W + kLT - 1) / kLT), (unsigned)((H + kLT - 1) / kLT), 3);
+// forward: one workgroup per (tile, channel); backward: one per tile (its three channels in turn)
+static int loss_grid(int H, int W, dim3& grid, int channels = 3) {
+    grid = dim3((unsigned)((W + kLT - 1) / kLT), (unsigned)((H + kLT - 1) / kLT), (unsigned)channels);
     return (int)(grid.x * grid.y * grid.z);
 }
 
@@ -284,20 +290,16 @@ extern "C" size_t gstex_loss_workspace_size(int32_t H, int32_t W) {
     dim3 g;
     const size_t parts = (size_t)loss_grid(H, W, g) * sizeof(float2);
     const size_t gm = (size_t)3 * 3 * (H - kHalo) * (W - kHalo) * sizeof(float);
-    const size_t drgb = (size_t)3 * H * W * sizeof(float);
-    return ((parts + 255) & ~(size_t)255) + ((gm + 255) & ~(size_t)255) + drgb;
+    return ((parts + 255) & ~(size_t)255) + gm;
 }
 
-static void loss_ws(int H, int W, void* ws, float2** part, float** gmaps, float** drgb) {
+static void loss_ws(int H, int W, void* ws, float2** part, float** gmaps) {
     dim3 g;
     const size_t parts = (size_t)loss_grid(H, W, g) * sizeof(float2);
-    const size_t gm = (size_t)3 * 3 * (H - kHalo) * (W - kHalo) * sizeof(float);
     char* b = (char*)ws;
     *part = (float2*)b;
     b += (parts + 255) & ~(size_t)255;
     *gmaps = (float*)b;
-    b += (gm + 255) & ~(size_t)255;
-    *drgb = (float*)b;
 }
 
 extern "C" int gstex_loss_fwd(int32_t H, int32_t W, int32_t C, const float* img, const float* tex,
@@ -313,8 +315,8 @@ extern "C" int gstex_loss_fwd(int32_t H, int32_t W, int32_t C, const float* img,
     Win win;
     for (int k = 0; k < kWin; ++k) win.w[k] = window[k];  // host array
     float2* part;
-    float *gmaps, *drgb;
-    loss_ws(H, W, workspace, &part, &gmaps, &drgb);
+    float* gmaps;
+    loss_ws(H, W, workspace, &part, &gmaps);
     dim3 grid;
     const int nparts = loss_grid(H, W, grid);
     hipStream_t st = as_stream(stream);
@@ -337,15 +339,14 @@ extern "C" int gstex_loss_bwd(int32_t H, int32_t W, int32_t C, const float* img,
     Win win;
     for (int k = 0; k < kWin; ++k) win.w[k] = window[k];
     float2* part;
-    float *gmaps, *drgb;
-    loss_ws(H, W, workspace, &part, &gmaps, &drgb);
+    float* gmaps;
+    loss_ws(H, W, workspace, &part, &gmaps);
     dim3 grid;
-    loss_grid(H, W, grid);
+    loss_grid(H, W, grid, 1);
     hipStream_t st = as_stream(stream);
     const float k_l1 = (float)((1.0 - ssim_lambda) / (3.0 * H * W));
     const float k_ssim = (float)(ssim_lambda / (3.0 * (H - kHalo) * (W - kHalo)));
     loss_bwd_kernel<<<grid, 256, 0, st>>>(H, W, C, img, tex, alpha, background, gt, win, gmaps, grad_loss, k_l1,
-                                          k_ssim, drgb);
-    loss_scatter_kernel<<<(H * W + 255) / 256, 256, 0, st>>>(H * W, C, background, drgb, d_img, d_tex, d_alpha);
+                                          k_ssim, d_img, d_tex, d_alpha);
     return launch_status("gstex_loss_bwd");
 }
