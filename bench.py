@@ -243,12 +243,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # "nccl" is RCCL on ROCm; GSTEX_DIST_BACKEND=gloo rehearses several ranks on one GPU
-        dist.init_process_group(os.environ.get("GSTEX_DIST_BACKEND", "nccl"), init_method="env://")
     dev_idx = local_rank % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev_idx)
+    torch.cuda.set_device(dev_idx)  # before the process group: its collectives and barrier() use this rank's GPU
     dev = torch.device("cuda", dev_idx)
+    if world > 1:
+        # "nccl" is RCCL on ROCm (bound to this rank's GPU); GSTEX_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        backend = os.environ.get("GSTEX_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, init_method="env://", device_id=dev if backend == "nccl" else None)
 
     from gstex_amd import ops
     from gstex_amd.dist import GradSync

@@ -36,11 +36,14 @@ class GradSync:
     Parameter rebuilds it.  One backward per all_reduce(): gradient accumulation over several backward passes
     is not supported (the tail would be reduced after the first)."""
 
-    def __init__(self, trainer, world_size: int, group=None, overlap_tail: bool = True):
+    def __init__(self, trainer, world_size: int, group=None, overlap_tail: bool = True, tail_chunks: int = 4):
         self.trainer = trainer
         self.world = world_size
         self.group = group
         self.overlap_tail = overlap_tail
+        # head first: the tail's collective in this many pieces, so that a chunked texel update (all_reduce_and_step
+        # step_tail_range) steps each piece while the next one is still on the wire
+        self.tail_chunks = max(1, int(tail_chunks))
         self._key = None
         self.flat = None
         self._tail_off = 0
@@ -58,6 +61,8 @@ class GradSync:
     def _params(self):
         return self.trainer.parameters()
 
+    ALIGN = 64  # elements
+
     @staticmethod
     def _layout(params):
         return [(id(p), tuple(p.shape)) for p in params]
@@ -69,16 +74,19 @@ class GradSync:
             return False
         if self.flat is not None and hasattr(self.trainer, "wait_texture"):
             self.trainer.wait_texture()  # a side-stream texel update may still read the old buffer
-        total = sum(p.numel() for p in params)
+        # every slice starts on a 256-B boundary (the fused Adam's float4 path needs 16-B aligned gradients)
+        offs = []
+        total = 0
+        for p in params:
+            offs.append(total)
+            total += -(-p.numel() // self.ALIGN) * self.ALIGN
         dev = params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
-        off = 0
-        for p in params:
-            n = p.numel()
-            p.grad = self.flat[off:off + n].view_as(p)
-            off += n
+        self._offs = offs
+        for p, off in zip(params, offs):
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
         self._key = key
-        self._tail_off = total - params[-1].numel()
+        self._tail_off = offs[-1]
         if self._sink:
             self.trainer.texture_grad_sink = params[-1].grad
             self.trainer.texture_grad_ready = (self._tail_ready_sink if self.overlap_tail and not self.head_first
@@ -154,7 +162,14 @@ class GradSync:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
 
-    def all_reduce_and_step(self, step_tail, step_head, defer_tail: bool = False):
+    def tail_bounds(self, n: int):
+        """The head-first tail collective's pieces: [lo, hi) element ranges of the tail parameter, 1024-element
+        (4 KiB) aligned, at most tail_chunks of them."""
+        k = max(1, min(self.tail_chunks, n // 1024))
+        step = -(-(-(-n // k)) // 1024) * 1024
+        return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
+
+    def all_reduce_and_step(self, step_tail, step_head, defer_tail: bool = False, step_tail_range=None):
         """A data-parallel optimizer step with the collectives overlapped (the trainer's optimizer_step(sync=...)).
 
         The tail collective (the texel store, started from the raster backward) is followed on the wire by the head's;
@@ -164,20 +179,31 @@ class GradSync:
         over the buffer), so after this call the buffer holds sums, not averages.  Without a running tail collective
         (overlap_tail=False, or no backward hook fired) this is all_reduce() followed by both steps at scale 1.
         defer_tail: the head is stepped now and the tail's step is returned as a callable instead of run (the trainer's
-        defer_texture: it runs inside the next step's render, after the tail collective has had that much longer)."""
+        defer_texture: it runs inside the next step's render, after the tail collective has had that much longer).
+        step_tail_range(scale, lo, hi, first) (head first only): the tail's update of its elements [lo, hi), so the
+        tail's collective goes out in pieces (tail_bounds) and each piece is stepped as soon as it lands; `first` marks
+        the piece that advances the optimizer's step count."""
         work, self._work = self._work, None
         params = self._params()
         if defer_tail and self.head_first and work is None and self._layout(params) == self._key:
             self._reattach(params, skip_tail=self._sink)
             head = dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            tail = dist.all_reduce(self.flat[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            bounds = self.tail_bounds(params[-1].numel()) if step_tail_range is not None else [(0, params[-1].numel())]
+            tails = [dist.all_reduce(self.flat[self._tail_off + lo:self._tail_off + hi], op=dist.ReduceOp.SUM,
+                                     group=self.group, async_op=True) for lo, hi in bounds]
             scale = 1.0 / self.world
             head.wait()
             step_head(scale)
 
             def tail_step():
-                tail.wait()
-                step_tail(scale)
+                if step_tail_range is None:
+                    tails[0].wait()
+                    step_tail(scale)
+                    return
+                # each piece stepped as soon as it has landed, while the next ones are still on the wire
+                for i, ((lo, hi), w) in enumerate(zip(bounds, tails)):
+                    w.wait()
+                    step_tail_range(scale, lo, hi, i == 0)
             return tail_step
         if work is None or self._layout(params) != self._key:
             if work is not None:
@@ -210,12 +236,9 @@ class GradSync:
     def _reattach(self, params, skip_tail=False):
         """Point every .grad back at its slice of `flat`, copying a detached gradient in (None: zero, except the
         texel store's slice when the raster backward accumulated straight into it -- the sink)."""
-        off = 0
         last = len(params) - 1
-        for i, p in enumerate(params):
-            n = p.numel()
-            view = self.flat[off:off + n]
-            off += n
+        for i, (p, off) in enumerate(zip(params, self._offs)):
+            view = self.flat[off:off + p.numel()]
             if p.grad is not None and p.grad.data_ptr() == view.data_ptr():
                 continue
             g = p.grad
@@ -241,10 +264,8 @@ class GradSync:
                 if g is not None:
                     p.grad.copy_(g)
             return
-        off = 0
-        for p in params:
-            n = p.numel()
-            view = self.flat[off:off + n]
+        for p, off in zip(params, self._offs):
+            view = self.flat[off:off + p.numel()]
             if p.grad is None or p.grad.data_ptr() != view.data_ptr():
                 g = p.grad
                 p.grad = view.view_as(p)
@@ -252,4 +273,3 @@ class GradSync:
                     p.grad.copy_(g)
                 else:
                     p.grad.zero_()
-            off += n

@@ -169,6 +169,7 @@ class GStexTrainer:
         # Readers of texture_dc outside the step go through wait_texture() / texels(), which run a pending update.
         self.defer_texture = bool(defer_texture) and not self.async_texture and fused_adam and self.device.type == "cuda"
         self._pending_tex = None
+        self._pending_collective = False  # the pending update first waits for a GradSync collective
         self._tex_stream = torch.cuda.Stream(device=d) if self.async_texture else None
         self._tex_ready = None
         self._tex_grad = None
@@ -265,14 +266,20 @@ class GStexTrainer:
             rgbs = torch.sigmoid(self.features_dc)
         # SH2RGB(texture_dc) (gstex.py:1119) applied by the raster on read instead of materialised
         texture = self.texture_dc
+        # the deferred texel update: while the host waits for the pair count (one GPU: it fills the device's idle time
+        # there), or -- when it first waits for its data-parallel collective (GradSync) -- right before the raster
+        # forward, so that the binning's placement and sort do not queue behind that wait
+        pend = self._pending_tex is not None
+        late = pend and self._pending_collective
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
             ops.BLOCK_WIDTH, self.settings, background=self._bg_zero,
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs, texture_grad_sink=self.texture_grad_sink,
-            on_texture_grad=self.texture_grad_ready, texture_ready=self._tex_ready,
-            before_pair_wait=self._run_pending_texture if self._pending_tex is not None else None)
+            on_texture_grad=self.texture_grad_ready,
+            texture_ready=self._run_pending_texture if late else self._tex_ready,
+            before_pair_wait=self._run_pending_texture if pend and not late else None)
         self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
@@ -361,12 +368,17 @@ class GStexTrainer:
             self._run_pending_texture()  # (two steps without a render in between)
             tex = {id(self.texture_dc)}
             if sync is not None:
+                # the texel update in pieces, each as soon as its piece of the collective has landed (GradSync)
+                rng = (lambda s, lo, hi, first: self.optimizer.step_range(self.texture_dc, lo, hi, first, zero_grad=True,
+                                                                          grad_scale=s)) if self.fused_adam else None
                 self._pending_tex = sync.all_reduce_and_step(
                     lambda s: self.optimizer.step(only=tex, zero_grad=True, grad_scale=s),
-                    lambda s: self.optimizer.step(skip=tex, grad_scale=s), defer_tail=True)
+                    lambda s: self.optimizer.step(skip=tex, grad_scale=s), defer_tail=True, step_tail_range=rng)
+                self._pending_collective = True
             else:
                 self.optimizer.step(skip=tex)
                 self._pending_tex = lambda: self.optimizer.step(only=tex, zero_grad=True)
+                self._pending_collective = False
             self.step += 1
             return
         if sync is not None and self.fused_adam and not self.async_texture:

@@ -437,7 +437,9 @@ class _TextureGaussians(torch.autograd.Function):
         if needs_bwd:
             nb = int(_lib.load().gstex_raster_aux_bytes(n_isect, tile_ranges.shape[0], C))
             aux = torch.empty((nb,), device=dev, dtype=torch.uint8)
-        if texture_ready is not None:  # the texels (and the gradient buffer) are updated on another stream
+        if callable(texture_ready):  # the caller's texel update, enqueued right before the raster forward
+            texture_ready()
+        elif texture_ready is not None:  # the texels (and the gradient buffer) are updated on another stream
             torch.cuda.current_stream(dev).wait_event(texture_ready)
         _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
@@ -549,7 +551,8 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
 
     texture_ready (not in the reference API): a torch.cuda.Event the current stream waits on right before the raster
     forward -- the texel update of the previous optimizer step running on a side stream (GStexTrainer
-    async_texture), so preprocessing and binning overlap it.
+    async_texture), so preprocessing and binning overlap it -- or a callable run at that point (GStexTrainer
+    defer_texture under GradSync: the deferred texel update, which first waits for its collective).
 
     before_pair_wait (not in the reference API): a callable run after the pair-count read-back has been queued and
     before the host waits for it -- work it enqueues keeps the device busy through that wait (GStexTrainer

@@ -59,6 +59,42 @@ class FusedAdam(torch.optim.Optimizer):
                                             st["exp_avg_sq"].data_ptr(), p.numel(), step_size, bc2_sqrt)
                 key = (b1, b2, group["eps"], p.device)
                 batches.setdefault(key, []).append((desc, p))
+        self._launch(batches, zero_grad, grid, grad_scale)
+        return loss
+
+    @torch.no_grad()
+    def step_range(self, p, lo: int, hi: int, first: bool, zero_grad=False, grad_scale=1.0):
+        """The Adam update of elements [lo, hi) of parameter `p` only: the chunks of one step, launched one by one
+        (e.g. each as soon as its slice of an all-reduce has landed, gstex_amd.dist.GradSync), together equal one
+        step(only={id(p)}) bit for bit (the update is elementwise).  `first`: the chunk that advances the parameter's
+        step count (exactly one per step, before the others)."""
+        g = p.grad
+        if g is None:
+            return
+        if not (0 <= lo < hi <= p.numel()):
+            raise ValueError(f"FusedAdam.step_range: [{lo}, {hi}) outside the parameter's {p.numel()} elements")
+        if p.dtype != torch.float32 or g.dtype != torch.float32 or not p.is_cuda:
+            raise TypeError("FusedAdam: fp32 CUDA parameters and gradients only")
+        if not (p.is_contiguous() and g.is_contiguous()):
+            raise ValueError("FusedAdam: parameters and gradients must be contiguous")
+        group = next(gr for gr in self.param_groups if any(q is p for q in gr["params"]))
+        b1, b2 = group["betas"]
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        if first:
+            st["step"] += 1
+        t = st["step"]
+        step_size = group["lr"] / (1.0 - b1 ** t)
+        bc2_sqrt = (1.0 - b2 ** t) ** 0.5
+        o = 4 * lo
+        desc = _lib.GstexAdamTensor(p.data_ptr() + o, g.data_ptr() + o, st["exp_avg"].data_ptr() + o,
+                                    st["exp_avg_sq"].data_ptr() + o, hi - lo, step_size, bc2_sqrt)
+        self._launch({(b1, b2, group["eps"], p.device): [(desc, p)]}, zero_grad, 0, grad_scale)
+
+    def _launch(self, batches, zero_grad, grid, grad_scale):
         for (b1, b2, eps, dev), items in batches.items():
             st = _lib.stream_of(dev)
             for i in range(0, len(items), _lib.ADAM_MAX_TENSORS):
@@ -72,4 +108,3 @@ class FusedAdam(torch.optim.Optimizer):
                     _lib.call("gstex_adam_step_ex", len(chunk), arr, float(b1), float(b2), float(eps), flags, st)
                 else:
                     _lib.call("gstex_adam_step", len(chunk), arr, float(b1), float(b2), float(eps), st)
-        return loss

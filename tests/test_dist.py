@@ -52,7 +52,9 @@ def _worker(rank, world, port, q, overlap=True):
         sync.zero()
         ((rank + 1) * p.texture.sum()).backward()
         sync.all_reduce()
-        ok2 = torch.allclose(p.texture.grad, torch.full((9, 3), 1.5)) and sync.flat.numel() == 30 + 12 + 27
+        # (slices start on GradSync.ALIGN-element boundaries: 30, 12 and 27 elements -> offsets 0, 64, 128)
+        ok2 = torch.allclose(p.texture.grad, torch.full((9, 3), 1.5)) and sync._offs == [0, 64, 128]
+        ok2 = ok2 and sync.flat.numel() == 128 + 64
         q.put((rank, bool(ok1), bool(ok2)))
     finally:
         dist.destroy_process_group()
@@ -213,6 +215,30 @@ def _trainer_worker(rank, world, port, q):
                                   and all(abs(c[1] - 1.0 / world) < 1e-15 for c in calls)
                                   and bool(torch.allclose(calls[0][2], torch.full_like(tr2.means, sum_w)))
                                   and bool(torch.allclose(calls[1][2], sum_w * tr2.texture_dc.detach())))
+        # head first with a chunked texel update (GStexTrainer passes step_tail_range): the tail's collective goes out
+        # in tail_bounds pieces, each stepped once it has landed; together they cover the tail once, in order, the
+        # first one flagged
+        tr3 = _SinkTrainer(n_tex=1500)
+        tr3.defer_texture = True
+        sync3 = GradSync(tr3, world)
+        sync3.zero()
+        tr3.backward(rank)
+        calls = []
+        pending = sync3.all_reduce_and_step(
+            lambda sc: calls.append(("tail", sc)),
+            lambda sc: calls.append(("head", sc, tr3.means.grad.clone())), defer_tail=True,
+            step_tail_range=lambda sc, lo, hi, first: calls.append(
+                ("range", sc, lo, hi, first, tr3.texture_dc.grad.view(-1)[lo:hi].clone())))
+        pending()
+        rng = [c for c in calls if c[0] == "range"]
+        whole = (sum_w * tr3.texture_dc.detach()).view(-1)
+        res["chunked_tail"] = (len(rng) > 1 and [c[0] for c in calls] == ["head"] + ["range"] * len(rng)
+                               and rng[0][2] == 0 and rng[-1][3] == whole.numel()
+                               and all(a[3] == b[2] for a, b in zip(rng, rng[1:]))
+                               and [c[4] for c in rng] == [True] + [False] * (len(rng) - 1)
+                               and all(abs(c[1] - 1.0 / world) < 1e-15 for c in rng)
+                               and all(bool(torch.allclose(c[5], whole[c[2]:c[3]])) for c in rng)
+                               and all(sync3._offs[i] % GradSync.ALIGN == 0 for i in range(len(sync3._offs))))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -240,5 +266,6 @@ def test_trainer_layout_sink_and_recharts_world2():
         assert r["overlap_order"] and r["overlap_scale"] and r["overlap_sums"], r
         assert r["defer_head_first"] and r["defer_tail_later"], r
         assert r["head_first_no_early_tail"] and r["head_first_sums"], r
+        assert r["chunked_tail"], r
         for step in range(2):
             assert r[f"set_to_none_{step}"], f"rank {rank}: zero_grad(set_to_none) after zero() mis-reduced (step {step})"
