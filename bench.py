@@ -157,9 +157,10 @@ def _events_ms(pairs):
     return [a.elapsed_time(b) for a, b in pairs]
 
 
-def raster_only(n_splats, n_texels, H, W, reps, dev, backward=True, seed=42, opacity=0.1):
-    """Raster-only fwd(+bwd) median over `reps` on one sphere view (SURVEY §8d cfg1/cfg2 rows): preprocessing
-    + binning + texture_gaussians forward [+ backward with img/alpha/tex upstream gradients ~ N(0, 1e-3)].
+def raster_only(n_splats, n_texels, H, W, reps, dev, backward=True, seed=42, opacity=0.1, geo=False):
+    """Raster-only fwd(+bwd) median over `reps` on one sphere view (SURVEY §8d cfg1/cfg2/cfg5 rows): preprocessing
+    + binning + texture_gaussians forward [+ backward with img/alpha/tex upstream gradients ~ N(0, 1e-3); geo: every
+    output (depth, distortion and normal too, cfg5's depth + normal training) produced and differentiated].
     Returns per-kernel medians, the whole call's median and the roofline fraction of fwd+bwd."""
     from gstex_amd import ops
     from gstex_amd.scene import make_scene, sphere_view
@@ -176,7 +177,8 @@ def raster_only(n_splats, n_texels, H, W, reps, dev, backward=True, seed=42, opa
         for t in leaves:
             t.requires_grad_(True)
     g = torch.Generator(device="cpu").manual_seed(0)
-    ups = [torch.randn(s, generator=g).to(dev) * 1e-3 for s in [(H, W, 3), (H, W), (H, W, 3)]]
+    shapes = [(H, W, 3), (H, W), (H, W), (H, W), (H, W, 3), (H, W, 3)] if geo else [(H, W, 3), (H, W), (H, W, 3)]
+    ups = [torch.randn(s, generator=g).to(dev) * 1e-3 for s in shapes]
     intr = (v.fx, v.fy, v.cx, v.cy)
 
     def run():
@@ -185,9 +187,9 @@ def raster_only(n_splats, n_texels, H, W, reps, dev, backward=True, seed=42, opa
         nth = ops.get_num_tiles_hit_2d(c, e, H, W, 16)
         outs = ops.texture_gaussians((sc.n, 1, 3), dims, c, e, depths, nth, rgbs, opac, means, scales, 1, quats,
                                      uv0, umap, vmap, tex, v.viewmat, v.c2w, v.fx, v.fy, v.cx, v.cy, H, W, 16,
-                                     (1 << 9) | (1 << 10), background=None, geometry_outputs=not backward)
+                                     (1 << 9) | (1 << 10), background=None, geometry_outputs=geo or not backward)
         if backward:
-            torch.autograd.backward([outs[0], outs[3], outs[4]], ups)
+            torch.autograd.backward(list(outs) if geo else [outs[0], outs[3], outs[4]], ups)
             for t in leaves:
                 t.grad = None
         return nth
@@ -396,6 +398,9 @@ def main():
             sub["rechart_ms"] = round(statistics.median(rc), 3)
             sub["cfg2_fwd_bwd"] = raster_only(50_000, 1e6, 800, 800, 20, dev)
             sub["cfg1_fwd"] = raster_only(1_000, 0, 256, 256, 50, dev, backward=False)
+            # cfg5's per-GPU raster: one 1600x1200 view with depth + normal outputs and gradients (the DTU scan24
+            # COLMAP init is absent: a synthetic scene of the bench's size stands in)
+            sub["cfg5_fwd_bwd_geo"] = raster_only(200_000, 1e7, 1200, 1600, 10, dev, geo=True)
         except Exception as ex:  # sub-records must never kill the headline line
             sub["error"] = repr(ex)
 
