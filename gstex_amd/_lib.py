@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 REC_FLOATS = 32
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
@@ -88,6 +88,11 @@ SIGNATURES = {
         c_int32,
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P],
+    ),
+    "gstex_raster_fwd_zero": (
+        c_int32,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+         c_int64, _P, _P, c_int64, _P],
     ),
     "gstex_raster_aux_bytes": (c_size_t, [c_int64, c_int32, c_int32]),
     "gstex_unit_order": (c_int32, [c_int32, _P, _P, _P, _P]),

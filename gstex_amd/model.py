@@ -155,7 +155,7 @@ class GStexTrainer:
         self.texture_grad_ready = None
         self.test_colors = None  # eval-render test colours (gstex.py:309)
         # async_texture (not in the reference; fused Adam on a HIP device): the texel parameter's Adam update (73 % of
-        # the parameters at cfg3) runs on a side stream and zeroes its gradient as it reads it; the next step's
+        # the parameters at cfg3) runs on a side stream (its gradient is zeroed by the next raster forward); the next step's
         # preprocessing and binning overlap it, and only its raster forward waits (texture_gaussians texture_ready).
         # The gradient lives in a persistent buffer the raster backward accumulates into (texture_grad_sink), so
         # no per-step zero fill remains.  Anything else reading texture_dc after optimizer_step() must call
@@ -165,7 +165,7 @@ class GStexTrainer:
         # parameter's Adam update of step k runs inside step k+1's render, queued right after the binning's pair count
         # is read back -- the device runs it while the host waits for that count and sizes the pair buffers (an idle
         # gap of the device otherwise), and before the raster forward, the first reader of the texels.  Same updates
-        # in the same order on the same stream; the gradient is a persistent buffer the update zeroes as it reads it.
+        # in the same order on the same stream; the gradient is a persistent buffer the raster forward zeroes.
         # Readers of texture_dc outside the step go through wait_texture() / texels(), which run a pending update.
         self.defer_texture = bool(defer_texture) and not self.async_texture and fused_adam and self.device.type == "cuda"
         self._pending_tex = None
@@ -188,9 +188,11 @@ class GStexTrainer:
 
     @property
     def texture_grad_zeroed_by_update(self) -> bool:
-        """The texel Adam update zeroes the texel gradient as it reads it (async_texture / defer_texture): a
-        gradient-buffer owner (gstex_amd.dist.GradSync) must not fill that slice itself."""
-        return self.async_texture or self.defer_texture
+        """The texel gradient buffer handed to the raster (texture_grad_sink) is zeroed by the raster forward
+        (gstex_raster_fwd_zero) before the backward accumulates into it: a gradient-buffer owner
+        (gstex_amd.dist.GradSync) must not fill that slice itself (with a side-stream or deferred texel update,
+        async_texture / defer_texture, that fill would also race or pre-empt the update still reading it)."""
+        return True
 
     def _run_pending_texture(self):
         fn, self._pending_tex = self._pending_tex, None
@@ -369,15 +371,15 @@ class GStexTrainer:
             tex = {id(self.texture_dc)}
             if sync is not None:
                 # the texel update in pieces, each as soon as its piece of the collective has landed (GradSync)
-                rng = (lambda s, lo, hi, first: self.optimizer.step_range(self.texture_dc, lo, hi, first, zero_grad=True,
+                rng = (lambda s, lo, hi, first: self.optimizer.step_range(self.texture_dc, lo, hi, first,
                                                                           grad_scale=s)) if self.fused_adam else None
                 self._pending_tex = sync.all_reduce_and_step(
-                    lambda s: self.optimizer.step(only=tex, zero_grad=True, grad_scale=s),
+                    lambda s: self.optimizer.step(only=tex, grad_scale=s),
                     lambda s: self.optimizer.step(skip=tex, grad_scale=s), defer_tail=True, step_tail_range=rng)
                 self._pending_collective = True
             else:
                 self.optimizer.step(skip=tex)
-                self._pending_tex = lambda: self.optimizer.step(only=tex, zero_grad=True)
+                self._pending_tex = lambda: self.optimizer.step(only=tex)
                 self._pending_collective = False
             self.step += 1
             return
@@ -405,7 +407,7 @@ class GStexTrainer:
         grads_ready.record(main)
         self._tex_stream.wait_event(grads_ready)
         with torch.cuda.stream(self._tex_stream):
-            self.optimizer.step(only=tex, zero_grad=True, grid=self._tex_grid)
+            self.optimizer.step(only=tex, grid=self._tex_grid)
             ev = torch.cuda.Event()
             ev.record(self._tex_stream)
         self._tex_ready = ev
@@ -415,7 +417,7 @@ class GStexTrainer:
         """Optimizers.zero_grad_all (engine/optimizers.py): torch's default set_to_none=True, so backward
         writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
         when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead).  With
-        async_texture the texel gradient buffer is kept (the side-stream Adam zeroes it)."""
+        async_texture / defer_texture the texel gradient buffer is kept (the raster forward zeroes it)."""
         if self.async_texture or self.defer_texture:
             keep = self.texture_dc.grad
             self.optimizer.zero_grad(set_to_none=set_to_none)

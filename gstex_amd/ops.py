@@ -44,7 +44,8 @@ def kernel_times() -> dict:
 
 
 def _launch(name: str, *args) -> None:
-    if _TIMING is None or name not in _TIMED:
+    key = name[:-len("_zero")] if name.endswith("_zero") else name  # gstex_raster_fwd_zero times as the forward
+    if _TIMING is None or key not in _TIMED:
         call(name, *args)
         return
     a = torch.cuda.Event(enable_timing=True)
@@ -52,7 +53,7 @@ def _launch(name: str, *args) -> None:
     a.record()
     call(name, *args)
     b.record()
-    _TIMING.setdefault(name, []).append((a, b))
+    _TIMING.setdefault(key, []).append((a, b))
 
 
 # ----------------------------------------------------------------------------------------
@@ -392,13 +393,14 @@ class _TextureGaussians(torch.autograd.Function):
         ctx.sink = texture_grad_sink is not None
         ctx.on_texture_grad = on_texture_grad
         if needs_bwd and ctx.needs_input_grad[15]:
-            if ctx.sink:  # the caller's (zeroed) gradient buffer: accumulated into, nothing returned to autograd
+            if ctx.sink:  # the caller's gradient buffer: zeroed by the raster forward, accumulated into by the
+                # backward, nothing returned to autograd
                 _check(texture_grad_sink.shape == texture.shape and texture_grad_sink.is_contiguous() and
                        texture_grad_sink.dtype == torch.float32 and texture_grad_sink.device == texture.device,
                        "texture_grad_sink must be a contiguous fp32 tensor shaped like texture on its device")
                 ctx.v_texture = texture_grad_sink
             else:
-                ctx.v_texture = torch.zeros_like(texture)
+                ctx.v_texture = torch.empty_like(texture)  # zeroed by the raster forward (gstex_raster_fwd_zero)
         if before_pair_wait is not None:
             before_pair_wait()  # caller's work for the device while the host waits for the pair count
         if binning is None:
@@ -441,11 +443,13 @@ class _TextureGaussians(torch.autograd.Function):
             texture_ready()
         elif texture_ready is not None:  # the texels (and the gradient buffer) are updated on another stream
             torch.cuda.current_stream(dev).wait_event(texture_ready)
-        _launch("gstex_raster_fwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
+        # the texel-gradient buffer the backward accumulates into is zeroed by the forward's grid (no fill pass)
+        zbuf = ctx.v_texture
+        _launch("gstex_raster_fwd_zero", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
              ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), geo_ptrs[0], geo_ptrs[1], ptr(alpha),
              ptr(tex), geo_ptrs[2],
-             ptr(state), n_isect, ptr(aux), st)
+             ptr(state), n_isect, ptr(aux), ptr(zbuf), 0 if zbuf is None else zbuf.numel(), st)
         ctx.aux = aux
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 10
+#define GSTEX_ABI_VERSION 11
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -157,6 +157,15 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                      float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
                      void* stream);
+/* The same, also zeroing zero_buf[0, zero_floats) (ABI 11): the texel-gradient buffer the backward accumulates
+ * into, cleared by the forward's grid with streaming stores the raster work hides (no separate fill). */
+int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
+                          const float* background, const float* records, const int32_t* tile_ranges,
+                          const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
+                          int64_t n_texels, float tex_scale, float tex_bias,
+                          float* out_img, float* out_depth, float* out_reg, float* out_alpha,
+                          float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
+                          float* zero_buf, int64_t zero_floats, void* stream);
 size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels);
 /* Launch order of n_units backward units: unit_key = cost (bits 0-23, clamped to 1023) | XCD group (bits 24-26).
  * Units of cost 0 get no position; the others are sorted by descending cost within their group and the groups

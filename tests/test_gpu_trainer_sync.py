@@ -84,7 +84,7 @@ def test_synced_step_matches_unsynced_across_rechart():
 
 
 def test_async_texture_update_matches_sync_step():
-    """async_texture: the texel Adam update on a side stream (zeroing its gradient buffer), overlapped with the
+    """async_texture: the texel Adam update on a side stream (its gradient buffer zeroed by the next raster forward), overlapped with the
     next step's preprocessing; alone and under GradSync (world 1), across an in-place rechart and an eval render,
     it must train like the plain step."""
     from gstex_amd.dist import GradSync
@@ -122,7 +122,12 @@ def test_async_texture_update_matches_sync_step():
         for tr in (alone, synced):
             tr.wait_texture()
         torch.cuda.synchronize()
-        # the persistent texel-gradient buffers are left zeroed by the side-stream update
+        # the persistent texel-gradient buffers hold the last gradient until the next differentiable raster forward
+        # zeroes them (gstex_raster_fwd_zero), before its backward accumulates into them
+        assert float(alone.texture_dc.grad.abs().max()) > 0.0
+        for tr in (alone, synced):
+            tr.render(views[0])
+        torch.cuda.synchronize()
         assert float(alone.texture_dc.grad.abs().max()) == 0.0
         assert float(sync.flat[sync._tail_off:].abs().max()) == 0.0
         for other in (alone, synced):
@@ -172,7 +177,12 @@ def test_deferred_texture_update_matches_plain_step():
         for tr in (alone, synced):
             tr.wait_texture()
         torch.cuda.synchronize()
-        # the persistent texel-gradient buffers are left zeroed by the deferred update
+        # the persistent texel-gradient buffers hold the last gradient until the next differentiable raster forward
+        # zeroes them (gstex_raster_fwd_zero)
+        assert float(alone.texture_dc.grad.abs().max()) > 0.0
+        for tr in (alone, synced):
+            tr.render(views[0])
+        torch.cuda.synchronize()
         assert float(alone.texture_dc.grad.abs().max()) == 0.0
         assert float(sync.flat[sync._tail_off:].abs().max()) == 0.0
         for other in (alone, synced):

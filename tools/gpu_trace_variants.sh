@@ -4,7 +4,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/tv; mkdir -p $OUT
 for v in "$@"; do
-  GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$v -o run -- python3 tools/raster_loop.py --photometric --iters 10 > $OUT/$v.log 2>&1 || { echo "FAIL $v"; exit 1; }
+  GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$v -o run -- python3 tools/raster_loop.py ${RL_ARGS:---photometric} --iters 10 > $OUT/$v.log 2>&1 || { echo "FAIL $v"; exit 1; }
   echo "== $v"
   python3 - "$OUT/$v/run_kernel_stats.csv" "${FILTER:-.}" <<'PY'
 import csv, re, sys
