@@ -120,6 +120,9 @@ struct BwdShape {
 #endif
 constexpr int kTexStage = GSTEX_TEX_STAGE;
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
+#ifndef GSTEX_ZERO_END
+#define GSTEX_ZERO_END 0  // forward: the texel-gradient buffer's zero stores after the tile's visit loop (0: before it)
+#endif
 #ifndef GSTEX_FWD_DEFER
 #define GSTEX_FWD_DEFER 1
 #endif
@@ -128,7 +131,8 @@ constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
                         // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
-                        // 256 = no partial-row / flag stores (backward ablations skip work: timing experiments only)
+                        // 256 = no partial-row / flag stores, 512 = forward without the gradient-buffer zeroing
+                        // (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 constexpr int kRowStride = GSTEX_PARTIAL_FLOATS;  // 32 floats between partial rows
@@ -604,7 +608,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     int n_tiles, float* __restrict__ zero_buf, int64_t zero_n) {
     const Camera cam = load_camera(cam_args);
     unsigned long long* __restrict__ visit_masks = aux.masks;
-    if (zero_buf) {
+    auto zero_grad_buf = [&]() {
         // the backward's texel-gradient buffer zeroed by the whole grid (gstex_raster_fwd_zero): plain streaming
         // stores the VALU-bound forward hides, instead of a fill pass (or an Adam update's zero stores) elsewhere
         const int64_t nthr = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -617,7 +621,8 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
         } else {
             for (int64_t i = t0; i < zero_n; i += nthr) zero_buf[i] = 0.0f;
         }
-    }
+    };
+    if (zero_buf && !GSTEX_ZERO_END) zero_grad_buf();
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     constexpr int kThr = FwdShape<ONE>::kThr, kStep = FwdShape<ONE>::kStep, kWords = kStep / 64;
@@ -824,6 +829,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
         }
     }
     fold_pending();
+    if (zero_buf && GSTEX_ZERO_END) zero_grad_buf();
     if (aux.cost) {
         const int cnt = wave_max_i(seg_visits);
         if (lane == 0 && cnt) {
@@ -1962,7 +1968,7 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     // (0 = no unit at that position) and the unit-order histogram the forward builds (contiguous in the layout)
     if (aux && hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
         return launch_status("gstex_raster_fwd (aux)");
-    float* zbuf = zero_floats > 0 ? zero_buf : nullptr;
+    float* zbuf = zero_floats > 0 && !(GSTEX_ABLATE & 512) ? zero_buf : nullptr;
 #define GSTEX_FWD(CC, GG)                                                                                      \
     do {                                                                                                       \
         if (GSTEX_FWD_WAVE)                                                                                    \
