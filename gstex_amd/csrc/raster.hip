@@ -300,6 +300,7 @@ struct AuxPtrs {
     int F;
 };
 struct AuxLayout { size_t masks, cost, order, order_ws, slot_tile, ckpt, bytes; int64_t n_slots, n_units; int F; };
+struct ZeroBufs { float* p[2]; int64_t n[2]; };  // buffers the forward's grid zeroes (gstex_raster_fwd_zero)
 __host__ inline AuxLayout aux_layout(int64_t n_isect, int n_tiles, int C) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     AuxLayout a;
@@ -605,24 +606,31 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     float tex_bias, float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
     float* __restrict__ out_tex, float* __restrict__ out_normal, float4* __restrict__ state, AuxPtrs aux,
-    int n_tiles, float* __restrict__ zero_buf, int64_t zero_n) {
+    int n_tiles, const ZeroBufs zb) {
     const Camera cam = load_camera(cam_args);
     unsigned long long* __restrict__ visit_masks = aux.masks;
     auto zero_grad_buf = [&]() {
-        // the backward's texel-gradient buffer zeroed by the whole grid (gstex_raster_fwd_zero): plain streaming
-        // stores the VALU-bound forward hides, instead of a fill pass (or an Adam update's zero stores) elsewhere
+        // the backward's accumulation buffers (texel gradient, splat-gradient sums) zeroed by the whole grid
+        // (gstex_raster_fwd_zero): plain streaming stores the VALU-bound forward hides, instead of fill passes (or an
+        // Adam update's zero stores) elsewhere
         const int64_t nthr = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if ((reinterpret_cast<uintptr_t>(zero_buf) & 15) == 0) {
-            typedef float z4v __attribute__((ext_vector_type(4)));
-            z4v* z4 = reinterpret_cast<z4v*>(zero_buf);
-            const z4v zero = {0.f, 0.f, 0.f, 0.f};
-            for (int64_t i = t0; i < zero_n / 4; i += nthr) __builtin_nontemporal_store(zero, z4 + i);
-            if (t0 < zero_n % 4) zero_buf[zero_n / 4 * 4 + t0] = 0.0f;
-        } else {
-            for (int64_t i = t0; i < zero_n; i += nthr) zero_buf[i] = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            float* zp = zb.p[b];
+            const int64_t zn = zb.n[b];
+            if (!zp) continue;
+            if ((reinterpret_cast<uintptr_t>(zp) & 15) == 0) {
+                typedef float z4v __attribute__((ext_vector_type(4)));
+                z4v* z4 = reinterpret_cast<z4v*>(zp);
+                const z4v zero = {0.f, 0.f, 0.f, 0.f};
+                for (int64_t i = t0; i < zn / 4; i += nthr) __builtin_nontemporal_store(zero, z4 + i);
+                if (t0 < zn % 4) zp[zn / 4 * 4 + t0] = 0.0f;
+            } else {
+                for (int64_t i = t0; i < zn; i += nthr) zp[i] = 0.0f;
+            }
         }
     };
-    if (zero_buf && !GSTEX_ZERO_END) zero_grad_buf();
+    if (!GSTEX_ZERO_END) zero_grad_buf();
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     constexpr int kThr = FwdShape<ONE>::kThr, kStep = FwdShape<ONE>::kStep, kWords = kStep / 64;
@@ -829,7 +837,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
         }
     }
     fold_pending();
-    if (zero_buf && GSTEX_ZERO_END) zero_grad_buf();
+    if (GSTEX_ZERO_END) zero_grad_buf();
     if (aux.cost) {
         const int cnt = wave_max_i(seg_visits);
         if (lane == 0 && cnt) {
@@ -1934,7 +1942,7 @@ extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32
                                 float* out_normal, float* state, int64_t n_isect, void* aux, void* stream) {
     return gstex_raster_fwd_zero(cam, channels, settings, background, records, tile_ranges, tile_order, sorted_ids,
                                  texture, n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg, out_alpha,
-                                 out_tex, out_normal, state, n_isect, aux, nullptr, 0, stream);
+                                 out_tex, out_normal, state, n_isect, aux, nullptr, 0, nullptr, 0, stream);
 }
 
 extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
@@ -1943,8 +1951,9 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
                                      int64_t n_texels, float tex_scale, float tex_bias, float* out_img,
                                      float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
                                      float* out_normal, float* state, int64_t n_isect, void* aux, float* zero_buf,
-                                     int64_t zero_floats, void* stream) {
-    GSTEX_REQUIRE(zero_floats >= 0 && (zero_floats == 0 || zero_buf), "gstex_raster_fwd: invalid zero_buf / zero_floats");
+                                     int64_t zero_floats, float* zero_buf2, int64_t zero_floats2, void* stream) {
+    GSTEX_REQUIRE(zero_floats >= 0 && (zero_floats == 0 || zero_buf) && zero_floats2 >= 0 &&
+                  (zero_floats2 == 0 || zero_buf2), "gstex_raster_fwd: invalid zero_buf / zero_floats");
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_fwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_fwd: block_width must be %d (got %d)", kTile, cam->block);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_fwd: channels must be in [1, 8] (got %d)",
@@ -1968,19 +1977,23 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     // (0 = no unit at that position) and the unit-order histogram the forward builds (contiguous in the layout)
     if (aux && hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
         return launch_status("gstex_raster_fwd (aux)");
-    float* zbuf = zero_floats > 0 && !(GSTEX_ABLATE & 512) ? zero_buf : nullptr;
+    ZeroBufs zbuf;
+    zbuf.p[0] = zero_floats > 0 && !(GSTEX_ABLATE & 512) ? zero_buf : nullptr;
+    zbuf.n[0] = zero_floats;
+    zbuf.p[1] = zero_floats2 > 0 && !(GSTEX_ABLATE & 512) ? zero_buf2 : nullptr;
+    zbuf.n[1] = zero_floats2;
 #define GSTEX_FWD(CC, GG)                                                                                      \
     do {                                                                                                       \
         if (GSTEX_FWD_WAVE)                                                                                    \
             raster_fwd_kernel<CC, GG, true><<<(unsigned)(((nblk + 7) / 8) * 32), 64, 0, st>>>(                \
                 dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, \
                 tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth,       \
-                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf, zero_floats);         \
+                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf);                      \
         else                                                                                                   \
             raster_fwd_kernel<CC, GG, false><<<nblk, kThreads, 0, st>>>(                                      \
                 dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, \
                 tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth,       \
-                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf, zero_floats);         \
+                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf);                      \
     } while (0)
     if (channels == 3 && geo) GSTEX_FWD(3, true);
     else if (channels == 3) GSTEX_FWD(3, false);

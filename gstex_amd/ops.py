@@ -443,13 +443,16 @@ class _TextureGaussians(torch.autograd.Function):
             texture_ready()
         elif texture_ready is not None:  # the texels (and the gradient buffer) are updated on another stream
             torch.cuda.current_stream(dev).wait_event(texture_ready)
-        # the texel-gradient buffer the backward accumulates into is zeroed by the forward's grid (no fill pass)
+        # the buffers the backward accumulates into are zeroed by the forward's grid (no fill passes): the texel
+        # gradient and the fast mode's per-splat partial sums (PARTIAL_FLOATS per splat: room for either row width)
         zbuf = ctx.v_texture
+        ctx.partials = torch.empty((n * PARTIAL_FLOATS,), device=dev, dtype=torch.float32) if needs_bwd else None
         _launch("gstex_raster_fwd_zero", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
              ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), geo_ptrs[0], geo_ptrs[1], ptr(alpha),
              ptr(tex), geo_ptrs[2],
-             ptr(state), n_isect, ptr(aux), ptr(zbuf), 0 if zbuf is None else zbuf.numel(), st)
+             ptr(state), n_isect, ptr(aux), ptr(zbuf), 0 if zbuf is None else zbuf.numel(), ptr(ctx.partials),
+             0 if ctx.partials is None else ctx.partials.numel(), st)
         ctx.aux = aux
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
@@ -493,6 +496,10 @@ class _TextureGaussians(torch.autograd.Function):
         if torch.are_deterministic_algorithms_enabled():
             partials = torch.empty((n_isect, 4, row_floats), device=dev, dtype=torch.float32)
             row_flags = torch.empty((n_isect,), device=dev, dtype=torch.int32)
+        elif ctx.partials is not None:  # zeroed by the forward (a second backward of the same graph zeroes its own)
+            partials = ctx.partials[:n * row_floats].view(n, row_floats)
+            ctx.partials = None
+            row_flags = None
         else:
             partials = torch.zeros((n, row_floats), device=dev, dtype=torch.float32)
             row_flags = None

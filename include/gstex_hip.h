@@ -157,15 +157,17 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                      float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
                      void* stream);
-/* The same, also zeroing zero_buf[0, zero_floats) (ABI 11): the texel-gradient buffer the backward accumulates
- * into, cleared by the forward's grid with streaming stores the raster work hides (no separate fill). */
+/* The same, also zeroing zero_buf[0, zero_floats) and zero_buf2[0, zero_floats2) (ABI 11; NULL / 0 = none): the
+ * buffers the backward accumulates into (the texel gradient, the fast mode's per-splat partials), cleared by the
+ * forward's grid with streaming stores the raster work hides (no separate fills). */
 int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
                           const float* background, const float* records, const int32_t* tile_ranges,
                           const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                           int64_t n_texels, float tex_scale, float tex_bias,
                           float* out_img, float* out_depth, float* out_reg, float* out_alpha,
                           float* out_tex, float* out_normal, float* state, int64_t n_isect, void* aux,
-                          float* zero_buf, int64_t zero_floats, void* stream);
+                          float* zero_buf, int64_t zero_floats, float* zero_buf2, int64_t zero_floats2,
+                          void* stream);
 size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels);
 /* Launch order of n_units backward units: unit_key = cost (bits 0-23, clamped to 1023) | XCD group (bits 24-26).
  * Units of cost 0 get no position; the others are sorted by descending cost within their group and the groups
