@@ -84,3 +84,57 @@ class _PhotometricLoss(torch.autograd.Function):
 def photometric_loss(img, tex, alpha, background, gt, ssim_lambda: float = 0.2):
     """Returns (loss, rgb): loss is the differentiable 0-dim training loss, rgb the composited image."""
     return _PhotometricLoss.apply(img, tex, alpha, background, gt, ssim_lambda)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# geometry regularisers of get_loss_dict (gstex.py:1313-1317), for a trainer with depth / normal renders
+# ---------------------------------------------------------------------------------------------------------------
+def depths_to_points(depth: torch.Tensor, viewmat: torch.Tensor, c2w: torch.Tensor, fx: float, fy: float, cx: float,
+                     cy: float) -> torch.Tensor:
+    """World-space points (H, W, 3) of a rendered depth map, as the reference's depths_to_points
+    (gstex.py:122-149): pixel (i, j) looks along the unit world ray of camera direction ((j - cx + 0.5) / fx,
+    (i - cy + 0.5) / fy, 1); the depth is view-space z ("don't use view depth", :145-146), so the distance along
+    the ray is depth / (the ray's view-space z component)."""
+    H, W = depth.shape[0], depth.shape[1]
+    dev, f = depth.device, torch.float32
+    rows = torch.arange(H, device=dev, dtype=f)[:, None].expand(H, W)
+    cols = torch.arange(W, device=dev, dtype=f)[None, :].expand(H, W)
+    cam_dir = torch.stack([(cols - cx + 0.5) / fx, (rows - cy + 0.5) / fy, torch.ones_like(rows)], dim=-1)
+    world_dir = cam_dir @ c2w[:3, :3].to(f).T
+    world_dir = world_dir / (world_dir.norm(dim=-1, keepdim=True) + 1e-9)
+    view_z = world_dir @ viewmat[2, :3].to(f)
+    dist = depth.reshape(H, W) / view_z
+    return c2w[:3, 3].to(f) + dist[..., None] * world_dir
+
+
+def depth_to_normal(depth: torch.Tensor, viewmat: torch.Tensor, c2w: torch.Tensor, fx: float, fy: float, cx: float,
+                    cy: float) -> torch.Tensor:
+    """Normals (H, W, 3) estimated from a depth map, as the reference's depth_to_normal (gstex.py:151-161): the unit
+    cross product of the central differences of depths_to_points down the rows and along the columns; the one-pixel
+    border is zero."""
+    p = depths_to_points(depth, viewmat, c2w, fx, fy, cx, cy)
+    d_rows = p[2:, 1:-1] - p[:-2, 1:-1]
+    d_cols = p[1:-1, 2:] - p[1:-1, :-2]
+    out = torch.zeros_like(p)
+    out[1:-1, 1:-1] = torch.nn.functional.normalize(torch.linalg.cross(d_rows, d_cols, dim=-1), dim=-1)
+    return out
+
+
+def scheduled(value, step: int) -> float:
+    """A loss weight as get_loss_dict reads it (gstex.py:1304-1311): a number, or [before, after, switch_step]."""
+    if isinstance(value, (int, float)):
+        return float(value)
+    return float(value[1] if step >= value[2] else value[0])
+
+
+def geometry_loss(alpha: torch.Tensor, normal: torch.Tensor, estimated_normal: torch.Tensor, reg: torch.Tensor,
+                  lambda_normal: float, lambda_reg: float) -> torch.Tensor:
+    """normal_loss + reg_loss of get_loss_dict (gstex.py:1316-1317): lambda_normal * mean(alpha - <n, n_est>) +
+    lambda_reg * mean(reg)."""
+    loss = alpha.new_zeros(())
+    if lambda_normal != 0.0:
+        loss = loss + lambda_normal * torch.mean(alpha.reshape(alpha.shape[0], alpha.shape[1])
+                                                 - torch.sum(normal * estimated_normal, dim=-1))
+    if lambda_reg != 0.0:
+        loss = loss + lambda_reg * torch.mean(reg)
+    return loss

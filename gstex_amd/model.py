@@ -26,7 +26,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .activations import activate, sh_rest
-from .loss import gaussian_window, photometric_loss
+from .loss import depth_to_normal, gaussian_window, geometry_loss, photometric_loss, scheduled
 from .optim import FusedAdam
 from .charts import SH2RGB, build_charts, get_uv_mapping, texture_dims_to_query
 from .scene import Scene, View
@@ -106,7 +106,8 @@ class GStexTrainer:
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
-                 async_texture: bool = False, defer_texture: bool = False):
+                 async_texture: bool = False, defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0,
+                 use_normal_loss: bool = False):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -149,6 +150,11 @@ class GStexTrainer:
         # depth / distortion / normal renders: only for losses or views that read them (the reference's normal
         # and distortion weights default to 0, gstex.py:198-201, so its training loss uses none of them)
         self.geometry_outputs = geometry_outputs
+        # the 2DGS regularisers of get_loss_dict (gstex.py:198-201, 207, 1218-1220, 1313-1317): weights as numbers or
+        # [before, after, switch_step] schedules; a non-zero weight renders depth / distortion / normal for the step
+        self.lambda_normal = lambda_normal
+        self.lambda_reg = lambda_reg
+        self.use_normal_loss = use_normal_loss
         # set by gstex_amd.dist.GradSync: the flat-buffer slice the raster backward accumulates the texel gradient
         # into, and the callback that starts its collective (None: autograd owns the texel gradient)
         self.texture_grad_sink = None
@@ -236,8 +242,9 @@ class GStexTrainer:
             self.optimizer = torch.optim.Adam(groups, eps=1e-15, foreach=True)
 
     # ------------------------------------------------------------------ forward
-    def render(self, view: View, sh_degree_now: int | None = None, composite: bool = True):
-        """get_outputs (gstex.py:992-1236), training branch."""
+    def render(self, view: View, sh_degree_now: int | None = None, composite: bool = True, geometry: bool | None = None):
+        """get_outputs (gstex.py:992-1236), training branch.  geometry: render depth / distortion / normal (default:
+        the trainer's geometry_outputs)."""
         means = self.means
         deg = self.sh_degree if sh_degree_now is None else sh_degree_now
         if self.fused_activations:  # one HIP launch each way (gstex_amd.activations)
@@ -278,7 +285,8 @@ class GStexTrainer:
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
             ops.BLOCK_WIDTH, self.settings, background=self._bg_zero,
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
-            geometry_outputs=self.geometry_outputs, texture_grad_sink=self.texture_grad_sink,
+            geometry_outputs=self.geometry_outputs if geometry is None else geometry,
+            texture_grad_sink=self.texture_grad_sink,
             on_texture_grad=self.texture_grad_ready,
             texture_ready=self._run_pending_texture if late else self._tex_ready,
             before_pair_wait=self._run_pending_texture if pend and not late else None)
@@ -352,12 +360,20 @@ class GStexTrainer:
         return min(self.step // self.sh_degree_interval, self.sh_degree)
 
     def forward_backward(self, view: View, gt: torch.Tensor) -> StepOutput:
-        out = self.render(view, sh_degree_now=self.sh_degree_now(), composite=not self.fused_loss)
+        lam_n, lam_r = scheduled(self.lambda_normal, self.step), scheduled(self.lambda_reg, self.step)
+        geo = lam_n != 0.0 or lam_r != 0.0
+        out = self.render(view, sh_degree_now=self.sh_degree_now(), composite=not self.fused_loss,
+                          geometry=True if geo else None)
         if self.fused_loss:  # composite + clamp + L1/SSIM in one HIP launch pair (gstex_amd.loss)
             loss, rgb = photometric_loss(out["img"], out["tex"], out["alpha"], self.background, gt.contiguous())
         else:
             rgb = out["rgb"]
             loss = self.loss(rgb, gt)
+        if geo:
+            # gstex.py:1218-1222: the depth-derived normal (detached) when use_normal_loss, else the rendered normal
+            est = (depth_to_normal(out["depth"], view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy).detach()
+                   if self.use_normal_loss else out["normal"])
+            loss = loss + geometry_loss(out["alpha"], out["normal"], est, out["reg"], lam_n, lam_r)
         loss.backward(self._one)  # (a cached seed: no per-step fill launch for the implicit ones_like)
         return StepOutput(loss.detach(), rgb.detach())
 

@@ -145,3 +145,28 @@ def test_hip_composite_and_l1_match_reference(z):
     loss, rgb = photometric_loss(img, tex, alpha, bg, gt, ssim_lambda=0.0)
     np.testing.assert_allclose(rgb.cpu().numpy(), z["loss_rgb"], rtol=0, atol=1e-7)
     assert abs(float(loss) - float(z["loss_l1"][0])) < 1e-6 * max(1.0, float(z["loss_l1"][0]))
+
+
+def test_depth_to_normal_and_geometry_loss_restate_reference(z):
+    """gstex_amd.loss.depths_to_points / depth_to_normal / geometry_loss (GStexTrainer's lambda_normal / lambda_reg
+    terms) against the reference's own functions' outputs in the golden (gstex.py:122-161, 1313-1317)."""
+    from gstex_amd.loss import depth_to_normal, depths_to_points, geometry_loss, scheduled
+
+    vm, c2w = torch.from_numpy(z["plane_viewmat"]), torch.from_numpy(z["plane_c2w"])
+    fx, fy, cx, cy = (float(v) for v in z["plane_intr"])
+    depth, alpha = torch.from_numpy(z["plane_depth"]), torch.from_numpy(z["plane_alpha"])
+    inside = alpha > 0.999
+    pts = depths_to_points((depth / alpha.clamp(min=1e-30))[..., None], vm, c2w, fx, fy, cx, cy)
+    np.testing.assert_allclose(pts.numpy()[inside.numpy()], z["plane_ref_points"][inside.numpy()], rtol=0, atol=2e-6)
+    est = depth_to_normal(depth[..., None], vm, c2w, fx, fy, cx, cy)
+    ref = torch.from_numpy(z["plane_ref_est_normal"])
+    m = torch.from_numpy(_interior(z["plane_alpha"]))
+    assert float((est - ref)[m].abs().max()) < 1e-4
+    assert float(est[0].abs().max()) == 0.0 and float(est[:, -1].abs().max()) == 0.0  # zero border
+    lam_ssim, lam_reg, lam_normal = (float(v) for v in z["loss_lambdas"])
+    normal, est_l, reg = (torch.from_numpy(z[k]) for k in ("loss_normal", "loss_est", "loss_reg"))
+    a = torch.from_numpy(z["loss_alpha"])
+    g = geometry_loss(a, normal, est_l, reg, lam_normal, lam_reg)
+    assert abs(float(g) - float(z["loss_normal_loss"][0] + z["loss_reg_loss"][0])) < 1e-7
+    assert scheduled([0.0, 0.05, 7000], 6999) == 0.0 and scheduled([0.0, 0.05, 7000], 7000) == 0.05
+    assert scheduled(3, 0) == 3.0

@@ -19,8 +19,9 @@ Exercised, per step:
 Checked on rank 0 against a single-rank reference trainer that runs the same `world` views per step, sums their
 gradients by autograd accumulation, scales by 1/world and takes the same Adam step (the mean-gradient step); every
 rank's parameters must equal rank 0's.  Tolerance: 1e-5 of each parameter's max magnitude; for the texels (float-
-atomic gradient sums whose order varies run to run, through Adam's m / sqrt(v)) the worst texel within one step's
-learning rate and the mean difference within 1e-6 of the max magnitude.
+atomic gradient sums whose order varies run to run, through Adam's m / sqrt(v)) the worst texel within two learning
+rates per step (a near-zero gradient's noise of either sign moves it by up to lr) and the mean difference within 1e-6
+of the max magnitude.
 Test infrastructure; prints one line per check and `REHEARSAL OK world=N` at the end.
 """
 import argparse
@@ -42,6 +43,9 @@ def main():
     ap.add_argument("--n-splats", type=int, default=20_000)
     ap.add_argument("--n-texels", type=float, default=4e5)
     ap.add_argument("--size", type=int, default=160)
+    ap.add_argument("--geo", action="store_true",
+                    help="cfg5's training mode: depth / distortion / normal rendered and regularised (lambda_normal 0.05, "
+                         "lambda_reg 0.01, use_normal_loss: the geometry backward under the exchange)")
     ap.add_argument("--defer-texture", action="store_true",
                     help="GStexTrainer(defer_texture=True): the texel update of step k runs in step k+1's render")
     args = ap.parse_args()
@@ -60,9 +64,10 @@ def main():
     views = [sphere_view(i, S, S, n_views=N_POSES).to(dev) for i in range(N_POSES)]
     g = torch.Generator().manual_seed(2024)
     gts = [torch.rand((S, S, 3), generator=g).to(dev) for _ in range(N_POSES)]
-    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=args.defer_texture)
+    geo = dict(lambda_normal=0.05, lambda_reg=0.01, use_normal_loss=True) if args.geo else {}
+    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=args.defer_texture, **geo)
     sync = GradSync(tr, world)
-    ref = GStexTrainer(sc, dev, start_step=3000) if rank == 0 else None
+    ref = GStexTrainer(sc, dev, start_step=3000, **geo) if rank == 0 else None
     log = []
 
     def say(msg):
@@ -128,11 +133,13 @@ def main():
             line += f",  |rank0 - mean-gradient reference| / max|p| = {d_ref:.2e}"
             if name == "texture_dc":
                 # texel gradients are float-atomic sums (summation order varies run to run) and Adam's m / sqrt(v)
-                # (eps 1e-15) turns a near-zero gradient's noise into up to one step (lr) of update: bound the worst
-                # texel by one step and the mean by 1e-6 of max|p|
+                # (eps 1e-15) turns a near-zero gradient's noise into an update of up to lr either way per step: bound
+                # the worst texel by 2 lr per step (the two runs' noise of opposite sign) and the mean by 1e-6 of max|p|
                 d_mean = float((r0 - rp).abs().mean()) / scale
-                line += f" (mean {d_mean:.2e})"
-                good &= float((r0 - rp).abs().max()) <= ref.optimizer.param_groups[-1]["lr"] and d_mean < 1e-6
+                d_abs = float((r0 - rp).abs().max())
+                lr = ref.optimizer.param_groups[-1]["lr"]
+                line += f" (mean {d_mean:.2e}; worst {d_abs / lr:.2f} lr)"
+                good &= d_abs <= 2 * args.steps * lr and d_mean < 1e-6
             else:
                 good &= d_ref < 1e-5
         flag = torch.tensor([1.0 if good else 0.0], device=dev)
