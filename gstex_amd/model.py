@@ -176,6 +176,9 @@ class GStexTrainer:
         self.defer_texture = bool(defer_texture) and not self.async_texture and fused_adam and self.device.type == "cuda"
         self._pending_tex = None
         self._pending_collective = False  # the pending update first waits for a GradSync collective
+        # the texel-gradient sink is zeroed by the first differentiable raster forward after an optimizer step
+        # (gstex_raster_fwd_zero), so several renders of one step still accumulate their texel gradients
+        self._sink_fresh = True
         self._tex_stream = torch.cuda.Stream(device=d) if self.async_texture else None
         self._tex_ready = None
         self._tex_grad = None
@@ -286,11 +289,13 @@ class GStexTrainer:
             ops.BLOCK_WIDTH, self.settings, background=self._bg_zero,
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs if geometry is None else geometry,
-            texture_grad_sink=self.texture_grad_sink,
+            texture_grad_sink=self.texture_grad_sink, zero_texture_grad_sink=self._sink_fresh,
             on_texture_grad=self.texture_grad_ready,
             texture_ready=self._run_pending_texture if late else self._tex_ready,
             before_pair_wait=self._run_pending_texture if pend and not late else None)
         self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
+        if torch.is_grad_enabled():
+            self._sink_fresh = False  # zeroed by this forward: further renders before the step accumulate on top
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
@@ -382,6 +387,7 @@ class GStexTrainer:
         of the step: the texel group is updated as soon as its collective lands, overlapping the head's collective,
         and the 1 / world averaging rides in the fused update (GradSync.all_reduce_and_step); otherwise call
         sync.all_reduce() before this."""
+        self._sink_fresh = True  # the next step's first render zeroes the texel-gradient sink
         if self.defer_texture:
             self._run_pending_texture()  # (two steps without a render in between)
             tex = {id(self.texture_dc)}

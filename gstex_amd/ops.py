@@ -349,7 +349,7 @@ class _TextureGaussians(torch.autograd.Function):
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                 block_width, settings, background, texture_transform=None, fold_aabb=False,
                 geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None,
-                texture_ready=None, binning=None, before_pair_wait=None):
+                texture_ready=None, binning=None, before_pair_wait=None, zero_sink=False):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -444,8 +444,9 @@ class _TextureGaussians(torch.autograd.Function):
         elif texture_ready is not None:  # the texels (and the gradient buffer) are updated on another stream
             torch.cuda.current_stream(dev).wait_event(texture_ready)
         # the buffers the backward accumulates into are zeroed by the forward's grid (no fill passes): the texel
-        # gradient and the fast mode's per-splat partial sums (PARTIAL_FLOATS per splat: room for either row width)
-        zbuf = ctx.v_texture
+        # gradient (this call's own buffer, or the caller's sink when zero_sink) and the fast mode's per-splat partial
+        # sums (PARTIAL_FLOATS per splat: room for either row width)
+        zbuf = ctx.v_texture if (not ctx.sink or zero_sink) else None
         ctx.partials = torch.empty((n * PARTIAL_FLOATS,), device=dev, dtype=torch.float32) if needs_bwd else None
         _launch("gstex_raster_fwd_zero", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
              ptr(sorted_ids),
@@ -532,14 +533,14 @@ class _TextureGaussians(torch.autograd.Function):
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
                       fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None,
-                      texture_ready=None, binning=None, before_pair_wait=None):
+                      texture_ready=None, binning=None, before_pair_wait=None, zero_texture_grad_sink=False):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -558,7 +559,8 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     texture_grad_sink (not in the reference API; multi-GPU training): a zeroed contiguous fp32 tensor shaped like
     `texture` that the backward accumulates the texel gradient into (e.g. the texel slice of a flat all-reduce
     buffer); autograd then receives no gradient for `texture`, and on_texture_grad() (if given) is called once the
-    kernel producing it has been enqueued.
+    kernel producing it has been enqueued.  zero_texture_grad_sink=True: the raster forward zeroes the sink itself
+    (the first render of a step; leave it False for the renders whose gradients accumulate on top).
 
     texture_ready (not in the reference API): a torch.cuda.Event the current stream waits on right before the raster
     forward -- the texel update of the previous optimizer step running on a side stream (GStexTrainer
@@ -585,7 +587,7 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
                                    fold_aabb, geometry_outputs, torch.is_grad_enabled(), texture_grad_sink,
-                                   on_texture_grad, texture_ready, binning, before_pair_wait)
+                                   on_texture_grad, texture_ready, binning, before_pair_wait, zero_texture_grad_sink)
 
 
 class Binning(NamedTuple):

@@ -191,3 +191,29 @@ def test_deferred_texture_update_matches_plain_step():
                 _assert_trains_alike(name, a[0], b[0], "deferred texel update")
     finally:
         dist.destroy_process_group()
+
+
+def test_texture_sink_accumulates_the_renders_of_one_step():
+    """Two views per optimizer step (gradient accumulation): the persistent texel-gradient sink of a deferred-update
+    trainer is zeroed by the step's first raster forward only, so both views' texel gradients reach the update -- it
+    must train like the plain trainer, whose autograd accumulates them."""
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    sc = make_scene(3000, 60_000, seed=12)
+    views = [sphere_view(i, 96, 96).to(dev) for i in range(2)]
+    g = torch.Generator().manual_seed(5)
+    gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(2)]
+    plain = GStexTrainer(sc, dev, start_step=3000)
+    deferred = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+    for _ in range(3):
+        for tr in (plain, deferred):
+            tr.zero_grad()
+            tr.forward_backward(views[0], gts[0])
+            tr.forward_backward(views[1], gts[1])
+            tr.optimizer_step()
+    deferred.wait_texture()
+    torch.cuda.synchronize()
+    for (name, a), b in zip(plain.param_groups().items(), deferred.param_groups().values()):
+        _assert_trains_alike(name, a[0], b[0], "texel sink over two renders")
