@@ -384,9 +384,11 @@ def main():
             trainer.geometry_outputs = False
             sub["raster_fwd_full_outputs_ms"] = round(statistics.median(kf["gstex_raster_fwd"]), 4)
             sub["eval_render"] = dict(ms_per_image=round(eval_render_ms(trainer, views[0], 10), 4),
-                                      raster_calls=3, channels=6,
+                                      reference_raster_calls=3, raster_passes=2, channels=6,
                                       note="gstex.py:1165-1203, no grad; one binning for the three calls, channels "
-                                           "3..5 (zero texels) not rasterised (GStexTrainer.eval_render)")
+                                           "3..5 (zero texels) not rasterised, the settings | 1 << 15 call (zero edit "
+                                           "texture, unit normals) derived from the first one's outputs "
+                                           "(GStexTrainer.eval_render)")
             sub["eval_render"]["fps"] = round(1e3 / sub["eval_render"]["ms_per_image"], 1)
             rc = []
             for _ in range(3):

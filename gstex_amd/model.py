@@ -345,15 +345,24 @@ class GStexTrainer:
         test_op[test_op <= 0.5] = 0.0
         test_op[test_op > 0.2] = 1.0
         t_out = tg(self.test_colors, upd, upd_tf, test_op, self.settings)
-        n_out = tg(self.test_colors, upd, upd_tf, opacities, self.settings | (1 << 15))
+        if edit_texture is not None:
+            n_edit, n_unit = tg(self.test_colors, upd, upd_tf, opacities, self.settings | (1 << 15))[4:6]
+        else:
+            # the settings | 1 << 15 call has the first call's geometry and weights: its texture output is the zero
+            # texture's (0) and its normal is the first call's accumulated normal as a unit vector (0 where none),
+            # the same fp32 operations as the kernel's bit-15 epilogue -- no third raster pass
+            n2 = (normal[..., 0] * normal[..., 0] + normal[..., 1] * normal[..., 1]) + normal[..., 2] * normal[..., 2]
+            inv = torch.where(n2 > 0, 1.0 / torch.sqrt(n2), torch.zeros_like(n2))
+            n_edit, n_unit = None, normal * inv[..., None]
         zeros3 = torch.zeros_like(img)  # texture channels 3..5 of every call
         bg = self.background[None, None, :]
         rgb = torch.clamp(img + tex[..., 0:3] + (1 - alpha[..., None]) * bg, 0.0, 1.0)
+        edit_tex_img = n_edit[..., :3] if n_edit is not None else zeros3
         return dict(rgb=rgb, depth=depth, alpha=alpha, normal=normal,
                     test_img=t_out[0] + (1 - t_out[3][..., None]) * bg,
                     uv_im=torch.clamp(zeros3 + (1 - t_out[3][..., None]) * bg, 0.0, 1.0),
-                    edit_img=torch.clamp(img + n_out[4][..., :3] + (1 - alpha[..., None]) * bg, 0.0, 1.0),
-                    clean_normal_img=torch.clamp(0.5 * (n_out[5] + 1) + (1 - alpha[..., None]) * bg, 0.0, 1.0))
+                    edit_img=torch.clamp(img + edit_tex_img + (1 - alpha[..., None]) * bg, 0.0, 1.0),
+                    clean_normal_img=torch.clamp(0.5 * (n_unit + 1) + (1 - alpha[..., None]) * bg, 0.0, 1.0))
 
     def loss(self, rgb: torch.Tensor, gt: torch.Tensor, ssim_lambda: float = 0.2) -> torch.Tensor:
         l1 = torch.abs(gt - rgb).mean()
