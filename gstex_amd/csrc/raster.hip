@@ -2016,6 +2016,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
+    const bool ordered = (settings & GSTEX_BWD_ORDERED) != 0;  // gstex_raster_bwd_order already ran on this aux
+    settings &= ~GSTEX_BWD_ORDERED;
     int rc = check_settings(settings);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && state && aux, "gstex_raster_bwd: null pointer (tile_ranges, state and the forward's aux)");
@@ -2033,8 +2035,10 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     if (n_isect > 0 && row_flags && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
     // costliest units first, from the histogram the forward built (order entries are unit + 1)
-    rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
-    if (rc) return rc;
+    if (!ordered) {
+        rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
+        if (rc) return rc;
+    }
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
 #define GSTEX_BWD(CC, GG)                                                                                      \
@@ -2050,6 +2054,18 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     else GSTEX_BWD(0, true);
 #undef GSTEX_BWD
     return launch_status("gstex_raster_bwd");
+}
+
+extern "C" int gstex_raster_bwd_order(const gstex_camera* cam, int32_t channels, int64_t n_isect, void* aux,
+                                      void* stream) {
+    GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0 && cam->block == kTile, "gstex_raster_bwd_order: invalid camera");
+    GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd_order: channels must be in [1, 8]");
+    GSTEX_REQUIRE(aux, "gstex_raster_bwd_order: null aux");
+    GSTEX_REQUIRE(n_isect >= 0 && n_isect < (int64_t)INT32_MAX, "gstex_raster_bwd_order: n_isect out of range");
+    const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
+    const AuxLayout al = aux_layout(n_isect, tiles_x * tiles_y, channels);
+    const AuxPtrs ap = aux_ptrs(aux, al);
+    return unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, as_stream(stream));
 }
 
 extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels) {

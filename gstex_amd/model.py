@@ -252,7 +252,7 @@ class GStexTrainer:
         deg = self.sh_degree if sh_degree_now is None else sh_degree_now
         if self.fused_activations:  # one HIP launch each way (gstex_amd.activations)
             quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
-                means, self.quats, self.scales, self.opacities, self.mappings, view.c2w[:3, 3])
+                means, self.quats, self.scales, self.opacities, self.mappings, view.campos)
         else:
             quats = self.quats / self.quats.norm(dim=-1, keepdim=True)
             s = torch.exp(self.scales[:, :-1]).clamp(min=1e-9)
@@ -312,7 +312,7 @@ class GStexTrainer:
         self.wait_texture()
         means = self.means
         quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
-            means, self.quats, self.scales, self.opacities, self.mappings, view.c2w[:3, 3])
+            means, self.quats, self.scales, self.opacities, self.mappings, view.campos)
         if self.fix_init and self.sh_degree > 0:
             viewdirs = torch.stack([viewdirs[:, 0], -viewdirs[:, 2], viewdirs[:, 1]], -1)
         intr = (view.fx, view.fy, view.cx, view.cy)

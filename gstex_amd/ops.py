@@ -109,6 +109,17 @@ def _stream(t: torch.Tensor) -> int:
     return _lib.stream_of(t.device)
 
 
+_ORDER_STREAMS: dict = {}
+
+
+def _order_stream(dev: torch.device) -> torch.cuda.Stream:
+    """The side stream the backward's unit ordering runs on (one per device)."""
+    s = _ORDER_STREAMS.get(dev.index)
+    if s is None:
+        s = _ORDER_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
 # ----------------------------------------------------------------------------------------
 # project_points / get_aabb_2d / get_num_tiles_hit_2d
 # ----------------------------------------------------------------------------------------
@@ -455,6 +466,18 @@ class _TextureGaussians(torch.autograd.Function):
              ptr(state), n_isect, ptr(aux), ptr(zbuf), 0 if zbuf is None else zbuf.numel(), ptr(ctx.partials),
              0 if ctx.partials is None else ctx.partials.numel(), st)
         ctx.aux = aux
+        ctx.order_ready = None
+        if aux is not None and n_isect > 0:
+            # the backward's unit launch order (a scan and a scatter over the forward's per-unit costs, ~18 us of
+            # latency-bound launches) on a side stream, overlapping the loss kernels that run before the backward
+            main = torch.cuda.current_stream(dev)
+            side = _order_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                _launch("gstex_raster_bwd_order", cam, C, n_isect, ptr(aux), side.cuda_stream)
+                ctx.order_ready = torch.cuda.Event()
+                ctx.order_ready.record(side)
+            aux.record_stream(side)
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
                               bg if bg is not None else vm)
@@ -506,7 +529,12 @@ class _TextureGaussians(torch.autograd.Function):
             row_flags = None
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
-        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges),
+        if ctx.order_ready is not None:  # the unit order was computed on the side stream after the forward
+            torch.cuda.current_stream(dev).wait_event(ctx.order_ready)
+            settings_b = int(settings) | _lib.BWD_ORDERED
+        else:
+            settings_b = settings
+        _launch("gstex_raster_bwd", cam, C, settings_b, ptr(bg), ptr(records), ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
                 ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)

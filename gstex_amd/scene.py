@@ -61,6 +61,16 @@ class View:
     def to(self, device):
         return View(self.viewmat.to(device), self.c2w.to(device), self.fx, self.fy, self.cx, self.cy, self.H, self.W)
 
+    @property
+    def campos(self) -> torch.Tensor:
+        """The camera centre c2w[:3, 3] as a contiguous (3,) tensor, made once per view (a per-render copy of the
+        strided column was a kernel launch of its own)."""
+        c = self.__dict__.get("_campos")
+        if c is None or c.device != self.c2w.device:
+            c = self.c2w[:3, 3].contiguous()
+            self.__dict__["_campos"] = c
+        return c
+
 
 def sphere_view(index: int, H: int, W: int, n_views: int = 8, radius: float = CAM_RADIUS) -> View:
     """Camera `index` of `n_views` spread over a sphere (golden-angle spiral), Blender intrinsics."""

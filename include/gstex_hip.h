@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 11
+#define GSTEX_ABI_VERSION 12
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -51,6 +51,9 @@ extern "C" {
 #define GSTEX_SETTING_DIST_REG (1 << 10) /* 2DGS NDC depth-distortion output */
 #define GSTEX_SETTING_EDIT (1 << 13)     /* texture_edit request (gstex.py:599) */
 #define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198): normal output unit-length, forward only */
+/* gstex_raster_bwd only (ABI 12): the backward's unit launch order was already computed on this aux by
+ * gstex_raster_bwd_order (e.g. on a side stream while the loss kernels run): the backward skips it. */
+#define GSTEX_BWD_ORDERED (1 << 30)
 
 typedef enum {
     GSTEX_OK = 0,
@@ -198,6 +201,10 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const float* v_img, const float* v_depth, const float* v_reg, const float* v_alpha,
                      const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
                      uint32_t* row_flags, float* v_texture, void* aux, void* stream);
+/* The backward's unit launch order alone (ABI 12): computed from the forward's aux (its per-unit costs and
+ * histogram) into the same aux; a gstex_raster_bwd whose settings carry GSTEX_BWD_ORDERED then skips it.  Lets
+ * the ordering run on another stream between the forward and the backward. */
+int gstex_raster_bwd_order(const gstex_camera* cam, int32_t channels, int64_t n_isect, void* aux, void* stream);
 /* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
  * them to the splat parameters. Outputs are overwritten.  partials is consumed: each splat's sums are written
  * over its first row (the rows are backward scratch, not read again).  row_flags == NULL: partials is the
