@@ -107,7 +107,7 @@ class GStexTrainer:
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
                  async_texture: bool = False, defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0,
-                 use_normal_loss: bool = False):
+                 use_normal_loss: bool = False, defer_side_stream: bool | None = None):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -179,7 +179,14 @@ class GStexTrainer:
         # the texel-gradient sink is zeroed by the first differentiable raster forward after an optimizer step
         # (gstex_raster_fwd_zero), so several renders of one step still accumulate their texel gradients
         self._sink_fresh = True
-        self._tex_stream = torch.cuda.Stream(device=d) if self.async_texture else None
+        # defer_side_stream (one GPU, defer_texture): the deferred update is enqueued at the pair-count read-back on a
+        # side stream instead, so it overlaps the binning's placement and sort (latency-bound kernels that leave HBM
+        # mostly idle); the raster forward waits for it.  Measured slower (+15 us median per step): off
+        # by default, GSTEX_DEFER_SIDE=1 turns it on.
+        if defer_side_stream is None:
+            defer_side_stream = os.environ.get("GSTEX_DEFER_SIDE", "0") != "0"
+        self.defer_side = bool(defer_side_stream) and self.defer_texture
+        self._tex_stream = torch.cuda.Stream(device=d) if (self.async_texture or self.defer_side) else None
         self._tex_ready = None
         self._tex_grad = None
         # the side-stream update's workgroup cap (GSTEX_TEX_ADAM_GRID; 0 = full grid).  Measured at cfg3: no cap, 512,
@@ -207,6 +214,25 @@ class GStexTrainer:
         fn, self._pending_tex = self._pending_tex, None
         if fn is not None:
             fn()
+
+    def _launch_pending_texture_side(self):
+        """The deferred texel update on the side stream, after everything the current stream has enqueued (the
+        backward, the head update); the raster forward waits for its event (_wait_side_texture)."""
+        fn, self._pending_tex = self._pending_tex, None
+        if fn is None:
+            return
+        main = torch.cuda.current_stream(self.device)
+        self._tex_stream.wait_stream(main)
+        with torch.cuda.stream(self._tex_stream):
+            fn()
+            ev = torch.cuda.Event()
+            ev.record(self._tex_stream)
+        self._tex_ready = ev
+
+    def _wait_side_texture(self):
+        if self._tex_ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._tex_ready)
+            self._tex_ready = None
 
     def wait_texture(self):
         """Order the current stream after the pending texel update: a deferred one (defer_texture) is enqueued now,
@@ -283,6 +309,7 @@ class GStexTrainer:
         # forward, so that the binning's placement and sort do not queue behind that wait
         pend = self._pending_tex is not None
         late = pend and self._pending_collective
+        side = pend and not late and self.defer_side
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
@@ -291,8 +318,9 @@ class GStexTrainer:
             geometry_outputs=self.geometry_outputs if geometry is None else geometry,
             texture_grad_sink=self.texture_grad_sink, zero_texture_grad_sink=self._sink_fresh,
             on_texture_grad=self.texture_grad_ready,
-            texture_ready=self._run_pending_texture if late else self._tex_ready,
-            before_pair_wait=self._run_pending_texture if pend and not late else None)
+            texture_ready=(self._run_pending_texture if late else self._wait_side_texture if side else self._tex_ready),
+            before_pair_wait=(self._launch_pending_texture_side if side else
+                              self._run_pending_texture if pend and not late else None))
         self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
         if torch.is_grad_enabled():
             self._sink_fresh = False  # zeroed by this forward: further renders before the step accumulate on top
