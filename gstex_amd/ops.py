@@ -7,6 +7,7 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import NamedTuple, Tuple
 
@@ -110,6 +111,7 @@ def _stream(t: torch.Tensor) -> int:
 
 
 _ORDER_STREAMS: dict = {}
+_ORDER_SIDE = os.environ.get("GSTEX_ORDER_SIDE", "1") != "0"  # 0: the backward orders its units itself
 
 
 def _order_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -467,7 +469,7 @@ class _TextureGaussians(torch.autograd.Function):
              0 if ctx.partials is None else ctx.partials.numel(), st)
         ctx.aux = aux
         ctx.order_ready = None
-        if aux is not None and n_isect > 0:
+        if aux is not None and n_isect > 0 and _ORDER_SIDE:
             # the backward's unit launch order (a scan and a scatter over the forward's per-unit costs, ~18 us of
             # latency-bound launches) on a side stream, overlapping the loss kernels that run before the backward
             main = torch.cuda.current_stream(dev)

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-3 end-state evidence: -m gpu suite, smoke, the default bench line, the driver's bench command, and the
+# rocprofv3 trace + PMC passes (tools/profile_bench.sh r03w).
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/r03w; mkdir -p $OUT
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+grep -E "passed|failed" $OUT/gpu_tests.log | tail -1
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+timeout -k 10 400 python3 -u bench.py > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
+tail -1 $OUT/bench.log | cut -c1-300
+timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 > $OUT/bench_driver_cmd.log 2>&1 || { tail -20 $OUT/bench_driver_cmd.log; exit 1; }
+tail -1 $OUT/bench_driver_cmd.log | cut -c1-200
+timeout -k 10 1200 bash tools/profile_bench.sh r03w > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
+tail -2 $OUT/prof.log
