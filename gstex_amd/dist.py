@@ -128,6 +128,9 @@ class GradSync:
     def zero(self):
         if self._work is not None:
             raise RuntimeError("GradSync.zero(): the previous backward's all_reduce() was never called")
+        reset = getattr(self.trainer, "reset_texture_grad", None)
+        if reset is not None:
+            reset()  # the sink (the texel slice) is zeroed by the next differentiable raster forward
         if self.rebuild():
             return  # a new buffer is zero
         if getattr(self.trainer, "texture_grad_zeroed_by_update", False):

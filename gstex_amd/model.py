@@ -210,6 +210,12 @@ class GStexTrainer:
         async_texture / defer_texture, that fill would also race or pre-empt the update still reading it)."""
         return True
 
+    def reset_texture_grad(self):
+        """Zero the texel-gradient sink lazily: the next differentiable render's raster forward zeroes it before its
+        backward accumulates (gstex_raster_fwd_zero).  Called by zero_grad() and by gstex_amd.dist.GradSync.zero(), so
+        a gradient left by a backward whose step was skipped never leaks into the next step."""
+        self._sink_fresh = True
+
     def _run_pending_texture(self):
         fn, self._pending_tex = self._pending_tex, None
         if fn is not None:
@@ -477,6 +483,7 @@ class GStexTrainer:
         writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
         when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead).  With
         async_texture / defer_texture the texel gradient buffer is kept (the raster forward zeroes it)."""
+        self.reset_texture_grad()
         if self.async_texture or self.defer_texture:
             keep = self.texture_dc.grad
             self.optimizer.zero_grad(set_to_none=set_to_none)

@@ -64,12 +64,14 @@ class View:
     @property
     def campos(self) -> torch.Tensor:
         """The camera centre c2w[:3, 3] as a contiguous (3,) tensor, made once per view (a per-render copy of the
-        strided column was a kernel launch of its own)."""
-        c = self.__dict__.get("_campos")
-        if c is None or c.device != self.c2w.device:
-            c = self.c2w[:3, 3].contiguous()
-            self.__dict__["_campos"] = c
-        return c
+        strided column was a kernel launch of its own).  The cache is keyed on the c2w tensor's identity, storage and
+        version counter, so reassigning c2w or editing it in place recomputes it."""
+        key = (id(self.c2w), self.c2w.data_ptr(), self.c2w._version, self.c2w.device)
+        hit = self.__dict__.get("_campos")
+        if hit is None or hit[0] != key:
+            hit = (key, self.c2w[:3, 3].contiguous())
+            self.__dict__["_campos"] = hit
+        return hit[1]
 
 
 def sphere_view(index: int, H: int, W: int, n_views: int = 8, radius: float = CAM_RADIUS) -> View:

@@ -7,6 +7,10 @@ conventions its consumers fix:
     plane (residual ~1e-6), where integer pixel coordinates would miss it by ~1e-2;
   * world-space normals facing the camera: the reference's depth_to_normal (gstex.py:151-161), as its normal loss
     uses it (gstex.py:1218-1220, 1316), agrees with the rendered normal in direction and sign;
+  * the same with the AA low-pass (settings bit 9) on;
+  * texel placement and the bilinear lookup: texel values a linear ramp in the reference's own texel uv
+    (texture_dims_to_query, jagged_texture.py:23-34) render as that ramp at each pixel's uv (get_uv_mapping,
+    gstex.py:975-990, of the hit point depths_to_points gives);
   * the composite (gstex.py:1204-1205) and the loss terms of get_loss_dict (gstex.py:1301-1322).
 CPU tests: the oracle against the golden; -m gpu tests: the HIP path against the same golden.
 """
@@ -27,7 +31,7 @@ def z():
         return {k: f[k] for k in f.files}
 
 
-def _plane_inputs(z):
+def _plane_inputs(z, aa=False):
     H, W = (int(v) for v in z["plane_hw"])
     fx, fy, cx, cy = (float(v) for v in z["plane_intr"])
     vm = torch.from_numpy(z["plane_viewmat"])
@@ -42,8 +46,41 @@ def _plane_inputs(z):
     _, depths = O.project_points(means, cam)
     inp = O.RasterInputs(torch.zeros((n, 3), dtype=torch.int32), centers, extents, depths, torch.full((n, 3), 0.5),
                          opac, means, scales, 1.0, quats, torch.full((n, 1, 2), 0.5), torch.zeros((n, 1, 3)),
-                         torch.zeros((n, 1, 3)), torch.zeros((0, 3)), cam, settings=int(z["plane_settings"][0]))
+                         torch.zeros((n, 1, 3)), torch.zeros((0, 3)), cam,
+                         settings=int(z["plane_aa_settings" if aa else "plane_settings"][0]))
     return inp, (vm, c2w, fx, fy, cx, cy, H, W)
+
+
+def _tex_inputs(z):
+    H, W = (int(v) for v in z["tex_hw"])
+    fx, fy, cx, cy = (float(v) for v in z["tex_intr"])
+    vm = torch.from_numpy(z["tex_viewmat"])
+    c2w = torch.from_numpy(z["tex_c2w"])
+    cam = O.Camera(vm, fx, fy, cx, cy, H, W, 16, c2w[:3, 3])
+    t = {k: torch.from_numpy(z["tex_" + k]) for k in ("means", "scales", "quats", "opacities", "dims", "texture",
+                                                        "uv0", "umap", "vmap")}
+    n = t["means"].shape[0]
+    centers, extents = O.aabb_2d(t["means"], t["scales"], 1.0, t["quats"], cam)
+    _, depths = O.project_points(t["means"], cam)
+    inp = O.RasterInputs(t["dims"], centers, extents, depths, torch.full((n, 3), 0.5), t["opacities"], t["means"],
+                         t["scales"], 1.0, t["quats"], t["uv0"], t["umap"], t["vmap"], t["texture"], cam,
+                         settings=int(z["tex_settings"][0]))
+    return inp, (vm, c2w, fx, fy, cx, cy, H, W)
+
+
+def _hip_render(inp, vm, c2w, fx, fy, cx, cy, H, W):
+    import gstex_cuda
+
+    dev = "cuda"
+    d = lambda t: t.detach().to(dev).contiguous()  # noqa: E731
+    n = inp.means.shape[0]
+    C = inp.texture.shape[1]
+    nth = O.num_tiles_hit(inp.centers, inp.extents, H, W)
+    outs = gstex_cuda.texture_gaussians(
+        (n, 1, C), d(inp.texture_dims), d(inp.centers), d(inp.extents), d(inp.depths), d(nth), d(inp.rgbs),
+        d(inp.opacities), d(inp.means), d(inp.scales), 1.0, d(inp.quats), d(inp.uv0), d(inp.umap), d(inp.vmap),
+        d(inp.texture), d(vm), d(c2w), fx, fy, cx, cy, H, W, 16, inp.settings)
+    return {"depth": outs[1].cpu(), "alpha": outs[3].cpu(), "tex": outs[4].cpu(), "normal": outs[5].cpu()}
 
 
 def _interior(alpha):
@@ -90,6 +127,49 @@ def test_oracle_renders_the_golden_plane(z):
         np.testing.assert_array_equal(o32[k].numpy(), z[g], err_msg=k)
 
 
+def test_reference_points_lie_on_the_aa_plane(z):
+    """The same plane with the AA low-pass on (settings bit 9, the reference's default): the reference's
+    depths_to_points puts >= 99 % of the interior pixels on the plane to 1e-5 and its depth_to_normal agrees with the
+    rendered normals.  (The few off the plane -- 14 of 3,212 -- lie next to a splat's AABB centre, where 2 |centre -
+    pixel|^2 undercuts the ray-splat distance and the 2DGS screen-space branch, depth = the centre's, takes over.)"""
+    inside = z["plane_aa_alpha"] > 0.999
+    assert inside.mean() > 0.5
+    n = z["plane_normal"].astype(np.float64)
+    res = np.abs(z["plane_aa_ref_points"].astype(np.float64) @ n)[inside]
+    assert (res < 1e-5).mean() > 0.99, (res < 1e-5).mean()
+    assert np.abs(z["plane_aa_depth"] - z["plane_depth"]).max() > 0  # the bit changed some pixels
+    m = _interior(z["plane_aa_alpha"])
+    est = z["plane_aa_ref_est_normal"].astype(np.float64)
+    rn = z["plane_aa_rnormal"].astype(np.float64)
+    cos = (est * (rn / np.linalg.norm(rn, axis=-1, keepdims=True).clip(1e-30))).sum(-1)[m]
+    assert cos.min() > 0.999 and np.median(cos) > 0.99995, (cos.min(), np.median(cos))
+
+
+def test_textured_render_is_the_reference_texel_ramp(z):
+    """Texel values a linear ramp in the reference's texel uv (texture_dims_to_query, jagged_texture.py:23-34): the
+    rendered texture / alpha of each pixel equals the ramp at that pixel's uv (reference get_uv_mapping of the hit
+    point the reference's depths_to_points gives) to ~1e-6 -- texels corner-aligned at (i / h, j / w), bilinear --
+    while texel-centred placement ((i + 0.5) / h) misses by >= 5e-3."""
+    m = z["tex_mask"]
+    assert m.sum() > 500
+    val = z["tex_render"] / np.maximum(z["tex_alpha"], 1e-30)[..., None]
+    err = np.abs(val - z["tex_ref_pred"])[m]
+    ctrl = np.abs(val - z["tex_ref_pred_centre"])[m]
+    assert err.max() < 1e-5, err.max()
+    assert ctrl.min() > 1e-3 and ctrl.min() > 100 * err.max(), (ctrl.min(), err.max())
+
+
+def test_oracle_renders_the_golden_aa_plane_and_textured_splats(z):
+    inp, _ = _plane_inputs(z, aa=True)
+    o32, _, _ = O.rasterize(inp)
+    for k, g in (("depth", "plane_aa_depth"), ("alpha", "plane_aa_alpha"), ("normal", "plane_aa_rnormal")):
+        np.testing.assert_array_equal(o32[k].numpy(), z[g], err_msg=k)
+    inp, _ = _tex_inputs(z)
+    o32, _, _ = O.rasterize(inp)
+    for k, g in (("tex", "tex_render"), ("alpha", "tex_alpha"), ("depth", "tex_depth")):
+        np.testing.assert_array_equal(o32[k].numpy(), z[g], err_msg=k)
+
+
 def test_composite_and_loss_terms_match_reference(z):
     """The composite (gstex.py:1204-1205) as GStexTrainer.render forms it, and the loss combination of
     get_loss_dict with the golden's stubbed SSIM value."""
@@ -113,24 +193,33 @@ def test_composite_and_loss_terms_match_reference(z):
 def test_hip_plane_depth_normal_match_golden(z):
     """The HIP rasterizer's depth / alpha / normal of the plane: within the forward tolerance of the golden, so the
     reference's depths_to_points / depth_to_normal see the same geometry from the HIP path."""
-    import gstex_cuda
-
     from helpers import TOL_ABS, TOL_REL
 
-    inp, (vm, c2w, fx, fy, cx, cy, H, W) = _plane_inputs(z)
-    dev = "cuda"
-    d = lambda t: t.detach().to(dev).contiguous()  # noqa: E731
-    n = inp.means.shape[0]
-    nth = O.num_tiles_hit(inp.centers, inp.extents, H, W)
-    outs = gstex_cuda.texture_gaussians(
-        (n, 1, 3), d(inp.texture_dims), d(inp.centers), d(inp.extents), d(inp.depths), d(nth), d(inp.rgbs),
-        d(inp.opacities), d(inp.means), d(inp.scales), 1.0, d(inp.quats), d(inp.uv0), d(inp.umap), d(inp.vmap),
-        torch.zeros((0, 3), device=dev), d(vm), d(c2w), fx, fy, cx, cy, H, W, 16, inp.settings)
-    got = {"depth": outs[1].cpu(), "alpha": outs[3].cpu(), "normal": outs[5].cpu()}
-    for k, g in (("depth", "plane_depth"), ("alpha", "plane_alpha"), ("normal", "plane_rnormal")):
+    for aa in (False, True):
+        inp, geom = _plane_inputs(z, aa=aa)
+        got = _hip_render(inp, *geom)
+        p = "plane_aa_" if aa else "plane_"
+        for k in ("depth", "alpha", "normal"):
+            ref = torch.from_numpy(z[p + ("rnormal" if k == "normal" else k)]).double()
+            err = (got[k].double() - ref).abs()
+            assert bool((err <= TOL_ABS + TOL_REL * ref.abs()).all()), f"{p}{k}: max err {float(err.max()):.3e}"
+
+
+@pytest.mark.gpu
+def test_hip_textured_splats_match_golden_and_reference_ramp(z):
+    """The HIP path on the textured golden: within the forward tolerance of the golden render, and its texture /
+    alpha equal to the reference-predicted texel ramp (test_textured_render_is_the_reference_texel_ramp)."""
+    from helpers import TOL_ABS, TOL_REL
+
+    inp, geom = _tex_inputs(z)
+    got = _hip_render(inp, *geom)
+    for k, g in (("tex", "tex_render"), ("alpha", "tex_alpha"), ("depth", "tex_depth")):
         ref = torch.from_numpy(z[g]).double()
         err = (got[k].double() - ref).abs()
         assert bool((err <= TOL_ABS + TOL_REL * ref.abs()).all()), f"{k}: max err {float(err.max()):.3e}"
+    m = z["tex_mask"]
+    val = got["tex"].numpy() / np.maximum(got["alpha"].numpy(), 1e-30)[..., None]
+    assert np.abs(val - z["tex_ref_pred"])[m].max() < 1e-5
 
 
 @pytest.mark.gpu

@@ -193,6 +193,51 @@ def test_deferred_texture_update_matches_plain_step():
         dist.destroy_process_group()
 
 
+def test_skipped_step_leaves_no_stale_texel_gradient():
+    """a backward whose optimizer step is skipped (e.g. a non-finite loss) must not leak its texel
+    gradient into the next step.  zero_grad() (alone) and GradSync.zero() (data-parallel, world 1 over RCCL) mark the
+    persistent sink for re-zeroing by the next raster forward: zero_grad, backward, no step, zero_grad, backward, step
+    must train like the plain trainer doing only the second backward and step."""
+    from gstex_amd.dist import GradSync
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        sc = make_scene(3000, 60_000, seed=13)
+        views = [sphere_view(i, 96, 96).to(dev) for i in range(2)]
+        g = torch.Generator().manual_seed(6)
+        gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(2)]
+        plain = GStexTrainer(sc, dev, start_step=3000)
+        deferred = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+        synced = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+        sync = GradSync(synced, 1)
+        for step in range(3):
+            plain.zero_grad()
+            plain.forward_backward(views[1], gts[1])
+            plain.optimizer_step()
+            deferred.zero_grad()
+            deferred.forward_backward(views[0], gts[0])  # its step is skipped
+            deferred.zero_grad()
+            deferred.forward_backward(views[1], gts[1])
+            deferred.optimizer_step()
+            sync.zero()
+            synced.forward_backward(views[0], gts[0])  # skipped
+            sync.zero()
+            synced.forward_backward(views[1], gts[1])
+            synced.optimizer_step(sync=sync)
+        for tr in (deferred, synced):
+            tr.wait_texture()
+        torch.cuda.synchronize()
+        for other in (deferred, synced):
+            for (name, a), b in zip(plain.param_groups().items(), other.param_groups().values()):
+                _assert_trains_alike(name, a[0], b[0], "skipped step")
+    finally:
+        dist.destroy_process_group()
+
+
 def test_texture_sink_accumulates_the_renders_of_one_step():
     """Two views per optimizer step (gradient accumulation): the persistent texel-gradient sink of a deferred-update
     trainer is zeroed by the step's first raster forward only, so both views' texel gradients reach the update -- it

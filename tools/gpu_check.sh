@@ -5,8 +5,8 @@
 # VARIANTS="a b": also time scratch/<a>/libgstex_hip.so ... (tools/build_variant.sh); NOTESTS=1: timing only.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/check; mkdir -p $OUT
-timeout -k 10 180 python3 -u tools/raster_loop.py --photometric --iters 20 > $OUT/loop_new.log 2>&1 || { echo "loop_new FAILED"; tail -20 $OUT/loop_new.log; exit 1; }
-echo "new : $(tail -1 $OUT/loop_new.log)"
+[ -z "$NOLOOP" ] && { timeout -k 10 180 python3 -u tools/raster_loop.py --photometric --iters 20 > $OUT/loop_new.log 2>&1 || { echo "loop_new FAILED"; tail -20 $OUT/loop_new.log; exit 1; }
+echo "new : $(tail -1 $OUT/loop_new.log)"; }
 if [ -d scratch/head ]; then
   (cd scratch/head && timeout -k 10 180 python3 -u tools/raster_loop.py --photometric --iters 20) > $OUT/loop_head.log 2>&1 || { echo "loop_head FAILED"; tail -5 $OUT/loop_head.log; exit 1; }
   echo "head: $(tail -1 $OUT/loop_head.log)"
