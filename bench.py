@@ -452,11 +452,14 @@ def main():
             "sh_degree": trainer.sh_degree_now(), "settings": trainer.settings,
             "geometry_outputs": trainer.geometry_outputs,
             "fold_aabb": True, "texture_transform": "SH2RGB on read (0.28209479, 0.5)",
+            "pair_buffers": ("capacity-sized, pair total kept on the device: no host read-back or synchronisation in "
+                             "the step (ops.PairCapacity, capacity %d)" % trainer.pairs.capacity
+                             if trainer.pairs is not None else "sized by a host read-back of the pair total"),
             "texture_update": ("side stream: the texel Adam update (zeroing its gradient) overlaps the next step's "
                                "preprocessing and binning; the raster forward waits for it" if trainer.async_texture
-                               else "deferred: step k's texel Adam update runs in step k+1's render while the host "
-                                    "reads back the pair count (same stream, before the raster forward); the timed "
-                                    "region holds exactly K texel updates" if trainer.defer_texture
+                               else "deferred: step k's texel Adam update runs in step k+1's render (same stream, "
+                                    "before the raster forward); the timed region holds exactly K texel updates"
+                               if trainer.defer_texture
                                else "compute stream"),
         },
         "roofline": roofline,

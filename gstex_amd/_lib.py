@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 REC_FLOATS = 32
 BWD_ORDERED = 1 << 30  # GSTEX_BWD_ORDERED: gstex_raster_bwd skips the unit ordering
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
@@ -53,6 +53,15 @@ class GstexAdamTensor(ctypes.Structure):
     ]
 
 
+class GstexPairGuard(ctypes.Structure):
+    _fields_ = [
+        ("capacity", c_int64),
+        ("step_flag", c_void_p),
+        ("host_count", c_void_p),
+        ("first", c_int32),
+    ]
+
+
 ADAM_MAX_TENSORS = 16
 ADAM_ZERO_GRAD = 1  # GSTEX_ADAM_ZERO_GRAD
 ADAM_GRID_SHIFT = 8  # GSTEX_ADAM_GRID_SHIFT
@@ -81,6 +90,13 @@ SIGNATURES = {
         [c_int32, c_int64, _P, _P, _P, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_size_t, _P],
     ),
     "gstex_tile_order": (c_int32, [c_int32, _P, _P, _P]),
+    "gstex_scan_offsets_guarded": (c_int32, [c_int32, _P, _P, _P, c_size_t, POINTER(GstexPairGuard), _P]),
+    "gstex_bin_sort_capped": (
+        c_int32,
+        [c_int32, c_int64, _P, _P, _P, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_size_t, _P],
+    ),
+    "gstex_host_words_alloc": (c_int32, [c_int32, POINTER(c_void_p), POINTER(c_void_p)]),
+    "gstex_host_words_free": (c_int32, [c_void_p]),
     "gstex_raster_setup": (
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
@@ -130,6 +146,8 @@ SIGNATURES = {
     "gstex_adam_step_ex": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32, _P]),
     "gstex_adam_step_scaled": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32,
                                          c_float, _P]),
+    "gstex_adam_step_guarded": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32,
+                                          c_float, _P, _P]),
 }
 
 _lib = None

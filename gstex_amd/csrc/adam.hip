@@ -48,6 +48,7 @@ struct AdamArgs {
     int n;
     float beta1, beta2, eps, one_m_beta1, one_m_beta2;
     float gscale;  // gradient scale applied on read (gstex_adam_step_scaled: a data-parallel 1 / world), 1 = none
+    const float* skip;  // gstex_adam_step_guarded: nothing is updated when *skip != 0 (nullable)
 };
 
 template <bool SCALE>
@@ -122,6 +123,7 @@ __device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
 // grid-stride over the chunks: a capped grid (GSTEX_ADAM_GRID flags) leaves most of every CU to another stream
 template <bool ZERO_GRAD, bool SCALE>
 __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
+    if (a.skip && *a.skip != 0.0f) return;  // an overflowed step (pair-capacity guard): no update
     for (int64_t b = blockIdx.x; b < a.block_start[a.n]; b += gridDim.x) adam_chunk<ZERO_GRAD, SCALE>(a, b);
 }
 
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
 
 namespace {
 int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2, double eps,
-                int32_t flags, float grad_scale, void* stream) {
+                int32_t flags, float grad_scale, void* stream, const float* skip = nullptr) {
     GSTEX_REQUIRE(n_tensors >= 0 && n_tensors <= kAdamMaxTensors,
                   "gstex_adam_step: n_tensors must be in [0, %d] (got %d)", kAdamMaxTensors, n_tensors);
     GSTEX_REQUIRE(n_tensors == 0 || tensors, "gstex_adam_step: null tensor table");
@@ -156,6 +158,7 @@ int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta
     a.one_m_beta1 = (float)(1.0 - beta1);
     a.one_m_beta2 = (float)(1.0 - beta2);
     a.gscale = grad_scale;
+    a.skip = skip;
     const int64_t cap = (flags >> GSTEX_ADAM_GRID_SHIFT) & 0xFFFF;
     const unsigned grid = (unsigned)(cap > 0 && cap < blocks ? cap : blocks);
     const hipStream_t st = gstex::as_stream(stream);
@@ -187,4 +190,13 @@ extern "C" int gstex_adam_step_scaled(int32_t n_tensors, const gstex_adam_tensor
     GSTEX_REQUIRE(grad_scale == grad_scale && grad_scale > 0.0f && grad_scale <= 1.0f,
                   "gstex_adam_step_scaled: grad_scale must be in (0, 1] (got %g)", (double)grad_scale);
     return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, grad_scale, stream);
+}
+
+extern "C" int gstex_adam_step_guarded(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                                       double eps, int32_t flags, float grad_scale, const float* skip, void* stream) {
+    GSTEX_REQUIRE((flags & ~(GSTEX_ADAM_ZERO_GRAD | (0xFFFF << GSTEX_ADAM_GRID_SHIFT))) == 0,
+                  "gstex_adam_step_guarded: unknown flags 0x%x", flags);
+    GSTEX_REQUIRE(grad_scale == grad_scale && grad_scale > 0.0f && grad_scale <= 1.0f,
+                  "gstex_adam_step_guarded: grad_scale must be in (0, 1] (got %g)", (double)grad_scale);
+    return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, grad_scale, stream, skip);
 }

@@ -83,9 +83,27 @@ __global__ __launch_bounds__(kScanThreads) void scan_block_sums_kernel(int nb, i
     }
 }
 
+// Pair-capacity guard (gstex_scan_offsets_guarded, ABI 13), applied by the thread that writes the total out[n]: the
+// step's overflow flag (1.0f when the total exceeds the pair buffers' capacity; the first render of a step writes it,
+// later ones OR into it) and, when given, the total in device-writable host memory (no copy, no synchronisation:
+// the host reads it once the stream has passed this kernel).  Plain vector stores.
+struct ScanGuard {
+    long long capacity;
+    float* flag;
+    int32_t* host_count;
+    int first;
+};
+__device__ __forceinline__ void apply_guard(const ScanGuard& g, int total) {
+    if (g.flag) {
+        const float over = (long long)total > g.capacity ? 1.0f : 0.0f;
+        *g.flag = g.first ? over : fmaxf(*g.flag, over);
+    }
+    if (g.host_count) *g.host_count = total;
+}
+
 __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(int n, const int32_t* __restrict__ in,
                                                                   const int32_t* __restrict__ block_offs,
-                                                                  int32_t* __restrict__ out) {
+                                                                  int32_t* __restrict__ out, const ScanGuard guard) {
     __shared__ int s_wave[kScanThreads / 64];
     int base = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
     int vals[kScanItems];
@@ -102,12 +120,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(int n, const i
         if (base + k < n) out[base + k] = ex;
         ex += vals[k];
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = ex;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) {
+        out[n] = ex;
+        apply_guard(guard, ex);
+    }
 }
 
 // Short inputs (the per-tile scans): one workgroup walks the tiles with a running carry, one launch instead of three.
 __global__ __launch_bounds__(kScanThreads) void scan_single_kernel(int n, const int32_t* __restrict__ in,
-                                                                   int32_t* __restrict__ out) {
+                                                                   int32_t* __restrict__ out, const ScanGuard guard) {
     __shared__ int s_wave[kScanThreads / 64];
     int carry = 0;
     for (int b0 = 0; b0 < n; b0 += kScanTile) {
@@ -128,34 +149,42 @@ __global__ __launch_bounds__(kScanThreads) void scan_single_kernel(int n, const 
         }
         carry += total;
     }
-    if (threadIdx.x == 0) out[n] = carry;
+    if (threadIdx.x == 0) {
+        out[n] = carry;
+        apply_guard(guard, carry);
+    }
 }
 constexpr int kScanSingleMaxTiles = 16;
 
-int run_scan(int n, const int32_t* in, int32_t* out, int32_t* block_sums, hipStream_t st) {
+int run_scan(int n, const int32_t* in, int32_t* out, int32_t* block_sums, hipStream_t st,
+             const ScanGuard guard = ScanGuard{0, nullptr, nullptr, 0}) {
     int nb = div_up(n, kScanTile);
-    if (nb == 0) {
-        (void)hipMemsetAsync(out, 0, sizeof(int32_t), st);
-        return launch_status("scan(empty)");
-    }
-    if (nb <= kScanSingleMaxTiles) {
-        scan_single_kernel<<<1, kScanThreads, 0, st>>>(n, in, out);
+    if (nb <= kScanSingleMaxTiles) {  // (n = 0 included: the single workgroup writes out[0] = 0)
+        scan_single_kernel<<<1, kScanThreads, 0, st>>>(n, in, out, guard);
         return launch_status("scan");
     }
     scan_partials_kernel<<<nb, kScanThreads, 0, st>>>(n, in, block_sums);
     scan_block_sums_kernel<<<1, kScanThreads, 0, st>>>(nb, block_sums);
-    scan_final_kernel<<<nb, kScanThreads, 0, st>>>(n, in, block_sums, out);
+    scan_final_kernel<<<nb, kScanThreads, 0, st>>>(n, in, block_sums, out, guard);
     return launch_status("scan");
 }
 
 size_t scan_ws_bytes(int n) { return (size_t)(div_up(n, kScanTile) + 1) * sizeof(int32_t); }
 
 // 1. count + rank
+// Capacity mode (gstex_bin_sort_capped): the pair total offsets[n] is read on the device; a total beyond the pair
+// buffers' capacity leaves every tile empty (no pair is emitted, so nothing is written past the buffers) and the
+// step's guard flag (gstex_scan_offsets_guarded) tells the optimizer to skip the step.
+__device__ __forceinline__ bool over_capacity(const int32_t* offsets, int n, long long cap) {
+    return cap >= 0 && (long long)offsets[n] > cap;
+}
+
 __global__ __launch_bounds__(256) void count_kernel(int n, const float* __restrict__ centers,
                                                     const float* __restrict__ extents,
                                                     const int32_t* __restrict__ offsets, int tiles_x,
                                                     int tiles_y, int block, int32_t* __restrict__ tile_count,
-                                                    int32_t* __restrict__ rank) {
+                                                    int32_t* __restrict__ rank, long long cap) {
+    if (over_capacity(offsets, n, cap)) return;
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     Rect r = tile_rect(centers[2 * g], centers[2 * g + 1], extents[2 * g], extents[2 * g + 1], tiles_x,
@@ -219,7 +248,8 @@ __global__ __launch_bounds__(256) void count_lds_kernel(int n, const float* __re
                                                         const float* __restrict__ extents,
                                                         const int32_t* __restrict__ offsets, int tiles_x,
                                                         int tiles_y, int block, int32_t* __restrict__ tile_count,
-                                                        int32_t* __restrict__ rank) {
+                                                        int32_t* __restrict__ rank, long long cap) {
+    if (over_capacity(offsets, n, cap)) return;  // (uniform over the workgroup: before any barrier)
     __shared__ int s_hist[kCountLdsTiles];
     const int n_tiles = tiles_x * tiles_y;
     for (int t = threadIdx.x; t < n_tiles; t += 256) s_hist[t] = 0;
@@ -275,7 +305,8 @@ __global__ __launch_bounds__(256) void place_kernel(int n, const float* __restri
                                                     const int32_t* __restrict__ tile_start,
                                                     const int32_t* __restrict__ rank,
                                                     unsigned long long* __restrict__ keys,
-                                                    int32_t* __restrict__ slot_gid) {
+                                                    int32_t* __restrict__ slot_gid, long long cap) {
+    if (over_capacity(offsets, n, cap)) return;
     // key = depth bits << 32 | emission slot: a splat's slots lie in [offsets[g], offsets[g + 1]) and each
     // splat has at most one slot per tile, so inside a tile the slot orders exactly as the splat id does
     // and the sorted key hands over the slot directly (the id comes from slot_gid)
@@ -600,10 +631,12 @@ extern "C" size_t gstex_bin_workspace_size(int32_t n, int64_t n_isect, int32_t n
 namespace {
 // tile_order_out (nullable): the largest-first launch order the tile sort used, identical to what
 // gstex_tile_order computes from tile_ranges (both rank the same bucket sizes), so the forward reuses it
+// capped: n_isect is the pair buffers' capacity and the true total is read on the device (offsets[n]; above the
+// capacity every tile comes out empty) -- no host read-back of the total is needed to launch the binning
 int bin_sort_impl(int32_t n, int64_t n_isect, const float* centers, const float* extents, const float* depths,
                   const int32_t* offsets, int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
                   int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order_out, void* workspace,
-                  size_t workspace_bytes, void* stream) {
+                  size_t workspace_bytes, void* stream, bool capped = false) {
     GSTEX_REQUIRE(n >= 0 && n_isect >= 0 && n_isect < (1ll << 31) && H > 0 && W > 0 && block > 0,
                   "gstex_bin_sort: invalid sizes (n=%d, n_isect=%lld, H=%d, W=%d, block=%d)", n,
                   (long long)n_isect, H, W, block);
@@ -615,26 +648,27 @@ int bin_sort_impl(int32_t n, int64_t n_isect, const float* centers, const float*
     GSTEX_REQUIRE(workspace && workspace_bytes >= need, "gstex_bin_sort: workspace too small (%zu < %zu)",
                   workspace_bytes, need);
     hipStream_t st = as_stream(stream);
-    if (n_isect == 0) {
+    if (n_isect == 0 && !capped) {
         (void)hipMemsetAsync(tile_ranges, 0, (size_t)n_tiles * 2 * sizeof(int32_t), st);
         if (tile_order_out) iota_kernel<<<div_up(n_tiles, 256), 256, 0, st>>>(n_tiles, tile_order_out);
         return launch_status("gstex_bin_sort(empty)");
     }
     GSTEX_REQUIRE(centers && extents && depths && offsets && sorted_ids && sorted_slots,
                   "gstex_bin_sort: null pointer");
+    const long long cap = capped ? (long long)n_isect : -1;
     BinWorkspace ws;
     bin_layout(n_tiles, n_isect, (char*)workspace, &ws);
     (void)hipMemsetAsync(ws.tile_count, 0, (size_t)(n_tiles + 1) * sizeof(int32_t), st);
     if (n_tiles <= kCountLdsTiles)
         count_lds_kernel<<<div_up(n, 256 * kCountSplatsPerThread), 256, 0, st>>>(
-            n, centers, extents, offsets, tiles_x, tiles_y, block, ws.tile_count, ws.rank);
+            n, centers, extents, offsets, tiles_x, tiles_y, block, ws.tile_count, ws.rank, cap);
     else
         count_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, offsets, tiles_x, tiles_y, block,
-                                                      ws.tile_count, ws.rank);
+                                                      ws.tile_count, ws.rank, cap);
     int rc = run_scan(n_tiles, ws.tile_count, ws.tile_start, ws.scan_ws, st);
     if (rc) return rc;
     place_kernel<<<div_up(n, 256), 256, 0, st>>>(n, centers, extents, depths, offsets, tiles_x, tiles_y, block,
-                                                  ws.tile_start, ws.rank, ws.keys, ws.slot_gid);
+                                                  ws.tile_start, ws.rank, ws.keys, ws.slot_gid, cap);
     const bool ranked = n_tiles <= kOrderCap;
     int32_t* order = tile_order_out ? tile_order_out : ws.order;
     if (ranked)
@@ -666,6 +700,28 @@ extern "C" int gstex_bin_sort_ordered(int32_t n, int64_t n_isect, const float* c
     GSTEX_REQUIRE(tile_order, "gstex_bin_sort_ordered: null tile_order");
     return bin_sort_impl(n, n_isect, centers, extents, depths, offsets, H, W, block, tile_ranges, sorted_ids,
                          sorted_slots, tile_order, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* centers, const float* extents,
+                                     const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                                     int32_t H, int32_t W, int32_t block, int32_t* tile_ranges, int32_t* sorted_ids,
+                                     int32_t* sorted_slots, int32_t* tile_order, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    (void)num_tiles_hit;
+    GSTEX_REQUIRE(tile_order, "gstex_bin_sort_capped: null tile_order");
+    GSTEX_REQUIRE(capacity >= 0, "gstex_bin_sort_capped: capacity < 0");
+    return bin_sort_impl(n, capacity, centers, extents, depths, offsets, H, W, block, tile_ranges, sorted_ids,
+                         sorted_slots, tile_order, workspace, workspace_bytes, stream, true);
+}
+
+extern "C" int gstex_scan_offsets_guarded(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
+                                          size_t workspace_bytes, const gstex_pair_guard* guard, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && offsets && guard, "gstex_scan_offsets_guarded: invalid arguments");
+    GSTEX_REQUIRE(n == 0 || num_tiles_hit, "gstex_scan_offsets_guarded: null input");
+    GSTEX_REQUIRE(workspace_bytes >= scan_ws_bytes(n) && workspace, "gstex_scan_offsets_guarded: workspace too small");
+    GSTEX_REQUIRE(guard->capacity >= 0, "gstex_scan_offsets_guarded: capacity < 0");
+    const ScanGuard g{(long long)guard->capacity, guard->step_flag, guard->host_count, guard->first ? 1 : 0};
+    return run_scan(n, num_tiles_hit, offsets, (int32_t*)workspace, as_stream(stream), g);
 }
 
 extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int32_t* tile_order, void* stream) {

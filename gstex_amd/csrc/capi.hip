@@ -32,3 +32,35 @@ int launch_status(const char* what) {
 extern "C" const char* gstex_last_error(void) { return gstex::g_last_error.c_str(); }
 
 extern "C" int gstex_abi_version(void) { return GSTEX_ABI_VERSION; }
+
+// Device-writable host words (ABI 13): the pair-capacity guard writes each render's pair total into one of them
+// (gstex_scan_offsets_guarded), the host reads it after the stream has passed the scan -- no copy, no sync.
+extern "C" int gstex_host_words_alloc(int32_t n, int32_t** host, int32_t** device) {
+    if (n <= 0 || !host || !device) {
+        gstex::set_error("gstex_host_words_alloc: invalid arguments");
+        return GSTEX_ERR_INVALID_ARG;
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, (size_t)n * sizeof(int32_t), hipHostMallocMapped) != hipSuccess || !p) {
+        gstex::set_error("gstex_host_words_alloc: hipHostMalloc failed");
+        return GSTEX_ERR_LAUNCH;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+        (void)hipHostFree(p);
+        gstex::set_error("gstex_host_words_alloc: hipHostGetDevicePointer failed");
+        return GSTEX_ERR_LAUNCH;
+    }
+    for (int32_t i = 0; i < n; ++i) static_cast<int32_t*>(p)[i] = 0;
+    *host = static_cast<int32_t*>(p);
+    *device = static_cast<int32_t*>(d);
+    return GSTEX_OK;
+}
+
+extern "C" int gstex_host_words_free(int32_t* host) {
+    if (host && hipHostFree(host) != hipSuccess) {
+        gstex::set_error("gstex_host_words_free: hipHostFree failed");
+        return GSTEX_ERR_LAUNCH;
+    }
+    return GSTEX_OK;
+}

@@ -56,12 +56,17 @@ class GradSync:
         # so the head (45 MB) lands first, the next step starts on it, and the tail (120 MB) only has to land by that
         # step's raster forward
         self.head_first = bool(getattr(trainer, "defer_texture", False))
+        # a trainer with a pair-capacity guard (GStexTrainer.step_control): its per-step overflow flags live in the
+        # first CTRL elements of the flat buffer, so the head collective sums them over the ranks and every rank's
+        # Adam launches skip the same steps
+        self._ctrl = hasattr(trainer, "step_control")
         self.rebuild()
 
     def _params(self):
         return self.trainer.parameters()
 
     ALIGN = 64  # elements
+    CTRL = 64  # elements in front of the parameters: the trainer's step_control ring (pair-capacity guard flags)
 
     @staticmethod
     def _layout(params):
@@ -76,12 +81,17 @@ class GradSync:
             self.trainer.wait_texture()  # a side-stream texel update may still read the old buffer
         # every slice starts on a 256-B boundary (the fused Adam's float4 path needs 16-B aligned gradients)
         offs = []
-        total = 0
+        total = self.CTRL if self._ctrl else 0
         for p in params:
             offs.append(total)
             total += -(-p.numel() // self.ALIGN) * self.ALIGN
         dev = params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
+        if self._ctrl:  # the flags of steps still in flight move with the buffer
+            ring = self.trainer.step_control
+            self.flat[:ring.numel()].copy_(ring)
+            self.trainer.step_control = self.flat[:ring.numel()]
+        self._z0 = self.CTRL if self._ctrl else 0  # zero() leaves the control block alone
         self._offs = offs
         for p, off in zip(params, offs):
             p.grad = self.flat[off:off + p.numel()].view_as(p)
@@ -136,9 +146,9 @@ class GradSync:
         if getattr(self.trainer, "texture_grad_zeroed_by_update", False):
             # the texel slice is zeroed by the trainer's texel Adam as it reads it (GSTEX_ADAM_ZERO_GRAD: a side-stream
             # or deferred update, async_texture / defer_texture); filling it here would race or pre-empt that update
-            self.flat[:self._tail_off].zero_()
+            self.flat[self._z0:self._tail_off].zero_()
         else:
-            self.flat.zero_()
+            self.flat[self._z0:].zero_()
 
     def all_reduce(self):
         """Average the flat gradient buffer over all ranks (the tail's collective may already be running).
@@ -222,6 +232,13 @@ class GradSync:
         self._reattach(params, skip_tail=True)
         head = dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         scale = 1.0 / self.world
+        if self._ctrl and not defer_tail:
+            # the step's guard flag is agreed only once the head (which carries it) has landed
+            work.wait()
+            head.wait()
+            step_tail(scale)
+            step_head(scale)
+            return None
         if defer_tail:
             head.wait()
             step_head(scale)

@@ -107,7 +107,8 @@ class GStexTrainer:
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
                  async_texture: bool = False, defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0,
-                 use_normal_loss: bool = False, defer_side_stream: bool | None = None):
+                 use_normal_loss: bool = False, defer_side_stream: bool | None = None,
+                 pair_capacity: bool | None = None):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -187,6 +188,17 @@ class GStexTrainer:
             defer_side_stream = os.environ.get("GSTEX_DEFER_SIDE", "0") != "0"
         self.defer_side = bool(defer_side_stream) and self.defer_texture
         self._tex_stream = torch.cuda.Stream(device=d) if (self.async_texture or self.defer_side) else None
+        # pair_capacity (not in the reference; fused Adam on a HIP device): the training renders size their pair
+        # buffers from an ops.PairCapacity instead of reading the pair total back to the host (gstex.py:1045-1052,
+        # 1127), so a step has no host synchronisation.  Each step's renders write an overflow flag into
+        # step_control[step % 8] (a device fp32 ring; gstex_amd.dist.GradSync replaces it by a slice of its flat
+        # buffer, all-reduced with the gradients) that every Adam launch of the step reads (skip on overflow).
+        # GSTEX_SYNC_PAIRS=1 restores the read-back.
+        if pair_capacity is None:
+            pair_capacity = os.environ.get("GSTEX_SYNC_PAIRS", "0") == "0"
+        self.pairs = ops.PairCapacity(d) if (pair_capacity and fused_adam and self.device.type == "cuda") else None
+        self.step_control = torch.zeros(8, device=d, dtype=torch.float32)
+        self.skipped_steps = []  # steps whose update the pair-capacity guard skipped (found by _poll_pairs)
         self._tex_ready = None
         self._tex_grad = None
         # the side-stream update's workgroup cap (GSTEX_TEX_ADAM_GRID; 0 = full grid).  Measured at cfg3: no cap, 512,
@@ -215,6 +227,23 @@ class GStexTrainer:
         backward accumulates (gstex_raster_fwd_zero).  Called by zero_grad() and by gstex_amd.dist.GradSync.zero(), so
         a gradient left by a backward whose step was skipped never leaks into the next step."""
         self._sink_fresh = True
+
+    def _skip_flag(self):
+        """The current step's guard flag (1-element view of step_control) for its Adam launches, or None."""
+        if self.pairs is None:
+            return None
+        k = self.step % 8
+        return self.step_control[k:k + 1]
+
+    def _poll_pairs(self):
+        """Pair totals of finished renders (non-blocking): grows the capacity, records skipped steps."""
+        if self.pairs is not None and self.pairs.poll():
+            import warnings
+
+            new = self.pairs.overflows[len(self.skipped_steps):]
+            self.skipped_steps.extend(new)
+            warnings.warn(f"GStexTrainer: the pair total of step(s) {new} exceeded the pair capacity; their updates "
+                          f"were skipped on the device and the capacity grew to {self.pairs.capacity}")
 
     def _run_pending_texture(self):
         fn, self._pending_tex = self._pending_tex, None
@@ -315,6 +344,10 @@ class GStexTrainer:
         # forward, so that the binning's placement and sort do not queue behind that wait
         pend = self._pending_tex is not None
         late = pend and self._pending_collective
+        guard = None
+        if self.pairs is not None and torch.is_grad_enabled():
+            self._poll_pairs()
+            guard = (self.pairs, self._skip_flag(), self._sink_fresh, self.step)
         side = pend and not late and self.defer_side
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
@@ -326,7 +359,8 @@ class GStexTrainer:
             on_texture_grad=self.texture_grad_ready,
             texture_ready=(self._run_pending_texture if late else self._wait_side_texture if side else self._tex_ready),
             before_pair_wait=(self._launch_pending_texture_side if side else
-                              self._run_pending_texture if pend and not late else None))
+                              self._run_pending_texture if pend and not late else None),
+            pair_guard=guard)
         self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
         if torch.is_grad_enabled():
             self._sink_fresh = False  # zeroed by this forward: further renders before the step accumulate on top
@@ -431,33 +465,36 @@ class GStexTrainer:
         and the 1 / world averaging rides in the fused update (GradSync.all_reduce_and_step); otherwise call
         sync.all_reduce() before this."""
         self._sink_fresh = True  # the next step's first render zeroes the texel-gradient sink
+        sf = self._skip_flag()  # this step's pair-capacity guard (None without pair_capacity)
         if self.defer_texture:
             self._run_pending_texture()  # (two steps without a render in between)
             tex = {id(self.texture_dc)}
             if sync is not None:
                 # the texel update in pieces, each as soon as its piece of the collective has landed (GradSync)
                 rng = (lambda s, lo, hi, first: self.optimizer.step_range(self.texture_dc, lo, hi, first,
-                                                                          grad_scale=s)) if self.fused_adam else None
+                                                                          grad_scale=s, skip_flag=sf)) \
+                    if self.fused_adam else None
                 self._pending_tex = sync.all_reduce_and_step(
-                    lambda s: self.optimizer.step(only=tex, grad_scale=s),
-                    lambda s: self.optimizer.step(skip=tex, grad_scale=s), defer_tail=True, step_tail_range=rng)
+                    lambda s: self.optimizer.step(only=tex, grad_scale=s, skip_flag=sf),
+                    lambda s: self.optimizer.step(skip=tex, grad_scale=s, skip_flag=sf), defer_tail=True,
+                    step_tail_range=rng)
                 self._pending_collective = True
             else:
-                self.optimizer.step(skip=tex)
-                self._pending_tex = lambda: self.optimizer.step(only=tex)
+                self._step(skip=tex, skip_flag=sf)
+                self._pending_tex = lambda: self._step(only=tex, skip_flag=sf)
                 self._pending_collective = False
             self.step += 1
             return
         if sync is not None and self.fused_adam and not self.async_texture:
             tex = {id(self.texture_dc)}
-            sync.all_reduce_and_step(lambda s: self.optimizer.step(only=tex, grad_scale=s),
-                                     lambda s: self.optimizer.step(skip=tex, grad_scale=s))
+            sync.all_reduce_and_step(lambda s: self.optimizer.step(only=tex, grad_scale=s, skip_flag=sf),
+                                     lambda s: self.optimizer.step(skip=tex, grad_scale=s, skip_flag=sf))
             self.step += 1
             return
         if sync is not None:
             sync.all_reduce()
         if not self.async_texture:
-            self.optimizer.step()
+            self._step(skip_flag=sf)
             self.step += 1
             return
         # the texel update on the side stream, after everything enqueued so far (the backward, and a GradSync
@@ -465,18 +502,25 @@ class GStexTrainer:
         main = torch.cuda.current_stream(self.device)
         self.wait_texture()  # (a step without a render in between)
         tex = {id(self.texture_dc)}
-        self.optimizer.step(skip=tex)
+        self._step(skip=tex, skip_flag=sf)
         # recorded after the other groups' update: that one runs alone at full bandwidth, and the texel update then
         # overlaps the next step's latency-bound kernels (preprocessing, binning) instead of contending with it
         grads_ready = torch.cuda.Event()
         grads_ready.record(main)
         self._tex_stream.wait_event(grads_ready)
         with torch.cuda.stream(self._tex_stream):
-            self.optimizer.step(only=tex, grid=self._tex_grid)
+            self.optimizer.step(only=tex, grid=self._tex_grid, skip_flag=sf)
             ev = torch.cuda.Event()
             ev.record(self._tex_stream)
         self._tex_ready = ev
         self.step += 1
+
+    def _step(self, **kw):
+        """optimizer.step with the fused optimizer's extensions (skip_flag is None without pair_capacity, which needs
+        the fused Adam)."""
+        if kw.get("skip_flag") is None:
+            kw.pop("skip_flag", None)
+        self.optimizer.step(**kw)
 
     def zero_grad(self, set_to_none: bool = True):
         """Optimizers.zero_grad_all (engine/optimizers.py): torch's default set_to_none=True, so backward

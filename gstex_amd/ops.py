@@ -7,6 +7,7 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import time
 from typing import NamedTuple, Tuple
@@ -327,6 +328,113 @@ def bin_finish(begun, centers, extents, depths, H: int, W: int, block_width: int
     return offsets, tile_ranges, sorted_ids, sorted_slots, order
 
 
+class PairCapacity:
+    """Read-back-free pair buffers for a training loop (ABI 13; replaces the per-render pair-count read-back of
+    gstex.py:1045-1052, 1127 -- a device-to-host copy and a wait on it -- with buffers sized from a capacity).
+
+    Every render's scan writes its pair total on the device (gstex_scan_offsets_guarded): into the step's guard flag
+    (1.0 when the total exceeds the capacity; the binning then leaves every tile empty and the guarded Adam skips the
+    step's update, gstex_adam_step_guarded) and into one of RING device-writable host words, which the host reads
+    only after the stream has passed that scan (an event query; no copy, no synchronisation).  The capacity starts
+    from one read-back of the first render's total (headroom x total + slack) and grows when a total comes back
+    above grow_at of it, so an overflow needs a jump of more than 1 / grow_at in the total within the few renders the
+    host runs ahead; one that happens anyway skips that step's update (parameters and moments untouched, the step
+    counters still advance, identically on every rank) and is recorded in `overflows`."""
+
+    RING = 8
+
+    def __init__(self, device, capacity: int = 0, headroom: float = 1.5, slack: int = 1 << 16, grow_at: float = 0.8):
+        self.device = torch.device(device)
+        self.capacity = int(capacity)
+        self.headroom, self.slack, self.grow_at = float(headroom), int(slack), float(grow_at)
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        call("gstex_host_words_alloc", self.RING, ctypes.byref(h), ctypes.byref(d))
+        self._host_ptr, self._dev_ptr = h.value, d.value
+        self._words = (ctypes.c_int32 * self.RING).from_address(self._host_ptr)
+        self._events = [None] * self.RING
+        self._caps = [0] * self.RING
+        self._tags = [None] * self.RING
+        self._k = 0
+        self.max_total = 0
+        self.last_total = None
+        self.overflows = []  # tags (trainer steps) of renders whose total exceeded the capacity
+
+    def __del__(self):
+        try:
+            if self._host_ptr:
+                for ev in self._events:
+                    if ev is not None:
+                        ev.synchronize()
+                _lib.load().gstex_host_words_free(self._host_ptr)
+                self._host_ptr = None
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
+
+    def _absorb(self, k):
+        total = int(self._words[k])
+        self._events[k] = None
+        self.last_total = total
+        self.max_total = max(self.max_total, total)
+        if total > self._caps[k]:
+            self.overflows.append(self._tags[k])
+        if total > self.grow_at * self.capacity:
+            self.capacity = max(self.capacity, int(self.headroom * total) + self.slack)
+
+    def poll(self):
+        """Read the totals of the renders the stream has passed (non-blocking); returns the number of overflows."""
+        before = len(self.overflows)
+        for k in range(self.RING):
+            ev = self._events[k]
+            if ev is not None and ev.query():
+                self._absorb(k)
+        return len(self.overflows) - before
+
+    def scan(self, nth: torch.Tensor, step_flag: torch.Tensor, first: bool, tag=None):
+        """The offsets scan of one render with the guard: -> (offsets (n+1,), capacity for this render)."""
+        n = nth.shape[0]
+        k = self._k % self.RING
+        if self._events[k] is not None:  # the host is RING renders ahead: wait for that one (normally long done)
+            self._events[k].synchronize()
+            self._absorb(k)
+        self._k += 1
+        offsets = torch.empty((n + 1,), device=nth.device, dtype=torch.int32)
+        ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=nth.device, dtype=torch.uint8)
+        first_use = self.capacity <= 0
+        cap = (1 << 62) if first_use else self.capacity
+        guard = _lib.GstexPairGuard(cap, ptr(step_flag), self._dev_ptr + 4 * k, 1 if first else 0)
+        call("gstex_scan_offsets_guarded", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), ctypes.byref(guard),
+             _stream(nth))
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(nth.device))
+        self._events[k], self._caps[k], self._tags[k] = ev, cap, tag
+        if first_use:  # the one read-back: the first render sizes the capacity
+            ev.synchronize()
+            self._absorb(k)
+            self.capacity = max(self.capacity, int(self.headroom * self.last_total) + self.slack)
+        return offsets, self.capacity
+
+
+def bin_capped(nth, offsets, capacity: int, centers, extents, depths, H: int, W: int, block_width: int = BLOCK_WIDTH):
+    """bin_finish without the host's pair count: buffers of `capacity` pairs, the total read on the device
+    (gstex_bin_sort_capped).  -> (offsets, tile_ranges, sorted_ids (capacity,), sorted_slots (capacity,), order)."""
+    n = nth.shape[0]
+    dev = nth.device
+    tiles_x = (W + block_width - 1) // block_width
+    tiles_y = (H + block_width - 1) // block_width
+    n_tiles = tiles_x * tiles_y
+    tile_ranges = torch.empty((n_tiles, 2), device=dev, dtype=torch.int32)
+    sorted_ids = torch.empty((capacity,), device=dev, dtype=torch.int32)
+    sorted_slots = torch.empty((capacity,), device=dev, dtype=torch.int32)
+    order = torch.empty((n_tiles,), device=dev, dtype=torch.int32)
+    bws = torch.empty((max(int(_lib.load().gstex_bin_workspace_size(n, capacity, n_tiles)), 1),), device=dev,
+                      dtype=torch.uint8)
+    keep = [t.detach().contiguous() for t in (centers, extents, depths)]
+    _launch("gstex_bin_sort_capped", n, capacity, ptr(keep[0]), ptr(keep[1]), ptr(keep[2]), ptr(nth), ptr(offsets),
+            int(H), int(W), int(block_width), ptr(tile_ranges), ptr(sorted_ids), ptr(sorted_slots), ptr(order),
+            ptr(bws), bws.numel(), _stream(nth))
+    return offsets, tile_ranges, sorted_ids, sorted_slots, order
+
+
 def bin_and_sort(centers, extents, depths, num_tiles_hit, H: int, W: int, block_width: int = BLOCK_WIDTH):
     """Tile binning + per-tile depth sort.  Returns (offsets (N+1,), tile_ranges (n_tiles,2),
     sorted_ids (I,), sorted_slots (I,)), all int32.  One host read of the pair count I to size the I-length
@@ -362,7 +470,7 @@ class _TextureGaussians(torch.autograd.Function):
                 scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                 block_width, settings, background, texture_transform=None, fold_aabb=False,
                 geometry_outputs=True, grad_enabled=True, texture_grad_sink=None, on_texture_grad=None,
-                texture_ready=None, binning=None, before_pair_wait=None, zero_sink=False):
+                texture_ready=None, binning=None, before_pair_wait=None, zero_sink=False, pair_guard=None):
         N, L, C = (int(v) for v in texture_info)
         _check(L == 1, f"texture_info[1] (texture layers) must be 1 (got {L})")
         _check(1 <= C <= 8, f"texture_info[2] (channels) must be in [1, 8] (got {C})")
@@ -394,7 +502,11 @@ class _TextureGaussians(torch.autograd.Function):
         # the pair count is read to the host once; work that does not depend on the tile lists is queued
         # between the copy and the wait, so the device runs it while the host waits and sizes the pair
         # buffers: the splat records and the zeroed texel-gradient buffer of the backward
-        begun = bin_begin(nth) if binning is None else None
+        capped = None
+        if binning is None and pair_guard is not None:  # capacity mode: no host read of the pair total
+            pcap, step_flag, first, tag = pair_guard
+            capped = pcap.scan(nth, step_flag, first, tag)
+        begun = bin_begin(nth) if binning is None and capped is None else None
         records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
              ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
@@ -416,7 +528,10 @@ class _TextureGaussians(torch.autograd.Function):
                 ctx.v_texture = torch.empty_like(texture)  # zeroed by the raster forward (gstex_raster_fwd_zero)
         if before_pair_wait is not None:
             before_pair_wait()  # caller's work for the device while the host waits for the pair count
-        if binning is None:
+        if capped is not None:
+            offsets, tile_ranges, sorted_ids, sorted_slots, order = bin_capped(
+                nth, capped[0], capped[1], centers_c.detach(), extents_c, depths_c, H, W, BLOCK_WIDTH)
+        elif binning is None:
             offsets, tile_ranges, sorted_ids, sorted_slots, order = bin_finish(
                 begun, centers_c.detach(), extents_c, depths_c, H, W, BLOCK_WIDTH, with_order=True)
         else:  # a previous call's binning of the same centres / extents / depths / num_tiles_hit (bin_gaussians)
@@ -563,14 +678,15 @@ class _TextureGaussians(torch.autograd.Function):
             v_centers = None  # already chained through the AABB centre into v_means / v_scales / v_quats
         return (None, None, v_centers, None, None, None, v_rgbs, v_opac, v_means, v_scales, None, v_quats, v_uv0,
                 None, None, v_texture, None, None, None, None, None, None, None, None, None, None, v_bg, None, None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_tiles_hit, rgbs, opacities, means,
                       scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat, c2w, fx, fy, cx, cy, H, W,
                       block_width, settings, background=None, use_torch_impl=False, texture_transform=None,
                       fold_aabb=False, geometry_outputs=True, texture_grad_sink=None, on_texture_grad=None,
-                      texture_ready=None, binning=None, before_pair_wait=None, zero_texture_grad_sink=False):
+                      texture_ready=None, binning=None, before_pair_wait=None, zero_texture_grad_sink=False,
+                      pair_guard=None):
     """Differentiable textured-2DGS rasterizer (gstex.py:1133-1162).
 
     texture_transform=(s, b) (not in the reference API; default None = as stored) makes the raster read
@@ -601,6 +717,12 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
     before the host waits for it -- work it enqueues keeps the device busy through that wait (GStexTrainer
     defer_texture: the previous step's texel update).
 
+    pair_guard (not in the reference API; training loops): (PairCapacity, step_flag, first, tag) -- capacity mode: the
+    pair buffers are sized from the PairCapacity and the pair total stays on the device (no read-back, no wait); the
+    render's guard writes 1.0 into step_flag (a 1-element device fp32 view; first=True overwrites it, else the larger
+    value is kept) when the total exceeds the capacity, in which case every output is the empty render's and the
+    optimizer step guarded by that flag does nothing (FusedAdam.step(skip_flag=...)).
+
     binning (not in the reference API): a Binning from bin_gaussians() on the same centers / extents / depths /
     num_tiles_hit tensors -- several renders of one geometry (the eval render's three calls, gstex.py:1165-1200)
     bin and sort once.
@@ -617,7 +739,8 @@ def texture_gaussians(texture_info, texture_dims, centers, extents, depths, num_
                                    opacities, means, scales, glob_scale, quats, uv0, umap, vmap, texture, viewmat,
                                    c2w, fx, fy, cx, cy, H, W, block_width, settings, background, texture_transform,
                                    fold_aabb, geometry_outputs, torch.is_grad_enabled(), texture_grad_sink,
-                                   on_texture_grad, texture_ready, binning, before_pair_wait, zero_texture_grad_sink)
+                                   on_texture_grad, texture_ready, binning, before_pair_wait, zero_texture_grad_sink,
+                                   pair_guard)
 
 
 class Binning(NamedTuple):

@@ -20,13 +20,16 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
 
     @torch.no_grad()
-    def step(self, closure=None, only=None, skip=None, zero_grad=False, grid=0, grad_scale=1.0):
+    def step(self, closure=None, only=None, skip=None, zero_grad=False, grid=0, grad_scale=1.0, skip_flag=None):
         """The Adam update.  Extensions (not in torch.optim.Adam): `only` / `skip` (sets of id(param)) restrict the
         update to / exclude a set of parameters (so one group can be launched on another stream), and `zero_grad` writes zeros over each
         gradient after reading it (gstex_adam_step_ex, GSTEX_ADAM_ZERO_GRAD); `grid` > 0 caps the launch's
         workgroups (GSTEX_ADAM_GRID: each loops over the chunks), leaving CUs to another stream; `grad_scale` in (0, 1]
         multiplies every gradient as it is read (gstex_adam_step_scaled: a data-parallel step's 1 / world, applied to the
-        all-reduced sums -- bit-identical to averaging the buffer first).  The launch goes to the current stream."""
+        all-reduced sums -- bit-identical to averaging the buffer first); `skip_flag` (a 1-element device fp32 tensor)
+        makes the launch a no-op on the device when the value is non-zero (gstex_adam_step_guarded: the pair-capacity
+        guard of the step's renders, ops.PairCapacity) -- the step counts still advance.  The launch goes to the
+        current stream."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -59,11 +62,11 @@ class FusedAdam(torch.optim.Optimizer):
                                             st["exp_avg_sq"].data_ptr(), p.numel(), step_size, bc2_sqrt)
                 key = (b1, b2, group["eps"], p.device)
                 batches.setdefault(key, []).append((desc, p))
-        self._launch(batches, zero_grad, grid, grad_scale)
+        self._launch(batches, zero_grad, grid, grad_scale, skip_flag)
         return loss
 
     @torch.no_grad()
-    def step_range(self, p, lo: int, hi: int, first: bool, zero_grad=False, grad_scale=1.0):
+    def step_range(self, p, lo: int, hi: int, first: bool, zero_grad=False, grad_scale=1.0, skip_flag=None):
         """The Adam update of elements [lo, hi) of parameter `p` only: the chunks of one step, launched one by one
         (e.g. each as soon as its slice of an all-reduce has landed, gstex_amd.dist.GradSync), together equal one
         step(only={id(p)}) bit for bit (the update is elementwise).  `first`: the chunk that advances the parameter's
@@ -92,16 +95,19 @@ class FusedAdam(torch.optim.Optimizer):
         o = 4 * lo
         desc = _lib.GstexAdamTensor(p.data_ptr() + o, g.data_ptr() + o, st["exp_avg"].data_ptr() + o,
                                     st["exp_avg_sq"].data_ptr() + o, hi - lo, step_size, bc2_sqrt)
-        self._launch({(b1, b2, group["eps"], p.device): [(desc, p)]}, zero_grad, 0, grad_scale)
+        self._launch({(b1, b2, group["eps"], p.device): [(desc, p)]}, zero_grad, 0, grad_scale, skip_flag)
 
-    def _launch(self, batches, zero_grad, grid, grad_scale):
+    def _launch(self, batches, zero_grad, grid, grad_scale, skip_flag=None):
         for (b1, b2, eps, dev), items in batches.items():
             st = _lib.stream_of(dev)
             for i in range(0, len(items), _lib.ADAM_MAX_TENSORS):
                 chunk = items[i:i + _lib.ADAM_MAX_TENSORS]
                 arr = (_lib.GstexAdamTensor * len(chunk))(*[d for d, _ in chunk])
                 flags = (_lib.ADAM_ZERO_GRAD if zero_grad else 0) | ((int(grid) & 0xFFFF) << _lib.ADAM_GRID_SHIFT)
-                if grad_scale != 1.0:
+                if skip_flag is not None:
+                    _lib.call("gstex_adam_step_guarded", len(chunk), arr, float(b1), float(b2), float(eps), flags,
+                              float(grad_scale), _lib.ptr(skip_flag), st)
+                elif grad_scale != 1.0:
                     _lib.call("gstex_adam_step_scaled", len(chunk), arr, float(b1), float(b2), float(eps), flags,
                               float(grad_scale), st)
                 elif flags:

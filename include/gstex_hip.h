@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 12
+#define GSTEX_ABI_VERSION 13
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -125,6 +125,39 @@ int gstex_bin_sort_ordered(int32_t n, int64_t n_isect, const float* centers, con
                            int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
                            int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order,
                            void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- read-back-free binning (ABI 13) -------------------------------------------------------
+ * The reference sizes its pair buffers from the pair total on the host (gstex.py:1045-1052, 1127: a device-to-host
+ * read and a stream synchronisation every render).  Capacity mode sizes them from a capacity instead and keeps the
+ * total on the device:
+ *   gstex_scan_offsets_guarded: gstex_scan_offsets, and the thread that writes the total offsets[n] also writes
+ *     *step_flag = (total > capacity) ? 1.0f : 0.0f (first != 0: the step's first render; otherwise the larger of
+ *     the two) and, when host_count != NULL, the total into host_count -- memory the device can write and the host
+ *     reads (pinned, mapped) once the stream has passed the scan: no copy, no synchronisation;
+ *   gstex_bin_sort_capped: gstex_bin_sort_ordered with n_isect = the capacity (buffers, workspace); the kernels read
+ *     the total from offsets[n], and a total above the capacity leaves every tile empty (nothing is written past the
+ *     buffers);
+ *   gstex_adam_step_guarded: gstex_adam_step_scaled that does nothing when *skip != 0 (an overflowed step's update
+ *     is skipped on the device; the host grows the capacity when it sees the total).
+ * The raster entry points take the capacity as n_isect (it only sizes the aux layout and the backward's grid, whose
+ * surplus units exit at once). */
+typedef struct gstex_pair_guard {
+    int64_t capacity;
+    float* step_flag;
+    int32_t* host_count; /* nullable */
+    int32_t first;
+} gstex_pair_guard;
+/* n device-writable host words (hipHostMalloc, mapped; zeroed): *host for the host, *device for
+ * gstex_pair_guard.host_count.  Freed with gstex_host_words_free(host). */
+int gstex_host_words_alloc(int32_t n, int32_t** host, int32_t** device);
+int gstex_host_words_free(int32_t* host);
+int gstex_scan_offsets_guarded(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
+                               size_t workspace_bytes, const gstex_pair_guard* guard, void* stream);
+int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* centers, const float* extents,
+                          const float* depths, const int32_t* num_tiles_hit, const int32_t* offsets,
+                          int32_t H, int32_t W, int32_t block, int32_t* tile_ranges, int32_t* sorted_ids,
+                          int32_t* sorted_slots, int32_t* tile_order, void* workspace, size_t workspace_bytes,
+                          void* stream);
 
 /* Largest-first launch order of the tiles: tile_order[n_tiles] lists the tiles by descending
  * pair count (ties by tile index).  Pass it to gstex_raster_fwd / gstex_texture_edit, whose
@@ -325,6 +358,11 @@ int gstex_adam_step_ex(int32_t n_tensors, const gstex_adam_tensor* tensors, doub
  * reference's DDP (pipelines/base_pipeline.py:281-283). */
 int gstex_adam_step_scaled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                            double eps, int32_t flags, float grad_scale, void* stream);
+/* gstex_adam_step_scaled that reads *skip (a device float, nullable = never) first and updates nothing when it is
+ * non-zero: the pair-capacity guard's step flag (gstex_scan_offsets_guarded), all-reduced with the gradients in
+ * data-parallel training so that every rank skips the same steps.  ABI 13. */
+int gstex_adam_step_guarded(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                            double eps, int32_t flags, float grad_scale, const float* skip, void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,18 +20,19 @@ scripts/train.py:97,138-144; DDP averaging, pipelines/base_pipeline.py:281-283).
 The check is on the GRADIENT each Adam launch consumes: every FusedAdam.step /
 step_range call of the data-parallel trainer is intercepted and the gradient it reads (times its grad_scale, i.e. the
 all-reduced mean gradient) is recorded per parameter group and step; rank 0 runs a single-rank reference trainer on
-the same `world` views per step (autograd sums them, the sum is scaled by 1/world) and records its Adam inputs the
-same way, and a second identical reference gives the run-to-run floor of the float-atomic sums.  Pass:
+the same `world` views per step (autograd sums them, the sum is scaled by 1/world) with its parameters set to the
+data-parallel trainer's before every step ("mirrored": each step compares gradients taken at identical parameters), and
+a second mirrored reference gives the run-to-run floor of the float-atomic sums.  Pass:
   * every group, every step: ||g_dist - g_ref|| / ||g_ref|| <= 1e-5 (and printed next to the floor
     ||g_ref2 - g_ref|| / ||g_ref||); a wrong 1/world factor, a dropped or doubled piece, or a stale sink shows up
     as an error of order 1;
   * with --deterministic (torch.use_deterministic_algorithms: splat-gradient rows summed in a fixed order)
-    at world 2, the splat groups of step 0 bit-exact (a + b == b + a; from step 1 on the float-atomic texel gradients
-    have moved the texels by run-to-run noise, which every later gradient inherits, so the floor is no longer 0);
+    at world 2, the splat groups bit-exact at every step (a + b == b + a);
   * every rank's parameters equal rank 0's bit for bit after the run.
-Parameters of rank 0 vs the reference are reported, not asserted for the texels: Adam (eps 1e-15) moves an element
-by ~lr whatever its gradient's size, so a texel whose gradient is float-atomic noise around zero differs by up to 2 lr
-per step between ANY two runs (shown for the worst texel: its per-step gradients next to the median |gradient|).
+Parameters of rank 0 vs a FREE-running single-rank reference (its own mean-gradient Adam steps) are reported, not
+asserted: Adam (eps 1e-15) moves an element by ~lr whatever its gradient's size, so a texel whose gradient is
+float-atomic noise around zero differs by up to 2 lr per step between ANY two runs (shown for the worst texel: its
+per-step gradients in both runs next to the median |gradient|) -- the mechanism behind round 3's geo4 "failure".
 Prints one line per check and `REHEARSAL OK world=N` at the end (exit status 0), else `REHEARSAL FAILED`.
 """
 import argparse
@@ -60,24 +61,41 @@ class AdamTap:
         def names():
             return {id(p): n for n, p in zip(trainer.param_groups(), trainer.parameters())}
 
-        def tap_step(closure=None, only=None, skip=None, zero_grad=False, grid=0, grad_scale=1.0):
+        def tap_step(closure=None, only=None, skip=None, grad_scale=1.0, **kw):
             nm = names()
             for p in trainer.parameters():
                 if p.grad is None or (only is not None and id(p) not in only) or (skip is not None and id(p) in skip):
                     continue
                 self.grads.setdefault(nm[id(p)], []).append((p.grad * grad_scale).detach().clone())
-            return step(closure=closure, only=only, skip=skip, zero_grad=zero_grad, grid=grid, grad_scale=grad_scale)
+            return step(closure=closure, only=only, skip=skip, grad_scale=grad_scale, **kw)
 
-        def tap_range(p, lo, hi, first, zero_grad=False, grad_scale=1.0):
+        def tap_range(p, lo, hi, first, grad_scale=1.0, **kw):
             name = names()[id(p)]
             if first:
                 self._piece[name] = torch.full_like(p.grad, float("nan"))
                 self.grads.setdefault(name, []).append(self._piece[name])
             self._piece[name].view(-1)[lo:hi] = p.grad.view(-1)[lo:hi] * grad_scale
-            return step_range(p, lo, hi, first, zero_grad=zero_grad, grad_scale=grad_scale)
+            return step_range(p, lo, hi, first, grad_scale=grad_scale, **kw)
 
         opt.step = tap_step
         opt.step_range = tap_range
+
+
+def mirror(ref, tr):
+    """Set reference trainer `ref` to `tr`'s parameters and charts (its own Adam state is never used)."""
+    with torch.no_grad():
+        if ref.texture_dc.shape != tr.texture_dc.shape:  # tr's texel store grew at a rechart
+            old = ref.texture_dc
+            ref.texture_dc = torch.nn.Parameter(tr.texture_dc.detach().clone())
+            for g in ref.optimizer.param_groups:
+                if g["name"] == "texture_dc":
+                    g["params"] = [ref.texture_dc]
+            ref.optimizer.state.pop(old, None)
+        ref.texture_dims = tr.texture_dims.clone()
+        ref.mappings.copy_(tr.mappings)
+        ref.n_texels = tr.n_texels
+        for p, q in zip(ref.parameters(), tr.parameters()):
+            p.copy_(q.detach())
 
 
 def rel(a, b):
@@ -123,8 +141,13 @@ def main():
     tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=args.defer_texture, **geo)
     sync = GradSync(tr, world)
     tap = AdamTap(tr)
+    # rank 0: two MIRRORED references (their parameters set to the data-parallel trainer's before each step's
+    # gradients, so every step compares gradients at identical inputs; the second one gives the float-atomic floor)
+    # and one FREE-running reference that steps its own Adam (the parameter-level report)
     refs = [GStexTrainer(sc, dev, start_step=3000, **geo) for _ in range(2)] if rank == 0 else []
-    taps = [AdamTap(r) for r in refs]
+    free = GStexTrainer(sc, dev, start_step=3000, **geo) if rank == 0 else None
+    ref_grads = [{} for _ in refs]
+    free_tap = AdamTap(free) if free is not None else None
 
     def say(msg):
         if rank == 0:
@@ -145,6 +168,10 @@ def main():
         if step == 1:
             tr.zero_grad()  # set_to_none after zero(): detached autograd .grad tensors, folded back by the exchange
         tr.forward_backward(views[pose], gts[pose])
+        # the parameters this step's gradients were taken at: the head groups as the last step left them, the texels
+        # after the deferred update the render above ran
+        for ref in refs:
+            mirror(ref, tr)
         # the tail's collective starts from the raster backward -- unless the exchange is head first (a deferring
         # trainer), where the step queues it behind the head's
         started = (sync._work is not None) != sync.head_first
@@ -158,19 +185,22 @@ def main():
             + ("queued behind the head's (head first)" if sync.head_first else "started from the raster backward")
             + f" on every rank: {flag}")
         ok &= flag
-        for ref in refs:
+        for ref, rg in zip(refs + ([free] if free is not None else []), ref_grads + [None]):
             ref.zero_grad()
             for r in range(world):
                 p = (r + step * world) % N_POSES
                 ref.forward_backward(views[p], gts[p])  # autograd accumulates the world gradients (sum)
-            for prm in ref.parameters():
+            for name, prm in zip(ref.param_groups(), ref.parameters()):
                 if prm.grad is not None:
-                    prm.grad.mul_(1.0 / world)
-            ref.optimizer_step()
+                    prm.grad.mul_(1.0 / world)  # the mean gradient
+                    if rg is not None:
+                        rg.setdefault(name, []).append(prm.grad.detach().clone())
+            if rg is None:
+                ref.optimizer_step()
         if step == 1:
             old = tr.texture_dc
             cap = old.shape[0]
-            for t in [tr] + refs:
+            for t in [tr] + ([free] if free is not None else []):
                 t.pixel_num = 1.3 * cap  # the new charts need more texels than the store holds: it grows
                 t.recharge()
             grew = tr.texture_dc is not old and tr.texture_dc.shape[0] > cap
@@ -187,7 +217,7 @@ def main():
     if rank == 0:
         say("gradient consumed by Adam, ||g_dist - g_ref|| / ||g_ref|| per step (floor: a second reference run):")
         for name in names:
-            gd, gr, g2 = tap.grads.get(name, []), taps[0].grads.get(name, []), taps[1].grads.get(name, [])
+            gd, gr, g2 = tap.grads.get(name, []), ref_grads[0].get(name, []), ref_grads[1].get(name, [])
             if not gr and not g2 and len(gd) == args.steps and all(float(t.abs().max()) == 0.0 for t in gd):
                 # a parameter no rank takes a gradient for (features_dc under SH colour, gstex.py:1100): its slice of the
                 # flat buffer is reduced as zeros (DDP's find_unused_parameters) and Adam's update of it is exactly 0
@@ -209,14 +239,12 @@ def main():
                     + " ".join(f"{f:.2e}" for f in floors))
             g_ok = max(errs) <= 1e-5
             if args.deterministic and world == 2 and name != "texture_dc":
-                # step 0 only: from step 1 on the texels (float-atomic gradients through Adam) differ run to run, and
-                # with them every later gradient -- the floor column shows the same for two single-rank runs
-                exact = bool(torch.equal(gd[0], gr[0]))
-                line += f"   step 0 bit-exact {exact}"
+                exact = all(bool(torch.equal(a, b)) for a, b in zip(gd, gr))
+                line += f"   bit-exact {exact}"
                 g_ok &= exact
             good &= g_ok
             say(line + ("" if g_ok else "   <-- FAIL"))
-        worst_tex = (tap.grads.get("texture_dc"), taps[0].grads.get("texture_dc"))
+        worst_tex = (tap.grads.get("texture_dc"), free_tap.grads.get("texture_dc"))
     ok &= agree(good)
 
     # 2. every rank equals rank 0 bit for bit; rank 0 vs the reference (reported; see the module docstring)
@@ -228,11 +256,11 @@ def main():
         ok &= same
         line = f"{name:14s} every rank == rank 0: {same}"
         if rank == 0:
-            rp = dict(zip(refs[0].param_groups(), refs[0].parameters()))[name].detach()
+            rp = dict(zip(free.param_groups(), free.parameters()))[name].detach()
             scale = max(float(rp.abs().max()), 1e-30)
             d = (r0 - rp).abs()
-            lr = refs[0].optimizer.param_groups[names.index(name)]["lr"]
-            line += f";  |rank0 - reference| max {float(d.max()) / scale:.2e}, mean {float(d.mean()) / scale:.2e} of max|p|"
+            lr = free.optimizer.param_groups[names.index(name)]["lr"]
+            line += f";  |rank0 - free-running reference| max {float(d.max()) / scale:.2e}, mean {float(d.mean()) / scale:.2e} of max|p|"
             line += f" (worst element {float(d.max()) / lr:.2f} lr)"
             if name == "texture_dc" and worst_tex is not None and worst_tex[0] is not None:
                 i = int(torch.argmax(d.reshape(-1)))

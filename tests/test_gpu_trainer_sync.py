@@ -262,3 +262,106 @@ def test_texture_sink_accumulates_the_renders_of_one_step():
     torch.cuda.synchronize()
     for (name, a), b in zip(plain.param_groups().items(), deferred.param_groups().values()):
         _assert_trains_alike(name, a[0], b[0], "texel sink over two renders")
+
+
+def test_pair_capacity_step_trains_like_the_readback_step():
+    """Capacity mode (ops.PairCapacity, the default): pair buffers sized from a capacity, the pair total kept on the
+    device -- must train like the reference's read-back sizing (pair_capacity=False), deferred texel update included,
+    across a growing rechart; and a step of it performs no host synchronisation (no .item() / .cpu() / pinned copy /
+    stream, event or device synchronisation; the pair totals are read later with non-blocking event queries)."""
+    from gstex_amd import ops
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    sc = make_scene(4000, 80_000, seed=21)
+    views = [sphere_view(i, 96, 96).to(dev) for i in range(3)]
+    g = torch.Generator().manual_seed(8)
+    gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(3)]
+    sync = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, pair_capacity=False)
+    capd = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+    assert sync.pairs is None and capd.pairs is not None
+    for step in range(5):
+        for tr in (sync, capd):
+            tr.zero_grad()
+            tr.forward_backward(views[step % 3], gts[step % 3])
+            tr.optimizer_step()
+        if step == 1:
+            for tr in (sync, capd):
+                tr.pixel_num = 1.3 * tr.texture_dc.shape[0]
+                tr.recharge()
+    # a step in capacity mode, with every host-synchronising call counted
+    calls = []
+
+    def spy(name, fn):
+        def w(*a, **k):
+            calls.append(name)
+            return fn(*a, **k)
+        return w
+
+    saved = {}
+    patch = [(torch.Tensor, n) for n in ("item", "cpu", "tolist", "numpy", "__bool__", "__float__", "__int__")]
+    patch += [(torch.cuda, "synchronize"), (torch.cuda.Stream, "synchronize"), (torch.cuda.Event, "synchronize"),
+              (ops, "_start_count"), (ops, "_finish_count")]
+    for obj, n in patch:
+        saved[(obj, n)] = getattr(obj, n)
+        setattr(obj, n, spy(n, saved[(obj, n)]))
+    try:
+        capd.zero_grad()
+        capd.forward_backward(views[0], gts[0])
+        capd.optimizer_step()
+    finally:
+        for (obj, n), fn in saved.items():
+            setattr(obj, n, fn)
+    assert calls == [], f"host synchronisation inside a capacity-mode step: {calls}"
+    sync.zero_grad()
+    sync.forward_backward(views[0], gts[0])
+    sync.optimizer_step()
+    for tr in (sync, capd):
+        tr.wait_texture()
+    torch.cuda.synchronize()
+    capd._poll_pairs()
+    assert capd.skipped_steps == [] and capd.pairs.max_total > 0
+    assert capd.pairs.capacity >= capd.pairs.max_total
+    for (name, a), b in zip(sync.param_groups().items(), capd.param_groups().values()):
+        _assert_trains_alike(name, a[0], b[0], "capacity-mode step")
+
+
+def test_pair_capacity_overflow_skips_the_update_and_grows():
+    """A capacity below the pair total: the render comes out empty, every Adam launch of the step (the deferred texel
+    update included) leaves parameters and moments untouched, the host finds the overflow from the totals it polls,
+    grows the capacity, and the next step trains."""
+    from gstex_amd import ops
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    sc = make_scene(3000, 60_000, seed=22)
+    view = sphere_view(0, 96, 96).to(dev)
+    gt = torch.rand((96, 96, 3), generator=torch.Generator().manual_seed(9)).to(dev)
+    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+    tr.pairs = ops.PairCapacity(dev, capacity=1000)  # far below this scene's ~20k pairs
+    before = [p.detach().clone() for p in tr.parameters()]
+    tr.zero_grad()
+    out = tr.render(view)
+    assert float(out["alpha"].abs().max()) == 0.0  # every tile empty
+    tr.zero_grad()
+    tr.forward_backward(view, gt)
+    tr.optimizer_step()
+    tr.wait_texture()
+    torch.cuda.synchronize()
+    for p, q in zip(before, tr.parameters()):
+        assert torch.equal(p, q.detach()), "an overflowed step changed a parameter"
+    for st in tr.optimizer.state.values():
+        assert float(st["exp_avg"].abs().max()) == 0.0 and float(st["exp_avg_sq"].abs().max()) == 0.0
+    with pytest.warns(UserWarning, match="exceeded the pair capacity"):
+        tr._poll_pairs()
+    assert tr.skipped_steps == [3000, 3000] and tr.pairs.capacity > tr.pairs.max_total > 1000
+    tr.zero_grad()
+    tr.forward_backward(view, gt)
+    tr.optimizer_step()
+    tr.wait_texture()
+    torch.cuda.synchronize()
+    tr._poll_pairs()
+    assert tr.skipped_steps == [3000, 3000]
+    assert any(not torch.equal(p, q.detach()) for p, q in zip(before, tr.parameters()))
