@@ -101,6 +101,10 @@ SIGNATURES = {
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
     ),
+    "gstex_raster_setup_hp": (
+        c_int32,
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P],
+    ),
     "gstex_raster_fwd": (
         c_int32,
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
@@ -119,6 +123,11 @@ SIGNATURES = {
         c_int32,
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, _P, _P, _P],
+    ),
+    "gstex_raster_bwd_hp": (
+        c_int32,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+         c_int64, _P, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_setup_bwd": (
         c_int32,

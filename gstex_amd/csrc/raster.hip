@@ -135,6 +135,22 @@ constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in
                         // (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
+// Near-edge-on splats (|normal . view direction| < kHpCos at the centre): (u, v) = p.xy / p.z is ill-conditioned in
+// the stored fp32 A, B, Pz -- their rounding alone left the means / quats gradients at ~5e-5.  For
+// those splats setup also writes A, B, Pz and the anchor in fp64 (GSTEX_HP_DOUBLES per splat, rec_hp) and flags the
+// record (bit 31 of R_OFF); the backward re-evaluates dx, dy, 1 / p.z, u, v from them in fp64 for the gradient
+// arithmetic, while every pair decision (alpha, depth, branch) stays the forward's fp32 one.  Measured on the cfg3
+// 96x96 window with the oracle (tools/grad_precision.py --hp-cos): 1.7 % of the splats at 0.02, 4.3 % at 0.05;
+// means / quats 4.9e-5 / 4.3e-5 -> 2.3e-6 / 1.9e-6 at 0.05.
+#ifndef GSTEX_HP
+#define GSTEX_HP 1  // 0: the backward ignores rec_hp (A/B builds)
+#endif
+#ifndef GSTEX_HP_COS
+#define GSTEX_HP_COS 0.05
+#endif
+constexpr double kHpCos = GSTEX_HP_COS;
+constexpr int kHpDoubles = 10;  // A.xyz, B.xyz, Pz, xa, ya, (pad)
+constexpr unsigned kHpFlag = 0x80000000u;
 constexpr int kRowStride = GSTEX_PARTIAL_FLOATS;  // 32 floats between partial rows
 
 // ------------------------------------------------------------------------------------------
@@ -151,7 +167,7 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
                                                     const float* __restrict__ vmap,
                                                     const int32_t* __restrict__ tdims,
                                                     const int32_t* __restrict__ nth, CamArgs cam_args,
-                                                    float* __restrict__ rec_out) {
+                                                    float* __restrict__ rec_out, double* __restrict__ rec_hp) {
     const Camera cam = load_camera(cam_args);
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
@@ -184,7 +200,16 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     r[R_AVV] = (float)(sv * dot3(fr.tv, vm));
     r[R_H] = __int_as_float(tdims[3 * g]);
     r[R_W] = __int_as_float(tdims[3 * g + 1]);
-    r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
+    // near-edge-on: the fp64 pair-evaluation inputs for the backward, and the flag
+    const double dn = sqrt(dot3(dir, dir));
+    const bool hp = rec_hp && dn > 0.0 && fabs(dot3(fr.tw, dir)) < kHpCos * dn;
+    r[R_OFF] = __uint_as_float((uint32_t)tdims[3 * g + 2] | (hp ? kHpFlag : 0u));
+    if (hp) {
+        double* q = rec_hp + (size_t)g * kHpDoubles;
+        q[0] = ah.A.x; q[1] = ah.A.y; q[2] = ah.A.z;
+        q[3] = ah.B.x; q[4] = ah.B.y; q[5] = ah.B.z;
+        q[6] = ah.Pz; q[7] = h.xa; q[8] = h.ya; q[9] = 0.0;
+    }
     r[R_XA] = (float)h.xa;
     r[R_YA] = (float)h.ya;
     r[R_HF] = (float)tdims[3 * g];
@@ -204,6 +229,7 @@ struct Rec {
     float rgb[3], nrm[3];
     float tu0, auu, auv, tv0, avu, avv;
     int h, w, off;
+    bool hp;  // near-edge-on: fp64 inputs in rec_hp for the backward (bit 31 of R_OFF)
     float xa, ya;
     float hf, wf;  // (float)h, (float)w
 };
@@ -222,7 +248,8 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.opac = v[R_OPAC];
     r.rgb[0] = v[R_RGB]; r.rgb[1] = v[R_RGB + 1]; r.rgb[2] = v[R_RGB + 2];
     r.tu0 = v[R_TU0]; r.auu = v[R_AUU]; r.auv = v[R_AUV]; r.tv0 = v[R_TV0]; r.avu = v[R_AVU]; r.avv = v[R_AVV];
-    r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = __float_as_int(v[R_OFF]);
+    r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = (int)(__float_as_uint(v[R_OFF]) & ~kHpFlag);
+    r.hp = (__float_as_uint(v[R_OFF]) & kHpFlag) != 0u;
     r.xa = v[R_XA]; r.ya = v[R_YA];
     r.nrm[0] = v[R_NRM]; r.nrm[1] = v[R_NRM + 1]; r.nrm[2] = v[R_NRM + 2];
     r.hf = v[R_HF]; r.wf = v[R_WF];
@@ -1141,6 +1168,16 @@ __device__ __forceinline__ void stage_add(float* a, float y) { atomicAdd(a, y); 
 #define GSTEX_FLUSH_U 4
 #endif
 constexpr int kFlushU = GSTEX_FLUSH_U;  // staging entries per lane per flush pass
+#ifndef GSTEX_TAIL_MIRROR
+#define GSTEX_TAIL_MIRROR 1
+#endif
+// Run tails of neighbouring half rows usually share their bilinear cell (a texel spans ~3 pixels at cfg3), and same-
+// address LDS atomics of one instruction serialise like bank conflicts.  So the corner order of the four staged adds
+// is mirrored per half row: the half rows of a pixel row alternate the column order (lane bit 2), the pixel rows
+// alternate the row order (lane bit 3), and four tails that share a cell add into four different texels in each
+// instruction.  The mirror is uniform inside a scan segment (a half row), so it is applied to the bilinear factors
+// before the scan (swapped operands, identical products) and to the corner addresses at the tails.
+constexpr bool kTailMirror = GSTEX_TAIL_MIRROR;
 static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging area");
 
 
@@ -1152,7 +1189,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
-    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux) {
+    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux,
+    const double* __restrict__ rec_hp) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
@@ -1280,6 +1318,24 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
+            if (GSTEX_HP && r.hp && rec_hp) {
+                // a near-edge-on splat (wave-uniform): the gradient's inputs dx, dy, 1 / p.z, u, v from its fp64
+                // homography; the decisions above (alpha, depth, branch) stay the forward's fp32 ones
+                // read through vector loads (a lane-varying zero offset): nine scalar-loaded doubles would spill
+                // the scalar register file of this 94-SGPR kernel
+                int vz;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+                const double* q = rec_hp + (size_t)gid * kHpDoubles + vz;
+                const double dx = (double)px - q[7], dy = (double)py - q[8];
+                const double qx = __builtin_fma(dx, q[0], dy * q[3]), qy = __builtin_fma(dx, q[1], dy * q[4]);
+                const double qz = __builtin_fma(dy, q[5], __builtin_fma(dx, q[2], q[6]));
+                const double iq = 1.0 / qz;
+                h.dx = (float)dx;
+                h.dy = (float)dy;
+                h.ipz = (float)iq;
+                h.u = (float)(qx * iq);
+                h.v = (float)(qy * iq);
+            }
             GSTEX_STAT(1, 1);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
@@ -1495,8 +1551,13 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 float tg[4 * CM];
                 {
 #pragma clang fp contract(fast)
-                    const float w00 = (1.0f - tax) * (1.0f - tay), w01 = (1.0f - tax) * tay;
-                    const float w10 = tax * (1.0f - tay), w11 = tax * tay;
+                    // row / column factors of the slot order (kTailMirror: swapped in mirrored half rows)
+                    const bool mi = kTailMirror && (lane & 8), mj = kTailMirror && (lane & 4);
+                    const float ax0 = 1.0f - tax, ay0 = 1.0f - tay;
+                    const float fi0 = mi ? tax : ax0, fi1 = mi ? ax0 : tax;
+                    const float fj0 = mj ? tay : ay0, fj1 = mj ? ay0 : tay;
+                    const float w00 = fi0 * fj0, w01 = fi0 * fj1;
+                    const float w10 = fi1 * fj0, w11 = fi1 * fj1;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) {
                         const float gt = (c < Cn) ? twq * Gtex[c] : 0.0f;
@@ -1516,8 +1577,21 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
                 } else if (tail) {
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
-                    const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
-                    const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
+                    int c00, c01, c10, c11;
+                    if (kTailMirror) {  // slot (p, q) = corner (p ^ mi, q ^ mj)
+                        const int di = tdi * r.w, dj = tdj;
+                        const int b = t0 + ((lane & 8) ? di : 0) + ((lane & 4) ? dj : 0);
+                        const int si = (lane & 8) ? -di : di, sj = (lane & 4) ? -dj : dj;
+                        c00 = b * Cn;
+                        c01 = (b + sj) * Cn;
+                        c10 = (b + si) * Cn;
+                        c11 = (b + si + sj) * Cn;
+                    } else {
+                        c00 = t0 * Cn;
+                        c01 = (t0 + tdj) * Cn;
+                        c10 = (t0 + tdi * r.w) * Cn;
+                        c11 = (t0 + tdi * r.w + tdj) * Cn;
+                    }
                     if (staged) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
@@ -1924,6 +1998,15 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
                                   const float* centers, const float* uv0, const float* umap, const float* vmap,
                                   const int32_t* texture_dims, const int32_t* num_tiles_hit,
                                   const gstex_camera* cam, float* records, void* stream) {
+    return gstex_raster_setup_hp(n, means, scales, glob_scale, quats, rgbs, opacities, centers, uv0, umap, vmap,
+                                 texture_dims, num_tiles_hit, cam, records, nullptr, stream);
+}
+
+extern "C" int gstex_raster_setup_hp(int32_t n, const float* means, const float* scales, float glob_scale,
+                                     const float* quats, const float* rgbs, const float* opacities,
+                                     const float* centers, const float* uv0, const float* umap, const float* vmap,
+                                     const int32_t* texture_dims, const int32_t* num_tiles_hit,
+                                     const gstex_camera* cam, float* records, double* rec_hp, void* stream) {
     GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup: invalid arguments");
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(means && scales && quats && rgbs && opacities && centers && uv0 && umap && vmap &&
@@ -1931,7 +2014,7 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
                   "gstex_raster_setup: null pointer");
     setup_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, means, scales, glob_scale, quats, rgbs, opacities,
                                                                  centers, uv0, umap, vmap, texture_dims,
-                                                                 num_tiles_hit, to_device_camera(*cam), records);
+                                                                 num_tiles_hit, to_device_camera(*cam), records, rec_hp);
     return launch_status("gstex_raster_setup");
 }
 
@@ -2013,6 +2096,19 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
                                 float* v_texture, void* aux, void* stream) {
+    return gstex_raster_bwd_hp(cam, channels, settings, background, records, tile_ranges, sorted_ids, sorted_slots,
+                               texture, n_texels, tex_scale, tex_bias, state, v_img, v_depth, v_reg, v_alpha, v_tex,
+                               v_normal, n_isect, partials, row_flags, v_texture, aux, nullptr, stream);
+}
+
+extern "C" int gstex_raster_bwd_hp(const gstex_camera* cam, int32_t channels, int32_t settings,
+                                   const float* background, const float* records, const int32_t* tile_ranges,
+                                   const int32_t* sorted_ids, const int32_t* sorted_slots,
+                                   const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
+                                   const float* state, const float* v_img,
+                                   const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
+                                   const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
+                                   float* v_texture, void* aux, const double* rec_hp, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
@@ -2045,7 +2141,8 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     raster_bwd_kernel<CC, GG><<<(unsigned)al.n_units, 64, 0, st>>>(                                            \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
-        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap)
+        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap,      \
+        rec_hp)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
     else if (channels == 3) GSTEX_BWD(3, true);
     else if (channels == 6 && !geo) GSTEX_BWD(6, false);

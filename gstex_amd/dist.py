@@ -60,6 +60,10 @@ class GradSync:
         # first CTRL elements of the flat buffer, so the head collective sums them over the ranks and every rank's
         # Adam launches skip the same steps
         self._ctrl = hasattr(trainer, "step_control")
+        # phase timing (bench.py at N > 1): when a dict, HIP events recorded on the compute stream as the head's
+        # ("head") and the whole tail's ("tail") collectives land -- with the raster kernels' own events they give
+        # the exposed exchange time per step
+        self.phase_events = None
         self.rebuild()
 
     def _params(self):
@@ -206,16 +210,20 @@ class GradSync:
                                      group=self.group, async_op=True) for lo, hi in bounds]
             scale = 1.0 / self.world
             head.wait()
+            self._mark("head")
             step_head(scale)
 
             def tail_step():
                 if step_tail_range is None:
                     tails[0].wait()
+                    self._mark("tail")
                     step_tail(scale)
                     return
                 # each piece stepped as soon as it has landed, while the next ones are still on the wire
                 for i, ((lo, hi), w) in enumerate(zip(bounds, tails)):
                     w.wait()
+                    if i == len(tails) - 1:
+                        self._mark("tail")
                     step_tail_range(scale, lo, hi, i == 0)
             return tail_step
         if work is None or self._layout(params) != self._key:
@@ -235,23 +243,36 @@ class GradSync:
         if self._ctrl and not defer_tail:
             # the step's guard flag is agreed only once the head (which carries it) has landed
             work.wait()
+            self._mark("tail")
             head.wait()
+            self._mark("head")
             step_tail(scale)
             step_head(scale)
             return None
         if defer_tail:
             head.wait()
+            self._mark("head")
             step_head(scale)
 
             def tail():
                 work.wait()
+                self._mark("tail")
                 step_tail(scale)
             return tail
         work.wait()
+        self._mark("tail")
         step_tail(scale)
         head.wait()
+        self._mark("head")
         step_head(scale)
         return None
+
+    def _mark(self, phase):
+        """A timing event on the current stream (phase_events enabled): the point a collective has landed at."""
+        if self.phase_events is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.phase_events.setdefault(phase, []).append(ev)
 
     def _reattach(self, params, skip_tail=False):
         """Point every .grad back at its slice of `flat`, copying a detached gradient in (None: zero, except the

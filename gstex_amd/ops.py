@@ -25,7 +25,8 @@ BLOCK_WIDTH = 16
 _TIMING: dict | None = None
 
 
-_TIMED = {"gstex_raster_fwd", "gstex_raster_bwd"}  # the roofline kernels; each event pair costs ~3 us of stream time
+_TIMED = {"gstex_raster_fwd", "gstex_raster_bwd"}
+HP_DOUBLES = 10  # raster.hip kHpDoubles  # the roofline kernels; each event pair costs ~3 us of stream time
 
 
 def set_kernel_timing(enabled: bool, names=None) -> None:
@@ -45,8 +46,14 @@ def kernel_times() -> dict:
     return {k: [a.elapsed_time(b) for a, b in v] for k, v in _TIMING.items()}
 
 
+def _TIMING_EVENTS(name: str) -> list:
+    """The (start, end) HIP event pairs recorded for `name` since set_kernel_timing(True) (no synchronisation)."""
+    return list((_TIMING or {}).get(name, []))
+
+
 def _launch(name: str, *args) -> None:
-    key = name[:-len("_zero")] if name.endswith("_zero") else name  # gstex_raster_fwd_zero times as the forward
+    # gstex_raster_fwd_zero times as the forward, gstex_raster_bwd_hp as the backward
+    key = name[:-len("_zero")] if name.endswith("_zero") else name[:-len("_hp")] if name.endswith("_hp") else name
     if _TIMING is None or key not in _TIMED:
         call(name, *args)
         return
@@ -508,12 +515,16 @@ class _TextureGaussians(torch.autograd.Function):
             capped = pcap.scan(nth, step_flag, first, tag)
         begun = bin_begin(nth) if binning is None and capped is None else None
         records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
-        _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
-             ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records),
-             st)
         # backward-only buffers only when a backward can follow: not under torch.no_grad() (eval renders of
         # trainable parameters), where apply() records no graph whatever the inputs' requires_grad
         needs_bwd = bool(grad_enabled) and any(ctx.needs_input_grad)
+        # the near-edge-on splats' fp64 pair-evaluation inputs for the backward (gstex_raster_setup_hp; rows written
+        # only for the flagged splats)
+        rec_hp = torch.empty((n, HP_DOUBLES), device=dev, dtype=torch.float64) if needs_bwd else None
+        _launch("gstex_raster_setup_hp", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
+                ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam,
+                ptr(records), ptr(rec_hp), st)
+        ctx.rec_hp = rec_hp
         ctx.v_texture = None
         ctx.sink = texture_grad_sink is not None
         ctx.on_texture_grad = on_texture_grad
@@ -651,11 +662,13 @@ class _TextureGaussians(torch.autograd.Function):
             settings_b = int(settings) | _lib.BWD_ORDERED
         else:
             settings_b = settings
-        _launch("gstex_raster_bwd", cam, C, settings_b, ptr(bg), ptr(records), ptr(tile_ranges),
+        _launch("gstex_raster_bwd_hp", cam, C, settings_b, ptr(bg), ptr(records), ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
-                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)
+                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux),
+                ptr(ctx.rec_hp), st)
         ctx.aux = None
+        ctx.rec_hp = None
         if ctx.sink:
             if ctx.on_texture_grad is not None:
                 ctx.on_texture_grad()  # the texel gradient is complete in stream order

@@ -174,6 +174,15 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
                        const float* vmap, const int32_t* texture_dims,
                        const int32_t* num_tiles_hit, const gstex_camera* cam, float* records,
                        void* stream);
+/* gstex_raster_setup that also writes, for every near-edge-on splat (|normal . view direction| < 0.05 at its
+ * centre), the fp64 inputs of its pair evaluation into rec_hp[n][10] (A.xyz, B.xyz, Pz, anchor x, y; caller-owned,
+ * only flagged rows written) and flags its record; gstex_raster_bwd_hp then takes that splat's gradient inputs (dx,
+ * dy, 1 / p.z, u, v) from them, fp64-evaluated, with the pair decisions unchanged.  ABI 13. */
+int gstex_raster_setup_hp(int32_t n, const float* means, const float* scales, float glob_scale,
+                          const float* quats, const float* rgbs, const float* opacities, const float* centers,
+                          const float* uv0, const float* umap, const float* vmap, const int32_t* texture_dims,
+                          const int32_t* num_tiles_hit, const gstex_camera* cam, float* records, double* rec_hp,
+                          void* stream);
 /* Texel values: the texels are read as tex_scale * texture + tex_bias (1, 0 = as stored), so a caller
  * that keeps SH-DC coefficients (gstex.py:1119 passes SH2RGB(texture_dc) = 0.28209 x + 0.5) can pass the
  * store itself; the backward's v_texture is then the gradient w.r.t. the stored values. */
@@ -234,6 +243,14 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const float* v_img, const float* v_depth, const float* v_reg, const float* v_alpha,
                      const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
                      uint32_t* row_flags, float* v_texture, void* aux, void* stream);
+/* gstex_raster_bwd with the near-edge-on splats' fp64 inputs from gstex_raster_setup_hp (rec_hp; NULL = none). */
+int gstex_raster_bwd_hp(const gstex_camera* cam, int32_t channels, int32_t settings, const float* background,
+                        const float* records, const int32_t* tile_ranges, const int32_t* sorted_ids,
+                        const int32_t* sorted_slots, const float* texture, int64_t n_texels, float tex_scale,
+                        float tex_bias, const float* state, const float* v_img, const float* v_depth,
+                        const float* v_reg, const float* v_alpha, const float* v_tex, const float* v_normal,
+                        int64_t n_isect, float* partials, uint32_t* row_flags, float* v_texture, void* aux,
+                        const double* rec_hp, void* stream);
 /* The backward's unit launch order alone (ABI 12): computed from the forward's aux (its per-unit costs and
  * histogram) into the same aux; a gstex_raster_bwd whose settings carry GSTEX_BWD_ORDERED then skips it.  Lets
  * the ordering run on another stream between the forward and the backward. */

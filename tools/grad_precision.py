@@ -10,7 +10,9 @@ gradient's norm-wise and max relative error against the all-fp64 evaluation:
   table32     table fp32, per-pair fp64;
 With the fp64 record (default) "table32" means the fp64 record rounded to fp32, so pair64/table32 isolates the
 rounding of the stored record: exact arithmetic everywhere else -- the conditioning floor of an fp32 record.
-Test infrastructure only (imports oracle/).  Usage: python tools/grad_precision.py [--win 48] [--cfg 3]
+  hp<c        --hp-cos c: as pair64/table32, but the table of the near-edge-on splats (|normal . view| < c) kept fp64
+              (raster.hip's GSTEX_HP_COS path)
+Test infrastructure only (imports oracle/).  Usage: python tools/grad_precision.py [--win 48] [--cfg 3] [--hp-cos 0.05]
 """
 import argparse
 import os
@@ -45,12 +47,49 @@ def grads(case, pair_dtype, table_dtype, outputs):
     return out
 
 
+def hp_mask_table(case, thr):
+    """Precision analysis of raster.hip's near-edge-on path (GSTEX_HP_COS): in the gradient pass, the per-splat table of
+    the splats with |normal . view direction| < thr stays fp64 while the others are rounded to fp32 -- what
+    gstex_raster_setup_hp / gstex_raster_bwd_hp do (fp64 dx, dy, 1 / p.z, u, v for those splats).  Returns a restore
+    function (patches the oracle; decisions stay the fp32 pass's)."""
+    inp = case.inp
+    with torch.no_grad():
+        _, _, tw = O.quat_frame(inp.quats.double())
+        _, cp, *_ = inp.cam.cast(F64)
+        d = cp[None] - inp.means.double()
+        mask = O._dot3(tw, d / d.norm(dim=-1, keepdim=True)).abs() < thr
+    orig_table, orig_render = O._splat_table, O._render
+    state = {"grad": False}
+
+    def render(inp_, dtype, tr, si, decisions, edit=None, table_dtype=None):
+        state["grad"] = table_dtype is not None
+        try:
+            return orig_render(inp_, dtype, tr, si, decisions, edit=edit, table_dtype=table_dtype)
+        finally:
+            state["grad"] = False
+
+    def table(inp_, dtype):
+        if dtype != F32 or not state["grad"]:
+            return orig_table(inp_, dtype)
+        t64 = orig_table(inp_, F64)
+        return {k: (torch.where(mask.view(-1, *([1] * (v.dim() - 1))), v, v.float().double()) if v.is_floating_point()
+                    else v) for k, v in t64.items()}
+
+    O._splat_table, O._render = table, render
+
+    def restore():
+        O._splat_table, O._render = orig_table, orig_render
+    return float(mask.double().mean()), restore
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--win", type=int, default=48)
     ap.add_argument("--cfg", type=int, default=3)
     ap.add_argument("--all-outputs", action="store_true")
     ap.add_argument("--fp32-record", action="store_true", help="all-fp32 per-splat record (round-2 formulation)")
+    ap.add_argument("--hp-cos", type=float, nargs="*", default=[],
+                    help="also: the table of splats with |normal . view dir| < each value kept fp64 (raster.hip GSTEX_HP_COS)")
     args = ap.parse_args()
     O.RECORD_FP64 = not args.fp32_record
     n, t = (200_000, 1e7) if args.cfg == 3 else (50_000, 1e6)
@@ -66,6 +105,12 @@ def main():
         for k in DIFF:
             cells.append(f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}")
         print(f"{name:16s} " + " ".join(f"{c:>18s}" for c in cells))
+    for thr in args.hp_cos:
+        frac, restore = hp_mask_table(case, thr)
+        g = grads(case, F64, F32, outputs)
+        restore()
+        cells = [f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}" for k in DIFF]
+        print(f"{'hp<' + str(thr) + f' ({100 * frac:.1f}%)':16s} " + " ".join(f"{c:>18s}" for c in cells))
     print("(norm-wise / max-element relative error vs all-fp64)")
 
 
