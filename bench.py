@@ -315,6 +315,8 @@ def main():
     base_mb = torch.cuda.memory_allocated(dev) / 2**20  # parameters, Adam state, scene, views, targets
     torch.cuda.reset_peak_memory_stats(dev)
     ops.set_kernel_timing(not args.no_kernel_timing)
+    if sync is not None and not args.no_kernel_timing:
+        sync.phase_events = {}  # when the head / tail collectives land, on rank 0's compute stream
     step_ev = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -330,6 +332,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20
+    raster_ev = {n: ops._TIMING_EVENTS(n) for n in ("gstex_raster_fwd", "gstex_raster_bwd")}
     kt = ops.kernel_times()
     ops.set_kernel_timing(False)
     step_ms = _events_ms(step_ev)
@@ -365,6 +368,25 @@ def main():
             roofline["valu_insts_per_launch"] = int(prow["valu_insts"])
             roofline["valu_issue_frac"] = round(prow["valu_insts"] / (dom_ms * 1e-3 * 1024 * 2.4e9 / 2), 4)
 
+    exchange = None
+    if sync is not None and sync.phase_events and kt.get("gstex_raster_bwd") and kt.get("gstex_raster_fwd"):
+        # per step k: raster bwd end -> head landed -> tail landed (in step k+1's render) -> next raster fwd start
+        pe = sync.phase_events
+        bwd, fwd = raster_ev["gstex_raster_bwd"], raster_ev["gstex_raster_fwd"]
+        rows = []
+        for k in range(min(len(bwd), len(pe.get("head", [])), len(pe.get("tail", [])))):
+            if k + 1 >= len(fwd):
+                break
+            b_end = bwd[k][1]
+            rows.append((b_end.elapsed_time(pe["head"][k]), b_end.elapsed_time(pe["tail"][k]),
+                         b_end.elapsed_time(fwd[k + 1][0])))
+        if rows:
+            med = [round(statistics.median(r[i] for r in rows), 4) for i in range(3)]
+            exchange = dict(bytes=int(sync.nbytes), steps=len(rows), bwd_end_to_head_landed_ms=med[0],
+                            bwd_end_to_tail_landed_ms=med[1], bwd_end_to_next_fwd_ms=med[2],
+                            note="rank 0 HIP events, medians over the timed steps; the exchange's exposed time is "
+                                 "bwd_end_to_next_fwd_ms minus the one-GPU gap (DESIGN.md §6)")
+        sync.phase_events = None
     sub = None
     if rank == 0 and world == 1 and not args.no_sub:
         sub = {}
@@ -468,6 +490,7 @@ def main():
         "kernel_ms_median": {k.replace("gstex_", ""): round(v, 4) for k, v in med.items()},
         "counts": {k: int(ab[k]) for k in ("N_v", "I", "T_v", "P")},
         "sub": sub,
+        "exchange": exchange,
         "setup_s": round(setup_s, 1),
     }
     print(json.dumps(line), flush=True)

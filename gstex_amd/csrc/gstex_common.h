@@ -415,12 +415,12 @@ constexpr int kPartRowGeo = 32;  // with (27 used)
 // (i/h, j/w), matching texture_dims_to_query, jagged_texture.py:23-34; clamp to edge).
 struct Bilerp { int i0, i1, j0, j1; float ax, ay; bool in_u, in_v; };
 
-// hf, wf = (float)h, (float)w (exact), passed in where the caller has them precomputed (raster records)
-__device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w, float hf, float wf) {
+// From the sample point in texel units (xr, yr) = (tu h, tv w); hf, wf = (float)h, (float)w (exact).  The clamps
+// to [0, h - 1] are single v_med3_f32 (= fminf(fmaxf(x, 0), h - 1) for every non-NaN x).
+__device__ __forceinline__ Bilerp bilerp_xy(float xr, float yr, int h, int w, float hf, float wf) {
     Bilerp b;
-    float xr = tu * hf, yr = tv * wf;
-    float x = fminf(fmaxf(xr, 0.0f), hf - 1.0f);
-    float y = fminf(fmaxf(yr, 0.0f), wf - 1.0f);
+    float x = __builtin_amdgcn_fmed3f(xr, 0.0f, hf - 1.0f);
+    float y = __builtin_amdgcn_fmed3f(yr, 0.0f, wf - 1.0f);
     b.in_u = (xr > 0.0f) && (xr < hf - 1.0f);
     b.in_v = (yr > 0.0f) && (yr < wf - 1.0f);
     b.i0 = (int)x; b.j0 = (int)y;
@@ -433,7 +433,8 @@ __device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w
 }
 
 __device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w) {
-    return bilerp_coords(tu, tv, h, w, (float)h, (float)w);
+    const float hf = (float)h, wf = (float)w;
+    return bilerp_xy(tu * hf, tv * wf, h, w, hf, wf);
 }
 
 __device__ __forceinline__ float bilerp_mix(float v00, float v01, float v10, float v11, float ax,

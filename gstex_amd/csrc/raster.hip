@@ -192,12 +192,15 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     r[R_OPAC] = opacities[g];
     r[R_RGB + 0] = rgbs[3 * g]; r[R_RGB + 1] = rgbs[3 * g + 1]; r[R_RGB + 2] = rgbs[3 * g + 2];
     r[R_NRM + 0] = (float)(sgn * fr.tw.x); r[R_NRM + 1] = (float)(sgn * fr.tw.y); r[R_NRM + 2] = (float)(sgn * fr.tw.z);
-    r[R_TU0] = uv0[2 * g];
-    r[R_AUU] = (float)(su * dot3(fr.tu, um));
-    r[R_AUV] = (float)(sv * dot3(fr.tv, um));
-    r[R_TV0] = uv0[2 * g + 1];
-    r[R_AVU] = (float)(su * dot3(fr.tu, vm));
-    r[R_AVV] = (float)(sv * dot3(fr.tv, vm));
+    // the texture affine in texel units: the sample point (tu h, tv w) = (tu0 + auu u + auv v) h, ... is read as
+    // fma(u, auu h, fma(v, auv h, tu0 h)) -- two fused multiply-adds per coordinate instead of three operations
+    const double hd = (double)tdims[3 * g], wd = (double)tdims[3 * g + 1];
+    r[R_TU0] = (float)((double)uv0[2 * g] * hd);
+    r[R_AUU] = (float)(su * dot3(fr.tu, um) * hd);
+    r[R_AUV] = (float)(sv * dot3(fr.tv, um) * hd);
+    r[R_TV0] = (float)((double)uv0[2 * g + 1] * wd);
+    r[R_AVU] = (float)(su * dot3(fr.tu, vm) * wd);
+    r[R_AVV] = (float)(sv * dot3(fr.tv, vm) * wd);
     r[R_H] = __int_as_float(tdims[3 * g]);
     r[R_W] = __int_as_float(tdims[3 * g + 1]);
     // near-edge-on: the fp64 pair-evaluation inputs for the backward, and the flag
@@ -590,9 +593,10 @@ __device__ __forceinline__ void load_texel_quad(__amdgpu_buffer_rsrc_t rs, const
     }
 }
 
-__device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float& tu, float& tv) {
-    tu = __builtin_fmaf(u, r.auu, __builtin_fmaf(v, r.auv, r.tu0));  // fused (oracle/raster.py restates it)
-    tv = __builtin_fmaf(u, r.avu, __builtin_fmaf(v, r.avv, r.tv0));
+// the sample point in texel units (xr, yr) = (tu h, tv w) from the record's prescaled texture affine (setup_kernel)
+__device__ __forceinline__ void tex_coords(const Rec& r, float u, float v, float& xr, float& yr) {
+    xr = __builtin_fmaf(u, r.auu, __builtin_fmaf(v, r.auv, r.tu0));  // fused (oracle/raster.py restates it)
+    yr = __builtin_fmaf(u, r.avu, __builtin_fmaf(v, r.avv, r.tv0));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -699,14 +703,27 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     constexpr bool kDefer = kFwdDefer && C == 3;
     float pend = 0.0f;  // (a float: see `alive`)
     float p00[CM], p01[CM], p10[CM], p11[CM], pax = 0.f, pay = 0.f, pw = 0.f;
+    // kDefer: tex[c] accumulates sum_k w_k bilerp_k(texels) with the weight folded into the four corner weights (4
+    // fused multiply-adds per channel), texw = sum_k w_k over the textured visits, and the affine (tex_scale, tex_bias)
+    // is applied once, by tex_value(): sum_k w_k (s m_k + b) = s sum_k w_k m_k + b sum_k w_k (9 + 4 C VALU per visit
+    // instead of 8 C; no decision depends on a texel value)
+    float texw = 0.0f;
     auto fold_pending = [&]() {
         if (kDefer && pend != 0.0f) {
+            const float c1 = pw * pax, c0 = pw * (1.0f - pax), qy = 1.0f - pay;
+            const float w00 = c0 * qy, w01 = c0 * pay, w10 = c1 * qy, w11 = c1 * pay;
 #pragma unroll
             for (int c = 0; c < CM; ++c) {
-                if (c < Cn) tex[c] = tex_accum(tex[c], p00[c], p01[c], p10[c], p11[c], pax, pay, tex_scale, tex_bias, pw);
+                if (c < Cn)
+                    tex[c] = __builtin_fmaf(p11[c], w11, __builtin_fmaf(p10[c], w10, __builtin_fmaf(p01[c], w01,
+                             __builtin_fmaf(p00[c], w00, tex[c]))));
             }
+            texw = texw + pw;
             pend = 0.0f;
         }
+    };
+    auto tex_value = [&](int c) {  // the texture output of channel c so far
+        return kDefer ? __builtin_fmaf(tex[c], tex_scale, tex_bias * texw) : tex[c];
     };
     const int lane = tid & 63, wave = tid >> 6;
     const size_t vm_base = visit_mask_base(rng.x, tile);
@@ -726,7 +743,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
         ck[192] = img[2];
 #pragma unroll
         for (int c = 0; c < CM; ++c)
-            if (c < Cn) ck[(4 + c) * 64] = tex[c];
+            if (c < Cn) ck[(4 + c) * 64] = tex_value(c);
         if (GEOF) {
             float* g = ck + (4 + Cn) * 64;
             g[0] = D;
@@ -815,7 +832,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
                 if (kDefer) {
                     float tu = 0.f, tv = 0.f;
                     if (has_tex) tex_coords(r, h.u, h.v, tu, tv);
-                    const Bilerp b = bilerp_coords(tu, tv, bh, bw, r.hf, r.wf);
+                    const Bilerp b = bilerp_xy(tu, tv, bh, bw, r.hf, r.wf);
                     fold_pending();
                     if (has_tex) {
                         const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
@@ -829,7 +846,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
                 } else if (has_tex) {
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
-                    const Bilerp b = bilerp_coords(tu, tv, r.h, r.w);
+                    const Bilerp b = bilerp_xy(tu, tv, r.h, r.w, r.hf, r.wf);
                     const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
                     float t00[CM], t01[CM], t10[CM], t11[CM];
                     load_texel_quad<CM>(rs, b, bw, Cn, t00, t01, t10, t11);
@@ -888,7 +905,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     out_alpha[pix] = 1.0f - T;
 #pragma unroll
     for (int c = 0; c < CM; ++c)
-        if (c < Cn) out_tex[(size_t)Cn * pix + c] = tex[c];
+        if (c < Cn) out_tex[(size_t)Cn * pix + c] = tex_value(c);
     if (GEOF) {
         if (settings & GSTEX_SETTING_EVAL_NORMAL) {
             // bit 15 (gstex.py:1198-1203, the eval "clean normal" render): the accumulated normal is returned
@@ -1387,9 +1404,10 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 #pragma unroll
                 for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
                 if (has_tex) {
-                    float tu, tv;
-                    tex_coords(r, h.u, h.v, tu, tv);
-                    b = bilerp_coords(tu, tv, r.h, r.w);  // (converting h, w here measured faster than r.hf, r.wf)
+                    float xr, yr;
+                    tex_coords(r, h.u, h.v, xr, yr);
+                    // (converting h, w here measured faster than reading r.hf, r.wf)
+                    b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h, (float)r.w);
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
                     // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
                     if (GSTEX_ABLATE & 8) {
@@ -1425,7 +1443,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // texture value (tex_scale * stored + tex_bias) and its uv-gradient.  Both are linear in the
                 // texels, so the channels are folded first: D_k = sum_c Gtex[c] * t_k[c] per bilinear corner,
                 // then one bilinear mix and one pair of differences serve all channels
-                float dtu = 0.f, dtv = 0.f;
+                float dtu = 0.f, dtv = 0.f, dxr = 0.f, dyr = 0.f;
                 if (has_tex) {
                     const float hf = (float)r.h, wf = (float)r.w;
                     float D00 = 0.f, D01 = 0.f, D10 = 0.f, D11 = 0.f;
@@ -1441,8 +1459,11 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     g += bilerp_mix(D00, D01, D10, D11, b.ax, b.ay) * tex_scale + Gtex_bias;
                     const float su = (1.0f - b.ay) * (D10 - D00) + b.ay * (D11 - D01);
                     const float sv = (1.0f - b.ax) * (D01 - D00) + b.ax * (D11 - D10);
-                    dtu = b.in_u ? w * (hf * su) : 0.0f;
-                    dtv = b.in_v ? w * (wf * sv) : 0.0f;
+                    // d value / d xr, d yr (texel units); the record's texture affine is prescaled by h, w
+                    dxr = b.in_u ? w * su : 0.0f;
+                    dyr = b.in_v ? w * sv : 0.0f;
+                    dtu = dxr * hf;
+                    dtv = dyr * wf;
                 }
                 if (GEO) {
                     g += Gd * h.z;
@@ -1461,10 +1482,14 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // texture coordinates
                 dtu *= tex_scale;  // the raw-value differences above, in value units
                 dtv *= tex_scale;
+                dxr *= tex_scale;
+                dyr *= tex_scale;
+                // gradients of the unscaled affine (uv0, auu, ...: what setup_bwd chains), and of u, v through the
+                // prescaled one
                 P[P_TU0] = dtu; P[P_AUU] = dtu * h.u; P[P_AUV] = dtu * h.v;
                 P[P_TV0] = dtv; P[P_AVU] = dtv * h.u; P[P_AVV] = dtv * h.v;
-                float du = dtu * r.auu + dtv * r.avu;
-                float dv = dtu * r.auv + dtv * r.avv;
+                float du = dxr * r.auu + dyr * r.avu;
+                float dv = dxr * r.auv + dyr * r.avv;
                 // ray-splat (use3) vs screen-space low-pass branch, per lane, as selects
                 const float du3 = GEO ? drho * 2.0f * h.u + dz * r.Tw.x : drho * 2.0f * h.u;
                 const float dv3 = GEO ? drho * 2.0f * h.v + dz * r.Tw.y : drho * 2.0f * h.v;
@@ -1960,7 +1985,7 @@ __global__ __launch_bounds__(kThreads) void texture_edit_kernel(
             if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && h.z >= dlo && h.z <= dhi) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp bl = bilerp_coords(tu, tv, r.h, r.w, r.hf, r.wf);
+                const Bilerp bl = bilerp_xy(tu, tv, r.h, r.w, r.hf, r.wf);
                 const float wc[4] = {(1.0f - bl.ax) * (1.0f - bl.ay), (1.0f - bl.ax) * bl.ay,
                                      bl.ax * (1.0f - bl.ay), bl.ax * bl.ay};
                 const int tc[4] = {bl.i0 * r.w + bl.j0, bl.i0 * r.w + bl.j1, bl.i1 * r.w + bl.j0, bl.i1 * r.w + bl.j1};

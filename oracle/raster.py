@@ -319,6 +319,9 @@ def _splat_table(inp: RasterInputs, dtype):
     sgn = torch.where(_dot3(tw, dirv) < 0, -1.0, 1.0).to(dtype).detach()
     um = inp.umap[:, 0, :].to(dtype).detach()
     vm = inp.vmap[:, 0, :].to(dtype).detach()
+    # the texture affine prescaled to texel units (raster.hip setup_kernel): the sample point (tu h, tv w)
+    hd = inp.texture_dims[:, 0].to(dtype)
+    wd = inp.texture_dims[:, 1].to(dtype)
     # affine form of the homography (gstex_common.h affine_homog): p = dx A + dy B + (0, 0, Pz)
     A = torch.stack([Tw[:, 2] * Tv[:, 1], -(Tw[:, 2] * Tv[:, 0]), Tw[:, 1] * Tv[:, 0] - Tw[:, 0] * Tv[:, 1]], -1)
     B = torch.stack([-(Tu[:, 1] * Tw[:, 2]), Tu[:, 0] * Tw[:, 2], Tu[:, 1] * Tw[:, 0] - Tu[:, 0] * Tw[:, 1]], -1)
@@ -329,9 +332,9 @@ def _splat_table(inp: RasterInputs, dtype):
         opac=inp.opacities[:, 0].to(dtype),
         rgb=inp.rgbs.to(dtype),
         nrm=tw * sgn[:, None],
-        tu0=inp.uv0[:, 0, 0].to(dtype), tv0=inp.uv0[:, 0, 1].to(dtype),
-        auu=su * _dot3(tu, um), auv=sv * _dot3(tv, um),
-        avu=su * _dot3(tu, vm), avv=sv * _dot3(tv, vm),
+        tu0=inp.uv0[:, 0, 0].to(dtype) * hd, tv0=inp.uv0[:, 0, 1].to(dtype) * wd,
+        auu=su * _dot3(tu, um) * hd, auv=sv * _dot3(tv, um) * hd,
+        avu=su * _dot3(tu, vm) * wd, avv=sv * _dot3(tv, vm) * wd,
         sgn=sgn,
     )
 
@@ -476,12 +479,11 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         w_ = tdims[ids, 1][:, None]
         off = tdims[ids, 2][:, None]
         has_tex = (h_ * w_) > 0
-        tu = _fma(u, g["auu"][:, None], _fma(v, g["auv"][:, None], g["tu0"][:, None]))  # raster.hip tex_coords
-        tv = _fma(u, g["avu"][:, None], _fma(v, g["avv"][:, None], g["tv0"][:, None]))
+        # raster.hip tex_coords: the sample point in texel units from the prescaled affine
+        xr = _fma(u, g["auu"][:, None], _fma(v, g["auv"][:, None], g["tu0"][:, None]))
+        yr = _fma(u, g["avu"][:, None], _fma(v, g["avv"][:, None], g["tv0"][:, None]))
         hf = h_.to(dtype)
         wf = w_.to(dtype)
-        xr = tu * hf
-        yr = tv * wf
         if decisions is None:
             x = torch.minimum(torch.maximum(xr, c(0.0)), hf - 1.0)
             y = torch.minimum(torch.maximum(yr, c(0.0)), wf - 1.0)

@@ -57,3 +57,30 @@ def test_cfg4_step_world2_at_cfg3_size():
 def test_cfg5_step_world4_geometry_1600x1200():
     _rehearse("cfg5_w4_geo", 4, "--n-splats", "200000", "--n-texels", "1e7", "--width", "1600", "--height", "1200",
               "--geo", "--defer-texture")
+
+
+@pytest.mark.timeout(300)
+def test_bench_world2_reports_the_exchange_phases():
+    """bench.py under torch.distributed.run at N = 2 (gloo, both ranks on the one GPU): the whole-job line, with the
+    per-phase exchange record (raster bwd end -> head landed -> tail landed -> next raster fwd) the driver's multi-GPU
+    run will carry over RCCL."""
+    import json
+
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    log = os.path.join(out_dir, "bench_w2_gloo.log")
+    env = dict(os.environ, GSTEX_DIST_BACKEND="gloo", OMP_NUM_THREADS="4", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "6", "--warmup", "3", "--no-cpu-baseline", "--no-sub"]
+    with open(log, "w") as f:
+        rc = subprocess.run(cmd, cwd=ROOT, env=env, stdout=f, stderr=subprocess.STDOUT, timeout=240).returncode
+    lines = [ln for ln in open(log).read().splitlines() if ln.startswith("{")]
+    assert rc == 0 and lines, f"bench at N=2 failed (rc {rc}), see {log}"
+    rec = json.loads(lines[-1])
+    print({k: rec[k] for k in ("value", "n_gpus", "ms_per_step", "exchange")})
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["views_per_step"] == 2
+    ex = rec["exchange"]
+    assert ex is not None and ex["steps"] >= 4 and ex["bytes"] > 150e6
+    assert 0 < ex["bwd_end_to_head_landed_ms"] <= ex["bwd_end_to_next_fwd_ms"]
+    assert 0 < ex["bwd_end_to_tail_landed_ms"] <= ex["bwd_end_to_next_fwd_ms"]
