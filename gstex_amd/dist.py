@@ -34,7 +34,12 @@ class GradSync:
     The buffer layout is keyed on parameter identity and shape: a rechart that reuses the texel store in place
     (GStexTrainer.recharge while the new charts fit its capacity) keeps the buffer; one that replaces the
     Parameter rebuilds it.  One backward per all_reduce(): gradient accumulation over several backward passes
-    is not supported (the tail would be reduced after the first)."""
+    is not supported (the tail would be reduced after the first).
+
+    Several differentiable renders per step (gradient accumulation over views) with the tail started early: the
+    trainer asks texture_grad_route(first) for each render's texel-gradient target; once the tail's collective is on
+    the wire, later renders of the step accumulate into a side buffer instead, which the step reduces and adds to the
+    slice after the tail has landed."""
 
     def __init__(self, trainer, world_size: int, group=None, overlap_tail: bool = True, tail_chunks: int = 4):
         self.trainer = trainer
@@ -50,6 +55,8 @@ class GradSync:
         self._hook = None
         self._hooked = None
         self._work = None
+        self._extra = None  # the side buffer of renders after the tail's early start (texture_grad_route)
+        self._extra_live = False
         self._sink = hasattr(trainer, "texture_grad_sink")
         # head first (a trainer that defers its texel update into the next step, GStexTrainer defer_texture): the
         # tail's collective is not started from the raster backward but queued right behind the head's at the step,
@@ -105,6 +112,7 @@ class GradSync:
             self.trainer.texture_grad_sink = params[-1].grad
             self.trainer.texture_grad_ready = (self._tail_ready_sink if self.overlap_tail and not self.head_first
                                                else None)
+            self.trainer.texture_grad_route = self._route
         else:
             self._install_hook(params[-1])
         return True
@@ -129,6 +137,28 @@ class GradSync:
             raise RuntimeError("GradSync: a second backward before all_reduce() (its texel gradient would race the "
                                "collective still reading the flat buffer)")
         self._start_tail()
+
+    def _route(self, first: bool):
+        """(target, zero, ready) of one render's texel gradient: the flat buffer's slice (zeroed by that render when
+        `first`, the tail collective started once its backward is enqueued), or -- when an earlier render of the step
+        already started the tail's collective -- the side buffer, reduced and added by the step."""
+        tail = self.trainer.texture_grad_sink
+        if self._work is None:
+            return tail, first, self.trainer.texture_grad_ready
+        if self._extra is None or self._extra.shape != tail.shape:
+            self._extra = torch.zeros_like(tail)
+            self._extra_live = True
+            return self._extra, False, None
+        zero = not self._extra_live
+        self._extra_live = True
+        return self._extra, zero, None
+
+    def _fold_extra(self):
+        """After the tail's collective has landed: reduce the side buffer of the step's later renders into it."""
+        if self._extra_live:
+            dist.all_reduce(self._extra, op=dist.ReduceOp.SUM, group=self.group)
+            self.flat[self._tail_off:self._tail_off + self._extra.numel()].add_(self._extra.view(-1))
+            self._extra_live = False
 
     def _tail_ready(self, param):
         # fires once the texel gradient is final for this backward; the view is still the flat buffer's
@@ -175,6 +205,7 @@ class GradSync:
             if work is not None:
                 dist.all_reduce(self.flat[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
                 work.wait()
+                self._fold_extra()
             else:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
@@ -243,6 +274,7 @@ class GradSync:
         if self._ctrl and not defer_tail:
             # the step's guard flag is agreed only once the head (which carries it) has landed
             work.wait()
+            self._fold_extra()
             self._mark("tail")
             head.wait()
             self._mark("head")
@@ -256,10 +288,12 @@ class GradSync:
 
             def tail():
                 work.wait()
+                self._fold_extra()
                 self._mark("tail")
                 step_tail(scale)
             return tail
         work.wait()
+        self._fold_extra()
         self._mark("tail")
         step_tail(scale)
         head.wait()

@@ -160,6 +160,7 @@ class GStexTrainer:
         # into, and the callback that starts its collective (None: autograd owns the texel gradient)
         self.texture_grad_sink = None
         self.texture_grad_ready = None
+        self.texture_grad_route = None  # GradSync: the per-render texel-gradient target (several renders per step)
         self.test_colors = None  # eval-render test colours (gstex.py:309)
         # async_texture (not in the reference; fused Adam on a HIP device): the texel parameter's Adam update (73 % of
         # the parameters at cfg3) runs on a side stream (its gradient is zeroed by the next raster forward); the next step's
@@ -344,6 +345,10 @@ class GStexTrainer:
         # forward, so that the binning's placement and sort do not queue behind that wait
         pend = self._pending_tex is not None
         late = pend and self._pending_collective
+        if self.texture_grad_route is not None and torch.is_grad_enabled():
+            sink, zero_sink, on_grad = self.texture_grad_route(self._sink_fresh)
+        else:
+            sink, zero_sink, on_grad = self.texture_grad_sink, self._sink_fresh, self.texture_grad_ready
         guard = None
         if self.pairs is not None and torch.is_grad_enabled():
             self._poll_pairs()
@@ -355,8 +360,7 @@ class GStexTrainer:
             ops.BLOCK_WIDTH, self.settings, background=self._bg_zero,
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs if geometry is None else geometry,
-            texture_grad_sink=self.texture_grad_sink, zero_texture_grad_sink=self._sink_fresh,
-            on_texture_grad=self.texture_grad_ready,
+            texture_grad_sink=sink, zero_texture_grad_sink=zero_sink, on_texture_grad=on_grad,
             texture_ready=(self._run_pending_texture if late else self._wait_side_texture if side else self._tex_ready),
             before_pair_wait=(self._launch_pending_texture_side if side else
                               self._run_pending_texture if pend and not late else None),

@@ -89,6 +89,8 @@ class _SinkTrainer:
         self.texture_dc = P(n_tex, 3)
         self.texture_grad_sink = None
         self.texture_grad_ready = None
+        self.texture_grad_route = None
+        self._fresh = True
 
     def parameters(self):
         return [self.means, self.features_dc, self.features_rest, self.opacities, self.scales, self.quats,
@@ -101,15 +103,23 @@ class _SinkTrainer:
             elif p.grad is not None:
                 p.grad.zero_()
 
-    def backward(self, rank):
-        w = float(rank + 1)
+    def backward(self, rank, scale=1.0):
+        w = float(rank + 1) * scale
         loss = w * (self.means.sum() + self.features_rest.sum() + 2 * self.opacities.sum() + self.scales.sum()
                     + self.quats.sum())
         loss.backward()  # features_dc unused under SH colour, like the real step
         assert self.texture_grad_sink is not None, "GradSync must hand the texel slice to the raster backward"
-        self.texture_grad_sink.add_(w * self.texture_dc.detach())  # the kernel's accumulation
-        if self.texture_grad_ready is not None:
-            self.texture_grad_ready()
+        if self.texture_grad_route is not None and scale != 1.0:
+            # several renders in one step (GStexTrainer.render): the per-render target, zeroed by its first render
+            sink, zero, ready = self.texture_grad_route(self._fresh)
+            self._fresh = False
+            if zero:
+                sink.zero_()
+        else:
+            sink, ready = self.texture_grad_sink, self.texture_grad_ready
+        sink.add_(w * self.texture_dc.detach())  # the kernel's accumulation
+        if ready is not None:
+            ready()
 
 
 def _trainer_worker(rank, world, port, q):
@@ -239,6 +249,44 @@ def _trainer_worker(rank, world, port, q):
                                and all(abs(c[1] - 1.0 / world) < 1e-15 for c in rng)
                                and all(bool(torch.allclose(c[5], whole[c[2]:c[3]])) for c in rng)
                                and all(sync3._offs[i] % GradSync.ALIGN == 0 for i in range(len(sync3._offs))))
+        # several renders in one step with the tail started early by the first one's backward: the later
+        # renders accumulate into GradSync's side buffer, reduced and added once the tail has landed
+        tr4 = _SinkTrainer()
+        sync4 = GradSync(tr4, world)
+        for step in range(2):
+            sync4.zero()
+            tr4._fresh = True
+            tr4.backward(rank, scale=1.0 + 1e-9)  # (scale != 1: through texture_grad_route)
+            started = sync4._work is not None
+            tr4.backward(rank, scale=2.0)
+            tr4.backward(rank, scale=3.0)
+            if step == 0:
+                sync4.all_reduce()
+                got = tr4.texture_dc.grad.clone()
+            else:
+                calls = []
+                sync4.all_reduce_and_step(lambda sc: calls.append(sc * tr4.texture_dc.grad.clone()),
+                                          lambda sc: calls.append(sc * tr4.means.grad.clone()))
+                got = calls[0]
+            want = (1.0 + 1e-9 + 2.0 + 3.0) * mean_w * tr4.texture_dc.detach()
+            res[f"multi_render_{step}"] = started and bool(torch.allclose(got, want, rtol=1e-6))
+        # the pair-capacity guard's control block (a trainer with step_control): the first CTRL elements of the flat
+        # buffer, summed over the ranks by the head's collective, left alone by zero(), carried over a rebuild
+        tr5 = _SinkTrainer()
+        tr5.step_control = torch.zeros(8)
+        sync5 = GradSync(tr5, world)
+        ok = sync5._offs[0] == GradSync.CTRL and tr5.step_control.data_ptr() == sync5.flat.data_ptr()
+        sync5.zero()
+        tr5.step_control[3] = 1.0 if rank == 0 else 0.0  # rank 0's render of step 3 overflowed
+        tr5.backward(rank)
+        sync5.all_reduce_and_step(lambda sc: None, lambda sc: None)
+        ok = ok and float(tr5.step_control[3]) > 0 and float(tr5.step_control.abs().sum()) == float(tr5.step_control[3])
+        sync5.zero()
+        ok = ok and float(tr5.step_control[3]) > 0  # zero() keeps the flags of steps in flight
+        tr5.texture_dc = torch.nn.Parameter(torch.ones(55, 3))
+        sync5.zero()  # rebuild: a new buffer, the flags copied over
+        ok = ok and float(tr5.step_control[3]) > 0 and tr5.step_control.data_ptr() == sync5.flat.data_ptr()
+        res["ctrl_block"] = bool(ok)
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -267,5 +315,7 @@ def test_trainer_layout_sink_and_recharts_world2():
         assert r["defer_head_first"] and r["defer_tail_later"], r
         assert r["head_first_no_early_tail"] and r["head_first_sums"], r
         assert r["chunked_tail"], r
+        assert r["multi_render_0"] and r["multi_render_1"], r
+        assert r["ctrl_block"], r
         for step in range(2):
             assert r[f"set_to_none_{step}"], f"rank {rank}: zero_grad(set_to_none) after zero() mis-reduced (step {step})"

@@ -365,3 +365,41 @@ def test_pair_capacity_overflow_skips_the_update_and_grows():
     tr._poll_pairs()
     assert tr.skipped_steps == [3000, 3000]
     assert any(not torch.equal(p, q.detach()) for p, q in zip(before, tr.parameters()))
+
+
+def test_two_renders_per_step_under_overlapped_gradsync():
+    """gradient accumulation over two views per step with the default overlapped exchange (a trainer that
+    does not defer its texel update, the tail's collective started from the first raster backward): the second render
+    accumulates into GradSync's side buffer, reduced and added once the tail has landed -- trains like the plain
+    trainer (world 1 over RCCL)."""
+    from gstex_amd.dist import GradSync
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        sc = make_scene(3000, 60_000, seed=14)
+        views = [sphere_view(i, 96, 96).to(dev) for i in range(2)]
+        g = torch.Generator().manual_seed(7)
+        gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(2)]
+        plain = GStexTrainer(sc, dev, start_step=3000)
+        synced = GStexTrainer(sc, dev, start_step=3000)
+        sync = GradSync(synced, 1)
+        assert not sync.head_first
+        for step in range(3):
+            plain.zero_grad()
+            plain.forward_backward(views[0], gts[0])
+            plain.forward_backward(views[1], gts[1])
+            plain.optimizer_step()
+            sync.zero()
+            synced.forward_backward(views[0], gts[0])
+            assert sync._work is not None  # the tail's collective started from the first raster backward
+            synced.forward_backward(views[1], gts[1])
+            synced.optimizer_step(sync=sync)
+        torch.cuda.synchronize()
+        for (name, a), b in zip(plain.param_groups().items(), synced.param_groups().values()):
+            _assert_trains_alike(name, a[0], b[0], "two renders per step under GradSync")
+    finally:
+        dist.destroy_process_group()
