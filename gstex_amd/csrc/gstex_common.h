@@ -343,7 +343,7 @@ enum RecField {
     R_A = 0, R_B = 3, R_PZ = 6, R_XA = 7, R_YA = 8, R_XY = 9, R_OPAC = 11,
     R_TW = 12, R_RGB = 15, R_TU0 = 18, R_AUU = 19, R_AUV = 20, R_TV0 = 21, R_AVU = 22, R_AVV = 23,
     R_H = 24, R_W = 25, R_OFF = 26, R_NRM = 27,
-    R_HF = 30, R_WF = 31  // (float)h, (float)w: exact, saves the forward's per-visit conversions
+    R_HM1 = 30, R_WM1 = 31  // (float)(h - 1), (float)(w - 1): exact, the forward's texel clamps without conversions
 };
 constexpr int kCullPlanes = 3;  // record planes holding the cull fields
 
@@ -415,14 +415,14 @@ constexpr int kPartRowGeo = 32;  // with (27 used)
 // (i/h, j/w), matching texture_dims_to_query, jagged_texture.py:23-34; clamp to edge).
 struct Bilerp { int i0, i1, j0, j1; float ax, ay; bool in_u, in_v; };
 
-// From the sample point in texel units (xr, yr) = (tu h, tv w); hf, wf = (float)h, (float)w (exact).  The clamps
-// to [0, h - 1] are single v_med3_f32 (= fminf(fmaxf(x, 0), h - 1) for every non-NaN x).
-__device__ __forceinline__ Bilerp bilerp_xy(float xr, float yr, int h, int w, float hf, float wf) {
+// From the sample point in texel units (xr, yr) = (tu h, tv w); hm1, wm1 = (float)(h - 1), (float)(w - 1) (exact).
+// The clamps to [0, h - 1] are single v_med3_f32 (= fminf(fmaxf(x, 0), h - 1) for every non-NaN x).
+__device__ __forceinline__ Bilerp bilerp_xy(float xr, float yr, int h, int w, float hm1, float wm1) {
     Bilerp b;
-    float x = __builtin_amdgcn_fmed3f(xr, 0.0f, hf - 1.0f);
-    float y = __builtin_amdgcn_fmed3f(yr, 0.0f, wf - 1.0f);
-    b.in_u = (xr > 0.0f) && (xr < hf - 1.0f);
-    b.in_v = (yr > 0.0f) && (yr < wf - 1.0f);
+    float x = __builtin_amdgcn_fmed3f(xr, 0.0f, hm1);
+    float y = __builtin_amdgcn_fmed3f(yr, 0.0f, wm1);
+    b.in_u = (xr > 0.0f) && (xr < hm1);
+    b.in_v = (yr > 0.0f) && (yr < wm1);
     b.i0 = (int)x; b.j0 = (int)y;
     b.i1 = min(b.i0 + 1, h - 1);
     b.j1 = min(b.j0 + 1, w - 1);
@@ -434,7 +434,7 @@ __device__ __forceinline__ Bilerp bilerp_xy(float xr, float yr, int h, int w, fl
 
 __device__ __forceinline__ Bilerp bilerp_coords(float tu, float tv, int h, int w) {
     const float hf = (float)h, wf = (float)w;
-    return bilerp_xy(tu * hf, tv * wf, h, w, hf, wf);
+    return bilerp_xy(tu * hf, tv * wf, h, w, hf - 1.0f, wf - 1.0f);
 }
 
 __device__ __forceinline__ float bilerp_mix(float v00, float v01, float v10, float v11, float ax,

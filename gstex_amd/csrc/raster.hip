@@ -215,8 +215,8 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     }
     r[R_XA] = (float)h.xa;
     r[R_YA] = (float)h.ya;
-    r[R_HF] = (float)tdims[3 * g];
-    r[R_WF] = (float)tdims[3 * g + 1];
+    r[R_HM1] = (float)(tdims[3 * g] - 1);
+    r[R_WM1] = (float)(tdims[3 * g + 1] - 1);
     float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
 #pragma unroll
     for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
@@ -234,7 +234,7 @@ struct Rec {
     int h, w, off;
     bool hp;  // near-edge-on: fp64 inputs in rec_hp for the backward (bit 31 of R_OFF)
     float xa, ya;
-    float hf, wf;  // (float)h, (float)w
+    float hm1, wm1;  // (float)(h - 1), (float)(w - 1)
 };
 
 // Record fields from its 8 float4 planes (gstex_common.h RecField)
@@ -255,7 +255,7 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.hp = (__float_as_uint(v[R_OFF]) & kHpFlag) != 0u;
     r.xa = v[R_XA]; r.ya = v[R_YA];
     r.nrm[0] = v[R_NRM]; r.nrm[1] = v[R_NRM + 1]; r.nrm[2] = v[R_NRM + 2];
-    r.hf = v[R_HF]; r.wf = v[R_WF];
+    r.hm1 = v[R_HM1]; r.wm1 = v[R_WM1];
     return r;
 }
 
@@ -830,9 +830,10 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
                 const int boff = __builtin_amdgcn_readfirstlane(r.off);
                 const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels && !(GSTEX_ABLATE & 4);
                 if (kDefer) {
-                    float tu = 0.f, tv = 0.f;
-                    if (has_tex) tex_coords(r, h.u, h.v, tu, tv);
-                    const Bilerp b = bilerp_xy(tu, tv, bh, bw, r.hf, r.wf);
+                    // (computed whether or not the splat has texels: used only when it has)
+                    float tu, tv;
+                    tex_coords(r, h.u, h.v, tu, tv);
+                    const Bilerp b = bilerp_xy(tu, tv, bh, bw, r.hm1, r.wm1);
                     fold_pending();
                     if (has_tex) {
                         const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
@@ -846,7 +847,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
                 } else if (has_tex) {
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
-                    const Bilerp b = bilerp_xy(tu, tv, r.h, r.w, r.hf, r.wf);
+                    const Bilerp b = bilerp_xy(tu, tv, r.h, r.w, r.hm1, r.wm1);
                     const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
                     float t00[CM], t01[CM], t10[CM], t11[CM];
                     load_texel_quad<CM>(rs, b, bw, Cn, t00, t01, t10, t11);
@@ -1407,7 +1408,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     float xr, yr;
                     tex_coords(r, h.u, h.v, xr, yr);
                     // (converting h, w here measured faster than reading r.hf, r.wf)
-                    b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h, (float)r.w);
+                    b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
                     // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
                     if (GSTEX_ABLATE & 8) {
@@ -1985,7 +1986,7 @@ __global__ __launch_bounds__(kThreads) void texture_edit_kernel(
             if (r.h * r.w > 0 && r.off + r.h * r.w <= n_texels && h.z >= dlo && h.z <= dhi) {
                 float tu, tv;
                 tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp bl = bilerp_xy(tu, tv, r.h, r.w, r.hf, r.wf);
+                const Bilerp bl = bilerp_xy(tu, tv, r.h, r.w, r.hm1, r.wm1);
                 const float wc[4] = {(1.0f - bl.ax) * (1.0f - bl.ay), (1.0f - bl.ax) * bl.ay,
                                      bl.ax * (1.0f - bl.ay), bl.ax * bl.ay};
                 const int tc[4] = {bl.i0 * r.w + bl.j0, bl.i0 * r.w + bl.j1, bl.i1 * r.w + bl.j0, bl.i1 * r.w + bl.j1};
