@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_TAG = "r03w"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+PROFILE_TAG = "r04b"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
 N_POSES = 8
 
 
@@ -381,9 +381,9 @@ def main():
             rows.append((b_end.elapsed_time(pe["head"][k]), b_end.elapsed_time(pe["tail"][k]),
                          b_end.elapsed_time(fwd[k + 1][0])))
         if rows:
-            med = [round(statistics.median(r[i] for r in rows), 4) for i in range(3)]
-            exchange = dict(bytes=int(sync.nbytes), steps=len(rows), bwd_end_to_head_landed_ms=med[0],
-                            bwd_end_to_tail_landed_ms=med[1], bwd_end_to_next_fwd_ms=med[2],
+            ph = [round(statistics.median(r[i] for r in rows), 4) for i in range(3)]
+            exchange = dict(bytes=int(sync.nbytes), steps=len(rows), bwd_end_to_head_landed_ms=ph[0],
+                            bwd_end_to_tail_landed_ms=ph[1], bwd_end_to_next_fwd_ms=ph[2],
                             note="rank 0 HIP events, medians over the timed steps; the exchange's exposed time is "
                                  "bwd_end_to_next_fwd_ms minus the one-GPU gap (DESIGN.md §6)")
         sync.phase_events = None

@@ -143,7 +143,8 @@ constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 // 96x96 window with the oracle (tools/grad_precision.py --hp-cos): 1.7 % of the splats at 0.02, 4.3 % at 0.05;
 // means / quats 4.9e-5 / 4.3e-5 -> 2.3e-6 / 1.9e-6 at 0.05.
 #ifndef GSTEX_HP
-#define GSTEX_HP 1  // 0: the backward ignores rec_hp (A/B builds)
+#define GSTEX_HP 0  // 1: the backward reads rec_hp (the fp64 near-edge-on experiment, with GSTEX_HP_RECORD=1: measured
+                    // not to close the fp32-record floor)
 #endif
 #ifndef GSTEX_HP_COS
 #define GSTEX_HP_COS 0.05

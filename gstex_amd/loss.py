@@ -16,6 +16,15 @@ from . import _lib
 from ._lib import call, ptr
 
 _WINDOWS: dict = {}
+_CWIN = None
+
+
+def _cwin():
+    """The 11-tap window as the C array the loss kernels take (built once: no per-step tensor-to-list work)."""
+    global _CWIN
+    if _CWIN is None:
+        _CWIN = (ctypes.c_float * 11)(*(float(x) for x in gaussian_window().numpy()))
+    return _CWIN
 
 
 def gaussian_window(size: int = 11, sigma: float = 1.5) -> torch.Tensor:
@@ -49,8 +58,7 @@ class _PhotometricLoss(torch.autograd.Function):
         img, tex, alpha, background, gt = (t.detach().contiguous() for t in (img, tex, alpha, background, gt))
         H, W = alpha.shape
         C = tex.shape[2]
-        win = gaussian_window()
-        cwin = (ctypes.c_float * 11)(*win.tolist())
+        cwin = _cwin()
         ws = torch.empty((int(_lib.load().gstex_loss_workspace_size(H, W)),), device=img.device, dtype=torch.uint8)
         out = torch.empty((3,), device=img.device, dtype=torch.float32)
         rgb = torch.empty((H, W, 3), device=img.device, dtype=torch.float32)
@@ -70,7 +78,7 @@ class _PhotometricLoss(torch.autograd.Function):
         img, tex, alpha, background, gt, ws = ctx.saved_tensors
         H, W = alpha.shape
         C = tex.shape[2]
-        cwin = (ctypes.c_float * 11)(*gaussian_window().tolist())
+        cwin = _cwin()
         d_img = torch.empty_like(img)
         d_tex = torch.empty_like(tex)
         d_alpha = torch.empty_like(alpha)

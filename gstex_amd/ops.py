@@ -26,7 +26,8 @@ _TIMING: dict | None = None
 
 
 _TIMED = {"gstex_raster_fwd", "gstex_raster_bwd"}
-HP_DOUBLES = 10  # raster.hip kHpDoubles  # the roofline kernels; each event pair costs ~3 us of stream time
+HP_DOUBLES = 10  # raster.hip kHpDoubles
+_HP_RECORD = os.environ.get("GSTEX_HP_RECORD", "0") != "0"  # the roofline kernels; each event pair costs ~3 us of stream time
 
 
 def set_kernel_timing(enabled: bool, names=None) -> None:
@@ -519,8 +520,10 @@ class _TextureGaussians(torch.autograd.Function):
         # trainable parameters), where apply() records no graph whatever the inputs' requires_grad
         needs_bwd = bool(grad_enabled) and any(ctx.needs_input_grad)
         # the near-edge-on splats' fp64 pair-evaluation inputs for the backward (gstex_raster_setup_hp; rows written
-        # only for the flagged splats)
-        rec_hp = torch.empty((n, HP_DOUBLES), device=dev, dtype=torch.float64) if needs_bwd else None
+        # only for the flagged splats): off unless GSTEX_HP_RECORD=1 -- measured not to close the fp32-record floor
+        # and to cost backward time, so the training path passes none
+        rec_hp = (torch.empty((n, HP_DOUBLES), device=dev, dtype=torch.float64) if needs_bwd and _HP_RECORD
+                  else None)
         _launch("gstex_raster_setup_hp", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
                 ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam,
                 ptr(records), ptr(rec_hp), st)
