@@ -318,13 +318,16 @@ def main():
     if sync is not None and not args.no_kernel_timing:
         sync.phase_events = {}  # when the head / tail collectives land, on rank 0's compute stream
     step_ev = []
+    host_s = []  # host time to enqueue each step (the device runs behind it when the step is not host-bound)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
+        h0 = time.perf_counter()
         a.record()
         step()
         b.record()
+        host_s.append(time.perf_counter() - h0)
         step_ev.append((a, b))
     trainer.wait_texture()  # the last timed step's deferred texel update, inside: K steps = K texel updates
     torch.cuda.synchronize()
@@ -459,6 +462,7 @@ def main():
         "ms_per_step": round(ms, 4),
         "ms_per_step_median": round(statistics.median(step_ms), 4),
         "step_ms_events": [round(x, 3) for x in step_ms],  # rank 0's per-step HIP-event times
+        "host_enqueue_ms_median": round(1e3 * statistics.median(host_s), 4),  # Python + launch time per step
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
