@@ -658,7 +658,8 @@ int bin_sort_impl(int32_t n, int64_t n_isect, const float* centers, const float*
     const long long cap = capped ? (long long)n_isect : -1;
     BinWorkspace ws;
     bin_layout(n_tiles, n_isect, (char*)workspace, &ws);
-    (void)hipMemsetAsync(ws.tile_count, 0, (size_t)(n_tiles + 1) * sizeof(int32_t), st);
+    // (the whole 256-B-aligned slot: a size that is not a multiple of 16 B costs the runtime a second fill kernel)
+    (void)hipMemsetAsync(ws.tile_count, 0, align256((size_t)(n_tiles + 1) * sizeof(int32_t)), st);
     if (n_tiles <= kCountLdsTiles)
         count_lds_kernel<<<div_up(n, 256 * kCountSplatsPerThread), 256, 0, st>>>(
             n, centers, extents, offsets, tiles_x, tiles_y, block, ws.tile_count, ws.rank, cap);
