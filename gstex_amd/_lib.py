@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 REC_FLOATS = 32
 BWD_ORDERED = 1 << 30  # GSTEX_BWD_ORDERED: gstex_raster_bwd skips the unit ordering
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
@@ -97,6 +97,10 @@ SIGNATURES = {
     ),
     "gstex_host_words_alloc": (c_int32, [c_int32, POINTER(c_void_p), POINTER(c_void_p)]),
     "gstex_host_words_free": (c_int32, [c_void_p]),
+    "gstex_timing_event_create": (c_int32, [POINTER(c_void_p)]),
+    "gstex_timing_event_record": (c_int32, [c_void_p, c_void_p]),
+    "gstex_timing_event_elapsed": (c_int32, [c_void_p, c_void_p, POINTER(ctypes.c_float)]),
+    "gstex_timing_event_destroy": (c_int32, [c_void_p]),
     "gstex_raster_setup": (
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
@@ -212,6 +216,35 @@ def ptr(t) -> int | None:
 
 def stream_of(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+class TimingEvent:
+    """A HIP event for timing only (gstex_timing_event_*, ABI 14: no system-scope fence when recorded, so a pair
+    around a kernel does not write back and invalidate the caches between launches).  record() on the current
+    stream of `device` (or an explicit stream handle); elapsed_time(end) in ms once both have completed."""
+
+    __slots__ = ("_h",)
+
+    def __init__(self):
+        h = c_void_p()
+        call("gstex_timing_event_create", ctypes.byref(h))
+        self._h = h.value
+
+    def record(self, device=None, stream: int | None = None) -> None:
+        call("gstex_timing_event_record", self._h,
+             stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
+
+    def elapsed_time(self, end: "TimingEvent") -> float:
+        ms = c_float()
+        call("gstex_timing_event_elapsed", self._h, end._h, ctypes.byref(ms))
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            if self._h:
+                load().gstex_timing_event_destroy(self._h)
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
 
 def make_camera(viewmat, c2w, fx, fy, cx, cy, H, W, block) -> GstexCamera:

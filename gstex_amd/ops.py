@@ -25,9 +25,10 @@ BLOCK_WIDTH = 16
 _TIMING: dict | None = None
 
 
-_TIMED = {"gstex_raster_fwd", "gstex_raster_bwd"}
+_TIMED_DEFAULT = ("gstex_raster_fwd", "gstex_raster_bwd")  # the roofline kernels
+_TIMED = set(_TIMED_DEFAULT)
 HP_DOUBLES = 10  # raster.hip kHpDoubles
-_HP_RECORD = os.environ.get("GSTEX_HP_RECORD", "0") != "0"  # the roofline kernels; each event pair costs ~3 us of stream time
+_HP_RECORD = os.environ.get("GSTEX_HP_RECORD", "0") != "0"
 
 
 def set_kernel_timing(enabled: bool, names=None) -> None:
@@ -35,8 +36,7 @@ def set_kernel_timing(enabled: bool, names=None) -> None:
     `names`) on the stream they run on (bench.py / profiling only)."""
     global _TIMING, _TIMED
     _TIMING = {} if enabled else None
-    if names is not None:
-        _TIMED = set(names)
+    _TIMED = set(names) if names is not None else set(_TIMED_DEFAULT)
 
 
 def kernel_times() -> dict:
@@ -58,8 +58,9 @@ def _launch(name: str, *args) -> None:
     if _TIMING is None or key not in _TIMED:
         call(name, *args)
         return
-    a = torch.cuda.Event(enable_timing=True)
-    b = torch.cuda.Event(enable_timing=True)
+    # fence-free timing events (_lib.TimingEvent): a default event pair around each launch cost ~10 us of device time
+    a = _lib.TimingEvent()
+    b = _lib.TimingEvent()
     a.record()
     call(name, *args)
     b.record()
