@@ -97,10 +97,11 @@ SIGNATURES = {
     ),
     "gstex_host_words_alloc": (c_int32, [c_int32, POINTER(c_void_p), POINTER(c_void_p)]),
     "gstex_host_words_free": (c_int32, [c_void_p]),
-    "gstex_timing_event_create": (c_int32, [POINTER(c_void_p)]),
-    "gstex_timing_event_record": (c_int32, [c_void_p, c_void_p]),
-    "gstex_timing_event_elapsed": (c_int32, [c_void_p, c_void_p, POINTER(ctypes.c_float)]),
-    "gstex_timing_event_destroy": (c_int32, [c_void_p]),
+    "gstex_event_create": (c_int32, [c_int32, POINTER(c_void_p)]),
+    "gstex_event_record": (c_int32, [c_void_p, c_void_p]),
+    "gstex_event_elapsed": (c_int32, [c_void_p, c_void_p, POINTER(ctypes.c_float)]),
+    "gstex_stream_wait_event": (c_int32, [c_void_p, c_void_p]),
+    "gstex_event_destroy": (c_int32, [c_void_p]),
     "gstex_raster_setup": (
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
@@ -218,33 +219,52 @@ def stream_of(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-class TimingEvent:
-    """A HIP event for timing only (gstex_timing_event_*, ABI 14: no system-scope fence when recorded, so a pair
-    around a kernel does not write back and invalidate the caches between launches).  record() on the current
-    stream of `device` (or an explicit stream handle); elapsed_time(end) in ms once both have completed."""
-
+class _Event:
     __slots__ = ("_h",)
+    KIND = 0
 
     def __init__(self):
         h = c_void_p()
-        call("gstex_timing_event_create", ctypes.byref(h))
+        call("gstex_event_create", self.KIND, ctypes.byref(h))
         self._h = h.value
 
     def record(self, device=None, stream: int | None = None) -> None:
-        call("gstex_timing_event_record", self._h,
+        """Record on `stream` (a HIP stream handle), default the current stream of `device`."""
+        call("gstex_event_record", self._h,
              stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
-
-    def elapsed_time(self, end: "TimingEvent") -> float:
-        ms = c_float()
-        call("gstex_timing_event_elapsed", self._h, end._h, ctypes.byref(ms))
-        return float(ms.value)
 
     def __del__(self):
         try:
             if self._h:
-                load().gstex_timing_event_destroy(self._h)
+                load().gstex_event_destroy(self._h)
         except Exception:  # noqa: BLE001  (interpreter shutdown)
             pass
+
+
+class TimingEvent(_Event):
+    """A HIP event for timing only (gstex_event_create(GSTEX_EVENT_TIMING), ABI 14: no system-scope fence when
+    recorded, so a pair around a kernel does not write back and invalidate the caches between launches);
+    elapsed_time(end) in ms once both have completed."""
+
+    __slots__ = ()
+    KIND = 0
+
+    def elapsed_time(self, end: "TimingEvent") -> float:
+        ms = c_float()
+        call("gstex_event_elapsed", self._h, end._h, ctypes.byref(ms))
+        return float(ms.value)
+
+
+class OrderEvent(_Event):
+    """A HIP event for ordering one stream after another on the same device (GSTEX_EVENT_ORDER: no timing, a
+    device-scope release instead of the default event's system-scope one); wait(stream) = hipStreamWaitEvent."""
+
+    __slots__ = ()
+    KIND = 1
+
+    def wait(self, device=None, stream: int | None = None) -> None:
+        call("gstex_stream_wait_event",
+             stream if stream is not None else torch.cuda.current_stream(device).cuda_stream, self._h)
 
 
 def make_camera(viewmat, c2w, fx, fy, cx, cy, H, W, block) -> GstexCamera:

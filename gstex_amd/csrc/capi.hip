@@ -65,40 +65,50 @@ extern "C" int gstex_host_words_free(int32_t* host) {
     return GSTEX_OK;
 }
 
-// Timing events (ABI 14): no system-scope fence at record time (see gstex_hip.h)
-extern "C" int gstex_timing_event_create(void** event) {
-    if (!event) {
-        gstex::set_error("gstex_timing_event_create: null event");
+// Lightweight events (ABI 14, see gstex_hip.h)
+extern "C" int gstex_event_create(int32_t kind, void** event) {
+    if (!event || (kind != GSTEX_EVENT_TIMING && kind != GSTEX_EVENT_ORDER)) {
+        gstex::set_error("gstex_event_create: invalid arguments (kind %d)", kind);
         return GSTEX_ERR_INVALID_ARG;
     }
+    const unsigned flags = kind == GSTEX_EVENT_TIMING ? hipEventDisableSystemFence
+                                                      : (hipEventDisableTiming | hipEventReleaseToDevice);
     hipEvent_t e = nullptr;
-    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
-        gstex::set_error("gstex_timing_event_create: hipEventCreateWithFlags failed");
+    if (hipEventCreateWithFlags(&e, flags) != hipSuccess) {
+        gstex::set_error("gstex_event_create: hipEventCreateWithFlags failed");
         return GSTEX_ERR_LAUNCH;
     }
     *event = (void*)e;
     return GSTEX_OK;
 }
 
-extern "C" int gstex_timing_event_record(void* event, void* stream) {
+extern "C" int gstex_event_record(void* event, void* stream) {
     if (!event || hipEventRecord((hipEvent_t)event, gstex::as_stream(stream)) != hipSuccess) {
-        gstex::set_error("gstex_timing_event_record: hipEventRecord failed");
+        gstex::set_error("gstex_event_record: hipEventRecord failed");
         return GSTEX_ERR_LAUNCH;
     }
     return GSTEX_OK;
 }
 
-extern "C" int gstex_timing_event_elapsed(void* start, void* end, float* ms) {
+extern "C" int gstex_event_elapsed(void* start, void* end, float* ms) {
     if (!start || !end || !ms || hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end) != hipSuccess) {
-        gstex::set_error("gstex_timing_event_elapsed: hipEventElapsedTime failed (events recorded and complete?)");
+        gstex::set_error("gstex_event_elapsed: hipEventElapsedTime failed (timing events, recorded and complete?)");
         return GSTEX_ERR_LAUNCH;
     }
     return GSTEX_OK;
 }
 
-extern "C" int gstex_timing_event_destroy(void* event) {
+extern "C" int gstex_stream_wait_event(void* stream, void* event) {
+    if (!event || hipStreamWaitEvent(gstex::as_stream(stream), (hipEvent_t)event, 0) != hipSuccess) {
+        gstex::set_error("gstex_stream_wait_event: hipStreamWaitEvent failed");
+        return GSTEX_ERR_LAUNCH;
+    }
+    return GSTEX_OK;
+}
+
+extern "C" int gstex_event_destroy(void* event) {
     if (event && hipEventDestroy((hipEvent_t)event) != hipSuccess) {
-        gstex::set_error("gstex_timing_event_destroy: hipEventDestroy failed");
+        gstex::set_error("gstex_event_destroy: hipEventDestroy failed");
         return GSTEX_ERR_LAUNCH;
     }
     return GSTEX_OK;

@@ -121,7 +121,11 @@ def _stream(t: torch.Tensor) -> int:
 
 
 _ORDER_STREAMS: dict = {}
-_ORDER_SIDE = os.environ.get("GSTEX_ORDER_SIDE", "1") != "0"  # 0: the backward orders its units itself
+# 1: the backward's unit ordering on a side stream right after the forward, overlapping the loss kernels (round 3:
+# 10-20 us faster); round 4, with the lighter timing events, the cross-stream fork / join costs what the overlap saves
+# (A/B, three interleaved 60-step triples: in stream 2.353-2.361 ms mean vs 2.362-2.364 on the side stream), so the
+# backward orders its units itself by default
+_ORDER_SIDE = os.environ.get("GSTEX_ORDER_SIDE", "0") != "0"
 
 
 def _order_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -602,13 +606,16 @@ class _TextureGaussians(torch.autograd.Function):
         if aux is not None and n_isect > 0 and _ORDER_SIDE:
             # the backward's unit launch order (a scan and a scatter over the forward's per-unit costs, ~18 us of
             # latency-bound launches) on a side stream, overlapping the loss kernels that run before the backward
+            # (fork and join by device-scope ordering events: a default event's system-scope release writes the
+            # caches back at each of these points)
             main = torch.cuda.current_stream(dev)
             side = _order_stream(dev)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                _launch("gstex_raster_bwd_order", cam, C, n_isect, ptr(aux), side.cuda_stream)
-                ctx.order_ready = torch.cuda.Event()
-                ctx.order_ready.record(side)
+            fork = _lib.OrderEvent()
+            fork.record(stream=main.cuda_stream)
+            fork.wait(stream=side.cuda_stream)
+            _launch("gstex_raster_bwd_order", cam, C, n_isect, ptr(aux), side.cuda_stream)
+            ctx.order_ready = _lib.OrderEvent()
+            ctx.order_ready.record(stream=side.cuda_stream)
             aux.record_stream(side)
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
@@ -662,7 +669,7 @@ class _TextureGaussians(torch.autograd.Function):
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
         if ctx.order_ready is not None:  # the unit order was computed on the side stream after the forward
-            torch.cuda.current_stream(dev).wait_event(ctx.order_ready)
+            ctx.order_ready.wait(stream=torch.cuda.current_stream(dev).cuda_stream)
             settings_b = int(settings) | _lib.BWD_ORDERED
         else:
             settings_b = settings

@@ -152,15 +152,19 @@ typedef struct gstex_pair_guard {
 int gstex_host_words_alloc(int32_t n, int32_t** host, int32_t** device);
 int gstex_host_words_free(int32_t* host);
 
-/* Timing events (ABI 14): HIP events created with hipEventDisableSystemFence, i.e. without the system-scope
- * release / acquire (an L2 writeback and invalidate) a default event performs when it is recorded -- for measuring
- * kernel durations on the launch stream inside a timed loop without perturbing it (a default-event pair around each
- * raster launch cost ~10 us of device time per pair, bench.py A/B).  Not for host synchronisation or cross-stream
- * ordering of data.  elapsed: milliseconds between two recorded events (both complete). */
-int gstex_timing_event_create(void** event);
-int gstex_timing_event_record(void* event, void* stream);
-int gstex_timing_event_elapsed(void* start, void* end, float* ms);
-int gstex_timing_event_destroy(void* event);
+/* Lightweight events (ABI 14).  kind GSTEX_EVENT_TIMING: timing only, created with hipEventDisableSystemFence -- no
+ * system-scope release / acquire (an L2 writeback and invalidate) when recorded, so a pair around a kernel measures it
+ * without perturbing the loop it sits in (a default-event pair around each raster launch cost ~10 us of device time per
+ * pair in bench.py's A/B); not for host synchronisation.  kind GSTEX_EVENT_ORDER: no timing, a device-scope release
+ * (hipEventReleaseToDevice) -- for ordering one stream after another on the same device (gstex_stream_wait_event).
+ * elapsed: milliseconds between two recorded, completed timing events. */
+#define GSTEX_EVENT_TIMING 0
+#define GSTEX_EVENT_ORDER 1
+int gstex_event_create(int32_t kind, void** event);
+int gstex_event_record(void* event, void* stream);
+int gstex_event_elapsed(void* start, void* end, float* ms);
+int gstex_stream_wait_event(void* stream, void* event);
+int gstex_event_destroy(void* event);
 int gstex_scan_offsets_guarded(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
                                size_t workspace_bytes, const gstex_pair_guard* guard, void* stream);
 int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* centers, const float* extents,
