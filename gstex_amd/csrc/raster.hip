@@ -146,6 +146,15 @@ constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 #define GSTEX_HP 0  // 1: the backward reads rec_hp (the fp64 near-edge-on experiment, with GSTEX_HP_RECORD=1: measured
                     // not to close the fp32-record floor)
 #endif
+#ifndef GSTEX_STAGE_DMA
+#define GSTEX_STAGE_DMA 0  // forward: a batch's records staged by LDS-DMA (global_load_lds_dwordx4; measured: no change, 0.525 -> 0.527 ms)
+#endif
+constexpr bool kStageDma = GSTEX_STAGE_DMA;
+static_assert(!GSTEX_STAGE_DMA || (kFwdBatch == 128 && kRecF4 == 8 && kThreads == 256),
+              "DMA staging: 4 waves x 2 planes x 2 halves of 64 splats");
+#ifndef GSTEX_WORD_WAIT
+#define GSTEX_WORD_WAIT 1  // backward: the visit loop's id wait hoisted to the word start (see raster_bwd_kernel)
+#endif
 #ifndef GSTEX_HP_COS
 #define GSTEX_HP_COS 0.05
 #endif
@@ -777,9 +786,27 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
             if (lane < nb) my_gid = sorted_ids[b0 + lane];
         } else {
             if (__syncthreads_count(GSTEX_FWD_DONE ? 1 : 0) == kThreads) break;
-            for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
-                const int j = q / kRecF4, k = q % kRecF4;
-                if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+            if constexpr (kStageDma) {
+                // LDS-DMA staging: wave w fills planes 2w and 2w + 1, each as two 64-splat halves (one
+                // global_load_lds_dwordx4 per half: lane l's 16 B land at the half's base + 16 l, i.e. s_rec[k][h 64 +
+                // l]).  Two memory round trips per batch (the ids, then the four DMAs, drained by the barrier) and no
+                // VGPRs for the data; the register form waits for each id, then each plane.  Past the list's end the
+                // last entry is loaded again (never read: the waves look at j < nb only).
+                const int jl = rng.y - 1 - b0;
+                const int id0 = sorted_ids[b0 + min(lane, jl)], id1 = sorted_ids[b0 + min(64 + lane, jl)];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int k = 2 * wave + (i >> 1), h = i & 1;
+                    const float4* src = records + (size_t)(h ? id1 : id0) * kRecF4 + k;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                     (__attribute__((address_space(3))) void*)&s_rec[k * kFwdBatch + h * 64],
+                                                     16, 0, 0);
+                }
+            } else {
+                for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
+                    const int j = q / kRecF4, k = q % kRecF4;
+                    if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+                }
             }
             __syncthreads();
         }
@@ -1328,6 +1355,13 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             my_gid = sorted_ids[rng.x + pos0 + lane];
             my_slot = sorted_slots[rng.x + pos0 + lane];
         }
+#if GSTEX_WORD_WAIT
+        // wait for the word's ids here, once: otherwise the waitcnt pass, which merges the loop's entry (ids
+        // pending) with its back edge (the previous visit's atomics pending), waits at the top of EVERY visit for
+        // all but one of the previous visit's atomics before the record can be addressed (vmcnt counts the
+        // no-return atomics in order with the loads)
+        asm volatile("; word ids %0 %1" ::"v"(my_gid), "v"(my_slot));
+#endif
         while (todo) {
             const int j = 63 - __builtin_clzll(todo);
             todo &= ~(1ull << j);
