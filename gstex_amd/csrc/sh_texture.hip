@@ -104,9 +104,25 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int k0, 
 // The same two kernels with the coefficient rows staged through LDS: a workgroup's 128 splats own one
 // contiguous span of coefficients, read (forward) or written (backward) with consecutive lanes on
 // consecutive words; the per-thread strided rows (180 B apart at K = 15) made every load instruction
-// touch 64 cache lines.  Same arithmetic and order as above.  Used for K <= kShStagedMaxK.
+// touch 64 cache lines.  Same arithmetic and order as above.  Used for K <= kShStagedMaxK.  The span is
+// copied whole (rows of 3K words, also when the degree uses fewer) as 16-B vectors, several in flight per
+// thread, when it is 16-B aligned (the scalar copy with a division per word was the kernels' latency chain).
 constexpr int kShBlock = 128;
 constexpr int kShStagedMaxK = 25;
+__device__ __forceinline__ void sh_copy_span(float* __restrict__ dst, const float* __restrict__ src, int total) {
+    const int t = threadIdx.x;
+    int done = 0;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+        const int n4 = total >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll 4
+        for (int q = t; q < n4; q += kShBlock) d4[q] = s4[q];
+        done = n4 << 2;
+    }
+    for (int q = done + t; q < total; q += kShBlock) dst[q] = src[q];
+}
+
 __global__ __launch_bounds__(kShBlock) void sh_fwd_staged_kernel(int n, int degree, int k0, int K,
                                                                 const float* __restrict__ dirs,
                                                                 const float* __restrict__ coeffs,
@@ -116,18 +132,14 @@ __global__ __launch_bounds__(kShBlock) void sh_fwd_staged_kernel(int n, int degr
     const int i0 = blockIdx.x * kShBlock;
     const int cnt = min(kShBlock, n - i0);
     const int nb = (degree + 1) * (degree + 1);
-    const int kn = (nb - k0) * 3;  // coefficient words used per splat (<= 3K)
-    const float* src = coeffs + (size_t)i0 * K * 3;
-    for (int q = t; q < cnt * kn; q += kShBlock) {
-        const int sp = q / kn, col = q - sp * kn;
-        s_c[sp * kn + col] = src[(size_t)sp * K * 3 + col];
-    }
+    const int kw = K * 3;  // words per splat row
+    sh_copy_span(s_c, coeffs + (size_t)i0 * kw, cnt * kw);
     __syncthreads();
     if (t >= cnt) return;
     const int i = i0 + t;
     float b[25];
     sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
-    const float* c = s_c + t * kn - 3 * k0;
+    const float* c = s_c + t * kw - 3 * k0;
     float r0 = 0.f, r1 = 0.f, r2 = 0.f;
     for (int k = k0; k < nb; ++k) {
         r0 = r0 + b[k] * c[3 * k];
@@ -163,8 +175,7 @@ __global__ __launch_bounds__(kShBlock) void sh_bwd_staged_kernel(int n, int degr
         }
     }
     __syncthreads();
-    float* dst = v_coeffs + (size_t)i0 * kw;
-    for (int q = t; q < cnt * kw; q += kShBlock) dst[q] = s_c[q];
+    sh_copy_span(v_coeffs + (size_t)i0 * kw, s_c, cnt * kw);
 }
 
 // One thread per (query, channel-group): query q reads its 4 corner texels.
