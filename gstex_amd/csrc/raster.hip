@@ -181,60 +181,42 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     const Camera cam = load_camera(cam_args);
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
-    // every input loaded up front and waited for once (the compiler otherwise gates them behind the pair count and
-    // sinks half of them below the fp64 arithmetic: three memory round trips per thread); a splat without pairs
-    // is evaluated too and only its store skipped
-    const int cnt = nth[g];
-    const float qv[4] = {quats[4 * g], quats[4 * g + 1], quats[4 * g + 2], quats[4 * g + 3]};
-    const float s0 = scales[3 * g], s1 = scales[3 * g + 1];
-    const float m0 = means[3 * g], m1 = means[3 * g + 1], m2 = means[3 * g + 2];
-    const float cx = centers[2 * g], cy = centers[2 * g + 1], op = opacities[g];
-    const float c0 = rgbs[3 * g], c1 = rgbs[3 * g + 1], c2 = rgbs[3 * g + 2];
-    const float um0 = umap[3 * g], um1 = umap[3 * g + 1], um2 = umap[3 * g + 2];
-    const float vm0 = vmap[3 * g], vm1 = vmap[3 * g + 1], vm2 = vmap[3 * g + 2];
-    const float u0 = uv0[2 * g], v0 = uv0[2 * g + 1];
-    const int th = tdims[3 * g], tw_ = tdims[3 * g + 1], toff = tdims[3 * g + 2];
-    asm volatile("; setup inputs %0 %1 %2 %3 %4 %5 %6 %7 %8 %9 %10 %11 %12 %13 %14 %15" ::"v"(cnt), "v"(qv[0]),
-                 "v"(qv[1]), "v"(qv[2]), "v"(qv[3]), "v"(s0), "v"(s1), "v"(m0), "v"(m1), "v"(m2), "v"(cx), "v"(cy),
-                 "v"(op), "v"(c0), "v"(c1), "v"(c2));
-    asm volatile("; setup inputs %0 %1 %2 %3 %4 %5 %6 %7 %8 %9 %10" ::"v"(um0), "v"(um1), "v"(um2), "v"(vm0),
-                 "v"(vm1), "v"(vm2), "v"(u0), "v"(v0), "v"(th), "v"(tw_), "v"(toff));
+    if (nth[g] <= 0) return;
     // the record is evaluated in fp64 and rounded once per value (one thread per splat, ~100 fp64 operations): its
     // fp32 evaluation was the dominant error of the means / quats gradients (tools/grad_precision.py)
-    const FrameT<double> fr = quat_frame_t<double>(qv);
-    const double su = (double)s0 * (double)glob, sv = (double)s1 * (double)glob;
-    const d3 mu = d3{(double)m0, (double)m1, (double)m2};
+    const FrameT<double> fr = quat_frame_t<double>(quats + 4 * g);
+    const double su = (double)scales[3 * g] * (double)glob, sv = (double)scales[3 * g + 1] * (double)glob;
+    const d3 mu = d3{(double)means[3 * g], (double)means[3 * g + 1], (double)means[3 * g + 2]};
     const AnchoredT<double> h = splat_anchored(cam, mu, su, sv, fr);
     const d3 dir = d3{(double)cam.campos[0] - mu.x, (double)cam.campos[1] - mu.y, (double)cam.campos[2] - mu.z};
     const double sgn = dot3(fr.tw, dir) < 0.0 ? -1.0 : 1.0;
-    const d3 um = d3{(double)um0, (double)um1, (double)um2};
-    const d3 vm = d3{(double)vm0, (double)vm1, (double)vm2};
+    const d3 um = d3{(double)umap[3 * g], (double)umap[3 * g + 1], (double)umap[3 * g + 2]};
+    const d3 vm = d3{(double)vmap[3 * g], (double)vmap[3 * g + 1], (double)vmap[3 * g + 2]};
     float r[GSTEX_REC_FLOATS];
     const AffineHomogT<double> ah = affine_homog(h.Tu, h.Tv, h.Tw);
     r[R_A + 0] = (float)ah.A.x; r[R_A + 1] = (float)ah.A.y; r[R_A + 2] = (float)ah.A.z;
     r[R_B + 0] = (float)ah.B.x; r[R_B + 1] = (float)ah.B.y; r[R_B + 2] = (float)ah.B.z;
     r[R_PZ] = (float)ah.Pz;
     r[R_TW + 0] = (float)h.Tw.x; r[R_TW + 1] = (float)h.Tw.y; r[R_TW + 2] = (float)h.Tw.z;
-    r[R_XY + 0] = cx; r[R_XY + 1] = cy;
-    r[R_OPAC] = op;
-    r[R_RGB + 0] = c0; r[R_RGB + 1] = c1; r[R_RGB + 2] = c2;
+    r[R_XY + 0] = centers[2 * g]; r[R_XY + 1] = centers[2 * g + 1];
+    r[R_OPAC] = opacities[g];
+    r[R_RGB + 0] = rgbs[3 * g]; r[R_RGB + 1] = rgbs[3 * g + 1]; r[R_RGB + 2] = rgbs[3 * g + 2];
     r[R_NRM + 0] = (float)(sgn * fr.tw.x); r[R_NRM + 1] = (float)(sgn * fr.tw.y); r[R_NRM + 2] = (float)(sgn * fr.tw.z);
     // the texture affine in texel units: the sample point (tu h, tv w) = (tu0 + auu u + auv v) h, ... is read as
     // fma(u, auu h, fma(v, auv h, tu0 h)) -- two fused multiply-adds per coordinate instead of three operations
-    const double hd = (double)th, wd = (double)tw_;
-    r[R_TU0] = (float)((double)u0 * hd);
+    const double hd = (double)tdims[3 * g], wd = (double)tdims[3 * g + 1];
+    r[R_TU0] = (float)((double)uv0[2 * g] * hd);
     r[R_AUU] = (float)(su * dot3(fr.tu, um) * hd);
     r[R_AUV] = (float)(sv * dot3(fr.tv, um) * hd);
-    r[R_TV0] = (float)((double)v0 * wd);
+    r[R_TV0] = (float)((double)uv0[2 * g + 1] * wd);
     r[R_AVU] = (float)(su * dot3(fr.tu, vm) * wd);
     r[R_AVV] = (float)(sv * dot3(fr.tv, vm) * wd);
-    r[R_H] = __int_as_float(th);
-    r[R_W] = __int_as_float(tw_);
-    if (cnt <= 0) return;
+    r[R_H] = __int_as_float(tdims[3 * g]);
+    r[R_W] = __int_as_float(tdims[3 * g + 1]);
     // near-edge-on: the fp64 pair-evaluation inputs for the backward, and the flag
     const double dn = sqrt(dot3(dir, dir));
     const bool hp = rec_hp && dn > 0.0 && fabs(dot3(fr.tw, dir)) < kHpCos * dn;
-    r[R_OFF] = __uint_as_float((uint32_t)toff | (hp ? kHpFlag : 0u));
+    r[R_OFF] = __uint_as_float((uint32_t)tdims[3 * g + 2] | (hp ? kHpFlag : 0u));
     if (hp) {
         double* q = rec_hp + (size_t)g * kHpDoubles;
         q[0] = ah.A.x; q[1] = ah.A.y; q[2] = ah.A.z;
@@ -243,8 +225,8 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     }
     r[R_XA] = (float)h.xa;
     r[R_YA] = (float)h.ya;
-    r[R_HM1] = (float)(th - 1);
-    r[R_WM1] = (float)(tw_ - 1);
+    r[R_HM1] = (float)(tdims[3 * g] - 1);
+    r[R_WM1] = (float)(tdims[3 * g + 1] - 1);
     float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
 #pragma unroll
     for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
