@@ -74,8 +74,6 @@ def parse():
     p.add_argument("--no-defer-texture", action="store_true",
                    help="run the texel Adam update inside optimizer_step instead of deferring it into the next "
                         "step's render (GStexTrainer defer_texture)")
-    p.add_argument("--async-texture", action="store_true",
-                   help="texel Adam update on a side stream, overlapping the next step (measured: no net gain)")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="diagnostics only: no HIP events around the raster launches (no roofline figures)")
@@ -263,8 +261,7 @@ def main():
     scene = make_scene(args.n_splats, args.n_texels, seed=args.seed)
     views = [sphere_view(i, H, W, n_views=N_POSES).to(dev) for i in range(N_POSES)]
     # start_step = 3 x sh_degree_interval: SH at its full degree 3 (the regime of 12k of the 15k iterations)
-    trainer = GStexTrainer(scene, dev, start_step=3000, async_texture=args.async_texture,
-                           defer_texture=not (args.async_texture or args.no_defer_texture))
+    trainer = GStexTrainer(scene, dev, start_step=3000, defer_texture=not args.no_defer_texture)
     sync = GradSync(trainer, world) if world > 1 else None
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     gts = [torch.rand((H, W, 3), generator=g).to(dev) for _ in range(N_POSES)]
@@ -490,9 +487,7 @@ def main():
             "pair_buffers": ("capacity-sized, pair total kept on the device: no host read-back or synchronisation in "
                              "the step (ops.PairCapacity, capacity %d)" % trainer.pairs.capacity
                              if trainer.pairs is not None else "sized by a host read-back of the pair total"),
-            "texture_update": ("side stream: the texel Adam update (zeroing its gradient) overlaps the next step's "
-                               "preprocessing and binning; the raster forward waits for it" if trainer.async_texture
-                               else "deferred: step k's texel Adam update runs in step k+1's render (same stream, "
+            "texture_update": ("deferred: step k's texel Adam update runs in step k+1's render (same stream, "
                                     "before the raster forward); the timed region holds exactly K texel updates"
                                if trainer.defer_texture
                                else "compute stream"),

@@ -16,9 +16,8 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 REC_FLOATS = 32
-BWD_ORDERED = 1 << 30  # GSTEX_BWD_ORDERED: gstex_raster_bwd skips the unit ordering
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
 SETTING_AA_BLUR = 1 << 9
@@ -106,10 +105,6 @@ SIGNATURES = {
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
     ),
-    "gstex_raster_setup_hp": (
-        c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P],
-    ),
     "gstex_raster_fwd": (
         c_int32,
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
@@ -120,7 +115,6 @@ SIGNATURES = {
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, c_int64, _P, c_int64, _P],
     ),
-    "gstex_raster_bwd_order": (c_int32, [_CAM, c_int32, c_int64, _P, _P]),
     "gstex_raster_aux_bytes": (c_size_t, [c_int64, c_int32, c_int32]),
     "gstex_unit_order": (c_int32, [c_int32, _P, _P, _P, _P]),
     "gstex_unit_order_scratch_words": (c_size_t, []),
@@ -129,18 +123,15 @@ SIGNATURES = {
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, _P, _P, _P],
     ),
-    "gstex_raster_bwd_hp": (
-        c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
-         c_int64, _P, _P, _P, _P, _P, _P],
-    ),
     "gstex_raster_setup_bwd": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, c_int64, _CAM, _P, _P, _P, _P, _P, _P, _P,
+         _P],
     ),
     "gstex_raster_setup_bwd_aabb": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, _CAM, _P, _P, _P, _P, _P, _P, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, c_int64, _CAM, _P, _P, _P, _P, _P, _P, _P,
+         _P],
     ),
     "gstex_sh_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),
     "gstex_sh_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P]),

@@ -13,10 +13,11 @@
 //   * backward: one wave64 workgroup per unit = (tile, 8x8 quadrant, segment), launched costliest first, no
 //     barriers and no shared state between waves; a unit starts from the forward's checkpoint after its
 //     segment and walks back to front; per visit the 24 splat partials are reduced across the wave with a
-//     reduce-scatter butterfly (permlane32/16 swaps + DPP) and stored as the (pair, quadrant) row at the
-//     pair's emission slot (summed in fixed order by setup_bwd: bitwise reproducible, no float atomics);
-//     texel gradients go through a DPP segmented scan, int32 fixed-point LDS staging of the splat's block
-//     and a flush of its non-zero entries with global fp32 atomics.
+//     reduce-scatter butterfly (permlane32/16 swaps + DPP) and added into the splat's accumulator row with one
+//     coalesced float-atomic instruction (deterministic mode: stored as the (pair, quadrant) row at the pair's
+//     emission slot and summed in fixed order by setup_bwd); texel gradients go through a DPP segmented scan,
+//     int32 fixed-point LDS staging of the splat's block and a flush of its non-zero entries with global fp32
+//     atomics.
 #include "gstex_common.h"
 #include "gstex_error.h"
 
@@ -28,22 +29,16 @@ constexpr int kThreads = kTilePixels;  // 256
 #ifndef GSTEX_FWD_BATCH
 #define GSTEX_FWD_BATCH 128
 #endif
-#ifndef GSTEX_WAVE_8X8
-#define GSTEX_WAVE_8X8 1  // each wave covers an 8x8 quadrant of the tile (0: 16x4 rows)
-#endif
 #ifndef GSTEX_SEG_W
-// texel-gradient segment width in lanes: half a pixel row (8x8 waves; 2 scan steps, twice the run tails of a
-// whole row: measured 4% faster backward than 8, 2 is slower again)
-#define GSTEX_SEG_W (GSTEX_WAVE_8X8 ? 4 : 16)
+// texel-gradient segment width in lanes: half a pixel row of the 8x8 quadrant (2 scan steps, twice the run tails of
+// a whole row: measured 4% faster backward than 8, 2 is slower again)
+#define GSTEX_SEG_W 4
 #endif
 #ifndef GSTEX_FAST_RCP
 #define GSTEX_FAST_RCP 1  // v_rcp_f32 for backward divisions that feed no threshold decision
 #endif
 #ifndef GSTEX_FAST_EVAL
 #define GSTEX_FAST_EVAL 1  // hardware v_exp_f32 / v_rcp_f32 in the pair evaluation (0: expf sequence, IEEE division)
-#endif
-#ifndef GSTEX_UNIT_FLAT
-#define GSTEX_UNIT_FLAT 0  // experiment: backward units in (XCD group, slot) order, costs ignored
 #endif
 #ifndef GSTEX_UNIT_COARSE
 #define GSTEX_UNIT_COARSE 3  // backward unit-order cost buckets of 2^k visits (inside a bucket: about slot order,
@@ -77,25 +72,8 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_FWD_OCC
 #define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower)
 #endif
-#ifndef GSTEX_FWD_WAVES
-#define GSTEX_FWD_WAVES 0
-#endif
-#if GSTEX_FWD_WAVES > 0
-#define GSTEX_FWD_ATTR __attribute__((amdgpu_num_vgpr((512 / GSTEX_FWD_WAVES) / 8 * 8 / 2)))
-#else
-#define GSTEX_FWD_ATTR
-#endif
-#ifndef GSTEX_CONIC_CULL
-#define GSTEX_CONIC_CULL 1  // per-wave ellipse-vs-rectangle cull on top of the contribution box
-#endif
 #ifndef GSTEX_XCD_MB
-#define GSTEX_XCD_MB 2
-#endif
-#ifndef GSTEX_XCD_GROUPS
-#define GSTEX_XCD_GROUPS 1  // backward units of one 2x2-tile macro-block dispatched to one XCD (unit_order groups)
-#endif
-#ifndef GSTEX_REC_SGPR
-#define GSTEX_REC_SGPR 1  // backward reads splat records into SGPRs (wave-uniform) instead of VGPRs
+#define GSTEX_XCD_MB 2  // backward units of one 2x2-tile macro-block dispatched to one XCD (unit_order groups)
 #endif
 // Backward occupancy: waves per SIMD the register allocation targets, per instantiation.  The photometric
 // training variant (C = 3, no geometry gradients) fits 7 (72 VGPRs, no spills; 8 forces 64 VGPRs with scratch
@@ -120,9 +98,6 @@ struct BwdShape {
 #endif
 constexpr int kTexStage = GSTEX_TEX_STAGE;
 constexpr int kFwdBatch = GSTEX_FWD_BATCH;
-#ifndef GSTEX_ZERO_END
-#define GSTEX_ZERO_END 0  // forward: the texel-gradient buffer's zero stores after the tile's visit loop (0: before it)
-#endif
 #ifndef GSTEX_FWD_DEFER
 #define GSTEX_FWD_DEFER 1
 #endif
@@ -135,33 +110,9 @@ constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in
                         // (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
-// Near-edge-on splats (|normal . view direction| < kHpCos at the centre): (u, v) = p.xy / p.z is ill-conditioned in
-// the stored fp32 A, B, Pz -- their rounding alone left the means / quats gradients at ~5e-5.  For
-// those splats setup also writes A, B, Pz and the anchor in fp64 (GSTEX_HP_DOUBLES per splat, rec_hp) and flags the
-// record (bit 31 of R_OFF); the backward re-evaluates dx, dy, 1 / p.z, u, v from them in fp64 for the gradient
-// arithmetic, while every pair decision (alpha, depth, branch) stays the forward's fp32 one.  Measured on the cfg3
-// 96x96 window with the oracle (tools/grad_precision.py --hp-cos): 1.7 % of the splats at 0.02, 4.3 % at 0.05;
-// means / quats 4.9e-5 / 4.3e-5 -> 2.3e-6 / 1.9e-6 at 0.05.
-#ifndef GSTEX_HP
-#define GSTEX_HP 0  // 1: the backward reads rec_hp (the fp64 near-edge-on experiment, with GSTEX_HP_RECORD=1: measured
-                    // not to close the fp32-record floor)
-#endif
-#ifndef GSTEX_STAGE_DMA
-#define GSTEX_STAGE_DMA 0  // forward: a batch's records staged by LDS-DMA (global_load_lds_dwordx4; measured: no change, 0.525 -> 0.527 ms)
-#endif
-constexpr bool kStageDma = GSTEX_STAGE_DMA;
-static_assert(!GSTEX_STAGE_DMA || (kFwdBatch == 128 && kRecF4 == 8 && kThreads == 256),
-              "DMA staging: 4 waves x 2 planes x 2 halves of 64 splats");
 #ifndef GSTEX_WORD_WAIT
 #define GSTEX_WORD_WAIT 1  // backward: the visit loop's id wait hoisted to the word start (see raster_bwd_kernel)
 #endif
-#ifndef GSTEX_HP_COS
-#define GSTEX_HP_COS 0.05
-#endif
-constexpr double kHpCos = GSTEX_HP_COS;
-constexpr int kHpDoubles = 10;  // A.xyz, B.xyz, Pz, xa, ya, (pad)
-constexpr unsigned kHpFlag = 0x80000000u;
-constexpr int kRowStride = GSTEX_PARTIAL_FLOATS;  // 32 floats between partial rows
 
 // ------------------------------------------------------------------------------------------
 // setup: per-splat record
@@ -177,7 +128,7 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
                                                     const float* __restrict__ vmap,
                                                     const int32_t* __restrict__ tdims,
                                                     const int32_t* __restrict__ nth, CamArgs cam_args,
-                                                    float* __restrict__ rec_out, double* __restrict__ rec_hp) {
+                                                    float* __restrict__ rec_out) {
     const Camera cam = load_camera(cam_args);
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
@@ -213,16 +164,7 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     r[R_AVV] = (float)(sv * dot3(fr.tv, vm) * wd);
     r[R_H] = __int_as_float(tdims[3 * g]);
     r[R_W] = __int_as_float(tdims[3 * g + 1]);
-    // near-edge-on: the fp64 pair-evaluation inputs for the backward, and the flag
-    const double dn = sqrt(dot3(dir, dir));
-    const bool hp = rec_hp && dn > 0.0 && fabs(dot3(fr.tw, dir)) < kHpCos * dn;
-    r[R_OFF] = __uint_as_float((uint32_t)tdims[3 * g + 2] | (hp ? kHpFlag : 0u));
-    if (hp) {
-        double* q = rec_hp + (size_t)g * kHpDoubles;
-        q[0] = ah.A.x; q[1] = ah.A.y; q[2] = ah.A.z;
-        q[3] = ah.B.x; q[4] = ah.B.y; q[5] = ah.B.z;
-        q[6] = ah.Pz; q[7] = h.xa; q[8] = h.ya; q[9] = 0.0;
-    }
+    r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
     r[R_XA] = (float)h.xa;
     r[R_YA] = (float)h.ya;
     r[R_HM1] = (float)(tdims[3 * g] - 1);
@@ -242,7 +184,6 @@ struct Rec {
     float rgb[3], nrm[3];
     float tu0, auu, auv, tv0, avu, avv;
     int h, w, off;
-    bool hp;  // near-edge-on: fp64 inputs in rec_hp for the backward (bit 31 of R_OFF)
     float xa, ya;
     float hm1, wm1;  // (float)(h - 1), (float)(w - 1)
 };
@@ -261,21 +202,11 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.opac = v[R_OPAC];
     r.rgb[0] = v[R_RGB]; r.rgb[1] = v[R_RGB + 1]; r.rgb[2] = v[R_RGB + 2];
     r.tu0 = v[R_TU0]; r.auu = v[R_AUU]; r.auv = v[R_AUV]; r.tv0 = v[R_TV0]; r.avu = v[R_AVU]; r.avv = v[R_AVV];
-    r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = (int)(__float_as_uint(v[R_OFF]) & ~kHpFlag);
-    r.hp = (__float_as_uint(v[R_OFF]) & kHpFlag) != 0u;
+    r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = __float_as_int(v[R_OFF]);
     r.xa = v[R_XA]; r.ya = v[R_YA];
     r.nrm[0] = v[R_NRM]; r.nrm[1] = v[R_NRM + 1]; r.nrm[2] = v[R_NRM + 2];
     r.hm1 = v[R_HM1]; r.wm1 = v[R_WM1];
     return r;
-}
-
-template <bool SGPR>
-__device__ __forceinline__ float4 uni4(float4 v) {  // wave-uniform value -> SGPRs
-    if (!SGPR) return v;
-    return make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
-                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
-                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
-                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w))));
 }
 
 // Pixel of thread tid inside a 16x16 tile and the wave's block of pixel centres.
@@ -283,27 +214,20 @@ struct WaveBlock { int px, py; float wx0, wx1, wy0, wy1; };
 __device__ __forceinline__ WaveBlock wave_block(int tx, int ty, int tid) {
     WaveBlock b;
     const int w = tid >> 6, l = tid & 63;
-    int ox, oy, bw, bh;
-    if (GSTEX_WAVE_8X8) { ox = (w & 1) * 8 + (l & 7); oy = (w >> 1) * 8 + (l >> 3); bw = 8; bh = 8; }
-    else { ox = l & 15; oy = 4 * w + (l >> 4); bw = 16; bh = 4; }
-    b.px = tx * kTile + ox;
-    b.py = ty * kTile + oy;
-    b.wx0 = (float)(tx * kTile + (GSTEX_WAVE_8X8 ? (w & 1) * 8 : 0)) + 0.5f;
-    b.wy0 = (float)(ty * kTile + (GSTEX_WAVE_8X8 ? (w >> 1) * 8 : 4 * w)) + 0.5f;
-    b.wx1 = b.wx0 + (float)(bw - 1);
-    b.wy1 = b.wy0 + (float)(bh - 1);
+    b.px = tx * kTile + (w & 1) * 8 + (l & 7);  // wave w covers the 8x8 quadrant (w & 1, w >> 1)
+    b.py = ty * kTile + (w >> 1) * 8 + (l >> 3);
+    b.wx0 = (float)(tx * kTile + (w & 1) * 8) + 0.5f;
+    b.wy0 = (float)(ty * kTile + (w >> 1) * 8) + 0.5f;
+    b.wx1 = b.wx0 + 7.0f;
+    b.wy1 = b.wy0 + 7.0f;
     return b;
 }
 
-// SGPR: move the (wave-uniform) record into scalar registers; frees ~30 VGPRs where the register
-// file, not issue, limits occupancy (backward), at the cost of one v_readfirstlane per value
-template <int NB, bool SGPR = false>
+// Record j of a batch staged in LDS as [plane][splat] float4
+template <int NB>
 __device__ __forceinline__ Rec read_rec(const float4* s, int j) {
-    const float4 a = uni4<SGPR>(s[0 * NB + j]), b = uni4<SGPR>(s[1 * NB + j]);
-    const float4 c = uni4<SGPR>(s[2 * NB + j]), d = uni4<SGPR>(s[3 * NB + j]);
-    const float4 e = uni4<SGPR>(s[4 * NB + j]), f = uni4<SGPR>(s[5 * NB + j]);
-    const float4 g = uni4<SGPR>(s[6 * NB + j]), q = uni4<SGPR>(s[7 * NB + j]);
-    return rec_from_planes(a, b, c, d, e, f, g, q);
+    return rec_from_planes(s[0 * NB + j], s[1 * NB + j], s[2 * NB + j], s[3 * NB + j], s[4 * NB + j], s[5 * NB + j],
+                           s[6 * NB + j], s[7 * NB + j]);
 }
 
 // Visit-mask layout: tile t owns 64-bit words [ceil(start_t / 64) + t, + ceil(len_t / 64)) (disjoint across tiles);
@@ -410,7 +334,6 @@ __device__ __forceinline__ bool may_hit_planes(float4 p0, float4 p1, float4 p2, 
     }
     const float xa = v[R_XA], ya = v[R_YA];
     if (xa >= x0 && xa <= x1 && ya >= y0 && ya <= y1) return true;
-    if (!GSTEX_CONIC_CULL) return true;
     const float Ax = v[R_A], Ay = v[R_A + 1], Az = v[R_A + 2], Bx = v[R_B], By = v[R_B + 1], Bz = v[R_B + 2];
     const float Pz = v[R_PZ];
     const float dx0 = x0 - xa, dx1 = x1 - xa, dy0 = y0 - ya, dy1 = y1 - ya;
@@ -623,24 +546,11 @@ __device__ __forceinline__ float tex_accum(float acc, float v00, float v01, floa
 }
 // GEOF = false: depth / distortion / normal not produced (their outputs are NULL: a caller whose loss does
 // not use them, e.g. the photometric training step); every other output is computed unchanged.
-// ONE = true (GSTEX_FWD_WAVE=1, an experiment): one wave64 workgroup per (tile, 8x8 quadrant) -- no barriers, no record
-// staging shared between the quadrants; each wave culls a 64-position word of the tile list at a time (lane k tests
-// position k from the record's first three planes, the cull fields) and reads each visited record with scalar loads
-// (as the backward does).  ONE = false (the default): one 256-thread workgroup per tile whose four quadrant waves share
-// 128-record batches staged in LDS (barrier per batch) -- 12 % faster: the shared staging reads each record once per
-// tile instead of once per quadrant and the quadrants' culls read LDS instead of gathering 48 B per candidate.
-template <bool ONE> struct FwdShape;
-template <> struct FwdShape<false> { static constexpr int kThr = kThreads, kStep = kFwdBatch; };
-template <> struct FwdShape<true> { static constexpr int kThr = 64, kStep = 64; };
-#ifndef GSTEX_FWD_WAVE
-#define GSTEX_FWD_WAVE 0  // measured at cfg3 (round 3): single-wave 0.666 ms (6 waves/SIMD), 0.677 (7), 0.752 (8) vs 0.592
-#endif
-#ifndef GSTEX_FWD1_OCC
-#define GSTEX_FWD1_OCC 8  // single-wave forward: waves per SIMD the register allocation targets
-#endif
-
-template <int C, bool GEOF, bool ONE>
-__global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_FWD_OCC) GSTEX_FWD_ATTR void raster_fwd_kernel(
+// One 256-thread workgroup per tile; its four quadrant waves share 128-record batches staged in LDS (a barrier per
+// batch).  (One wave64 workgroup per (tile, quadrant) with scalar record loads measured 12 % slower in round 3: the
+// shared staging reads each record once per tile instead of once per quadrant.)
+template <int C, bool GEOF>
+__global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, int n_texels, float tex_scale,
@@ -671,20 +581,15 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
             }
         }
     };
-    if (!GSTEX_ZERO_END) zero_grad_buf();
+    zero_grad_buf();
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
-    constexpr int kThr = FwdShape<ONE>::kThr, kStep = FwdShape<ONE>::kStep, kWords = kStep / 64;
-    __shared__ float4 s_rec[ONE ? 1 : kRecF4 * kFwdBatch];
-    // ONE: tile i of the largest-first order takes blocks 32 (i / 8) + 8 q + i % 8, q = quadrant, so the four quadrants
-    // of a tile are dispatched to one XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2
-    const int bidx = (int)blockIdx.x;
-    const int ti = ONE ? (bidx >> 5) * 8 + (bidx & 7) : bidx;
-    const int tq = ONE ? (bidx >> 3) & 3 : 0;
-    if (ti >= n_tiles) return;  // ONE: the grid is rounded up to whole groups of 8 tiles
+    constexpr int kStep = kFwdBatch, kWords = kStep / 64;
+    __shared__ float4 s_rec[kRecF4 * kFwdBatch];
+    const int ti = (int)blockIdx.x;
     const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int tid = ONE ? tq * 64 + (int)threadIdx.x : (int)threadIdx.x;
+    const int tid = (int)threadIdx.x;
     const WaveBlock wb = wave_block(tx, ty, tid);
     const int pxi = wb.px, pyi = wb.py;
     const bool inside = pxi < cam.W && pyi < cam.H;
@@ -740,10 +645,10 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
     const int sbase = seg_base(rng.x, tile);
     int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
     // XCD group of the tile's backward units: its GSTEX_XCD_MB x GSTEX_XCD_MB-tile macro-block
-    const int xgroup = GSTEX_XCD_GROUPS
-        ? (((tx / GSTEX_XCD_MB) + (ty / GSTEX_XCD_MB) * ((tiles_x + GSTEX_XCD_MB - 1) / GSTEX_XCD_MB)) & 7) << 24 : 0;
-    if (aux.slot_tile && (!ONE || tq == 0))
-        for (int k = (int)threadIdx.x; k * kSegLen < rng.y - rng.x; k += kThr) aux.slot_tile[sbase + k] = tile;
+    const int xgroup = (((tx / GSTEX_XCD_MB) + (ty / GSTEX_XCD_MB) * ((tiles_x + GSTEX_XCD_MB - 1) / GSTEX_XCD_MB)) & 7)
+                       << 24;
+    if (aux.slot_tile)
+        for (int k = tid; k * kSegLen < rng.y - rng.x; k += kThreads) aux.slot_tile[sbase + k] = tile;
     // one checkpoint record: field f of the wave's lane at ckpt[((slot * 4 + wave) * F + f) * 64 + lane]
     auto write_ck = [&](int slot) {
         float* ck = aux.ckpt + ((size_t)slot * 4 + wave) * aux.F * 64 + lane;
@@ -770,7 +675,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
             // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
             const int cnt = wave_max_i(seg_visits);  // lanes leave the visit loop as they finish: the wave's count
             if (lane == 0 && cnt) {
-                const int key = (GSTEX_UNIT_FLAT ? 1 : ((cnt >> GSTEX_UNIT_COARSE) + 1)) | xgroup;
+                const int key = ((cnt >> GSTEX_UNIT_COARSE) + 1) | xgroup;
                 aux.cost[(sbase + cur_seg) * 4 + wave] = key;
                 atomicAdd(&aux.order_ws[unit_bin(key)], 1);  // the backward's unit-order histogram
             }
@@ -780,50 +685,18 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
             ++cur_seg;
         }
         const int nb = min(kStep, rng.y - b0);
-        int my_gid = 0;  // ONE: lane k <-> position b0 + k
-        if constexpr (ONE) {
-            if (__all(GSTEX_FWD_DONE)) break;
-            if (lane < nb) my_gid = sorted_ids[b0 + lane];
-        } else {
-            if (__syncthreads_count(GSTEX_FWD_DONE ? 1 : 0) == kThreads) break;
-            if constexpr (kStageDma) {
-                // LDS-DMA staging: wave w fills planes 2w and 2w + 1, each as two 64-splat halves (one
-                // global_load_lds_dwordx4 per half: lane l's 16 B land at the half's base + 16 l, i.e. s_rec[k][h 64 +
-                // l]).  Two memory round trips per batch (the ids, then the four DMAs, drained by the barrier) and no
-                // VGPRs for the data; the register form waits for each id, then each plane.  Past the list's end the
-                // last entry is loaded again (never read: the waves look at j < nb only).
-                const int jl = rng.y - 1 - b0;
-                const int id0 = sorted_ids[b0 + min(lane, jl)], id1 = sorted_ids[b0 + min(64 + lane, jl)];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int k = 2 * wave + (i >> 1), h = i & 1;
-                    const float4* src = records + (size_t)(h ? id1 : id0) * kRecF4 + k;
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                     (__attribute__((address_space(3))) void*)&s_rec[k * kFwdBatch + h * 64],
-                                                     16, 0, 0);
-                }
-            } else {
-                for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
-                    const int j = q / kRecF4, k = q % kRecF4;
-                    if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
-                }
-            }
-            __syncthreads();
+        if (__syncthreads_count(GSTEX_FWD_DONE ? 1 : 0) == kThreads) break;
+        for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
+            const int j = q / kRecF4, k = q % kRecF4;
+            if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
         }
+        __syncthreads();
         // the batch splats whose contribution region meets this wave's 8x8 block, tested all at once
         unsigned long long todo[kWords];
 #pragma unroll
         for (int hb = 0; hb < kWords; ++hb) {
             const int jj = hb * 64 + lane;
-            bool hit = false;
-            if constexpr (ONE) {
-                if (jj < nb) {
-                    const float4* rc = records + (size_t)my_gid * kRecF4;
-                    hit = may_hit_planes(rc[0], rc[1], rc[2], wx0, wx1, wy0, wy1, aa);
-                }
-            } else {
-                hit = jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa);
-            }
+            const bool hit = jj < nb && wave_may_hit<kFwdBatch>(s_rec, jj < nb ? jj : 0, wx0, wx1, wy0, wy1, aa);
             todo[hb] = __ballot(hit);
             GSTEX_STAT(8, (unsigned long long)max(0, min(64, nb - hb * 64)));  // cull candidates (wave, splat)
             GSTEX_STAT(9, __popcll(todo[hb]));                                 // passing the wave's cull
@@ -841,9 +714,7 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
             ++seg_visits;
-            Rec r;
-            if constexpr (ONE) r = read_rec_global(records + (size_t)__builtin_amdgcn_readlane(my_gid, j) * kRecF4);
-            else r = read_rec<kFwdBatch>(s_rec, j);
+            const Rec r = read_rec<kFwdBatch>(s_rec, j);
             Hit h;
             const bool ok = eval_hit(r, px, py, aa, h) && alive != 0.0f;
             const float test_T = T * (1.0f - h.alpha);
@@ -910,11 +781,10 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
         }
     }
     fold_pending();
-    if (GSTEX_ZERO_END) zero_grad_buf();
     if (aux.cost) {
         const int cnt = wave_max_i(seg_visits);
         if (lane == 0 && cnt) {
-            const int key = (GSTEX_UNIT_FLAT ? 1 : ((cnt >> GSTEX_UNIT_COARSE) + 1)) | xgroup;
+            const int key = ((cnt >> GSTEX_UNIT_COARSE) + 1) | xgroup;
             aux.cost[(sbase + cur_seg) * 4 + wave] = key;
             atomicAdd(&aux.order_ws[unit_bin(key)], 1);
         }
@@ -959,19 +829,9 @@ __global__ __launch_bounds__(FwdShape<ONE>::kThr, ONE ? GSTEX_FWD1_OCC : GSTEX_F
 // xor-32 and xor-16 halvings with v_permlane32_swap / v_permlane16_swap, xor-8 with DPP row_ror:8,
 // then an 8-lane all-reduce (quad_perm xor1, xor2, row_half_mirror).  On return, lane l with
 // (l & 7) == 0 holds the wave sums of values [NV/2 b5 + NV/4 b4 + NV/8 b3 + 0 .. NV/8 - 1] (b5,b4,b3 = bits of l).
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    // every pattern used here reads a lane inside the same row, so the old value never shows: mov_dpp
-    // (undefined old) needs no zero materialised and folds into the consuming add
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-#ifndef GSTEX_DPP_ASM
-#define GSTEX_DPP_ASM 1
-#endif
 template <int NV>
 __device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
-    static_assert(NV % 8 == 0, "reduce-scatter over 8 lane groups");
+    static_assert(NV == 24 || NV == 32, "reduce-scatter over 8 lane groups of 3 or 4 values");
     constexpr int H = NV / 2, Q = NV / 4, E = NV / 8;
     const int lane = threadIdx.x & 63;
     // permlane32_swap(a, b) leaves a = [a_lo, b_lo], b = [a_hi, b_hi]: a + b holds a's half-sum in
@@ -986,7 +846,7 @@ __device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
         const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + Q]), false, false);
         v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
-    if (GSTEX_DPP_ASM && (E == 3 || E == 4)) {
+    {
         // the last four stages as single v_add_f32_dpp instructions (the compiler emits a DPP move plus an add):
         // row_ror:8 (lane ^ 8 inside a 16-lane row), quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror (the other
         // quad of the 8-lane group).  dpp(x) + y rounds as y + dpp(x).  The leading s_nop covers the VALU-write ->
@@ -1031,22 +891,6 @@ __device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
 #undef GSTEX_DPP_SELF
 #pragma unroll
         for (int i = 0; i < E; ++i) v[i] = keep[i];
-        return;
-    }
-    {
-        const bool hi = lane & 8;
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-            const float send = hi ? v[i] : v[i + E];
-            const float keep = hi ? v[i + E] : v[i];
-            v[i] = keep + dpp_f<0x128>(send);  // row_ror:8 == lane ^ 8 inside a 16-lane row
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-        v[i] = v[i] + dpp_f<0xB1>(v[i]);   // quad_perm [1,0,3,2]
-        v[i] = v[i] + dpp_f<0x4E>(v[i]);   // quad_perm [2,3,0,1]
-        v[i] = v[i] + dpp_f<0x141>(v[i]);  // row_half_mirror: the other quad of the 8-lane group
     }
 }
 
@@ -1056,10 +900,6 @@ __device__ __forceinline__ void wave_reduce(float (&v)[NV]) {
 // by cell key with DPP row shifts leaves each run's sum in its last lane; only run tails issue
 // the 4*C atomics (instead of every contributing lane, which serialised on the LDS atomic unit).
 // ------------------------------------------------------------------------------------------
-template <int OFF>
-__device__ __forceinline__ int dpp_shr_i(int old, int v) {
-    return __builtin_amdgcn_update_dpp(old, v, 0x110 + OFF, 0xF, 0xF, false);
-}
 // row_shr:OFF with out-of-row lanes reading 0 (bound_ctrl)
 template <int CTRL>
 __device__ __forceinline__ int dpp_bc_i(int v) {
@@ -1070,9 +910,6 @@ __device__ __forceinline__ float dpp_shr_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x110 + OFF, 0xF, 0xF, false));
 }
 
-#ifndef GSTEX_SEG_FMA
-#define GSTEX_SEG_FMA 1
-#endif
 // v += row_shr:OFF(v) * mf, mf = 1 where the lane OFF to the left is in the same segment, else 0: one
 // v_fmac_f32 with a DPP source per value (the compiler does not fold a DPP move into the tied-accumulator
 // fmac, so it is written out).  fma(t, 1, v) rounds as t + v and fma(t, 0, v) = v, so the result equals the
@@ -1090,25 +927,6 @@ __device__ __forceinline__ void fmac_dpp_shr(float& v, float mf) {
     else
         asm volatile("v_fmac_f32_dpp %0, %0, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(v) : "v"(mf));
 }
-template <int NV, int OFF>
-__device__ __forceinline__ void seg_step(int seg, float (&v)[NV]) {
-    const int ss = dpp_bc_i<0x110 + OFF>(seg);  // segment ids are >= 1: an out-of-row 0 never matches
-    const bool m = (ss == seg);
-    if (GSTEX_SEG_FMA) {
-        const float mf = m ? 1.0f : 0.0f;
-        asm volatile("s_nop 1" ::: "memory");
-#pragma unroll
-        for (int i = 0; i < NV; ++i) fmac_dpp_shr<OFF>(v[i], mf);
-        asm volatile("s_nop 1" ::: "memory");
-    } else {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            const float t = dpp_shr_f<OFF>(v[i]);
-            v[i] = m ? v[i] + t : v[i];
-        }
-    }
-}
-
 // Segments = maximal runs of equal key inside a 16-lane row (a lane whose key differs from its left
 // neighbour starts a segment, so a non-contributing lane splits a run instead of being bridged).
 // Returns true for the last lane of a segment with key >= 0; it then holds the segment's sums.
@@ -1118,14 +936,11 @@ __device__ __forceinline__ float mask_one(unsigned long long m) {
     asm("v_cndmask_b32_e64 %0, 0, 1.0, %1" : "=v"(r) : "s"(m));
     return r;
 }
-#ifndef GSTEX_SEG_MASK
-#define GSTEX_SEG_MASK 1
-#endif
-// Mask form (GSTEX_SEG_MASK): the segment heads as one wave mask H (ballot of key changes, plus every group's first
+// The segment heads as one wave mask H (ballot of key changes, plus every group's first
 // lane); lane l joins lane l - OFF iff no head lies in (l - OFF, l], i.e. bit l of ~(H | H << 1 | ... | H << (OFF-1)),
 // computed on the scalar unit; the run tails are the lanes before a head or at a group's end.
 template <int NV>
-__device__ __forceinline__ bool seg_reduce_rows_mask(int key, float (&v)[NV]) {
+__device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     constexpr int SW = GSTEX_SEG_W;
     static_assert(SW == 2 || SW == 4 || SW == 8 || SW == 16, "segment width");
     constexpr unsigned long long kFirst = SW == 2 ? 0x5555555555555555ull : SW == 4 ? 0x1111111111111111ull
@@ -1153,35 +968,15 @@ __device__ __forceinline__ bool seg_reduce_rows_mask(int key, float (&v)[NV]) {
     return mask_one(tails) != 0.0f;
 }
 
-template <int NV>
-__device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
-    if (GSTEX_SEG_MASK) return seg_reduce_rows_mask<NV>(key, v);
-    constexpr int SW = GSTEX_SEG_W;
-    const int pos = threadIdx.x & (SW - 1);
-    const int left = dpp_bc_i<0x111>(key);  // unused at pos 0 (a forced head)
-    int seg = (pos == 0 || left != key) ? 1 : 0;  // head flag: group start or key change
-    // segment id = inclusive prefix count of heads over the whole 16-lane DPP row (a shorter window would
-    // give two lanes of one segment different counts); the forced head at pos 0 separates groups
-    seg += dpp_shr_i<1>(0, seg);
-    seg += dpp_shr_i<2>(0, seg);
-    seg += dpp_shr_i<4>(0, seg);
-    seg += dpp_shr_i<8>(0, seg);
-    seg_step<NV, 1>(seg, v);
-    seg_step<NV, 2>(seg, v);
-    if (SW > 4) seg_step<NV, 4>(seg, v);
-    if (SW > 8) seg_step<NV, 8>(seg, v);
-    const int ns = dpp_bc_i<0x101>(seg);  // row_shl:1; 0 past the row end (ids are >= 1)
-    return key >= 0 && (ns != seg || pos == SW - 1);
-}
-
 // Backward: one wave64 workgroup per (tile, 8x8 quadrant) -- the 4 quadrant waves of a tile share nothing, so
 // no wave ever waits for another (no barriers; a finished wave frees its slot at once).  The wave walks the
 // tile list back to front over the forward's cull bits for its quadrant, up to its last contributor.  Per
-// visited splat it reduces its 24 gradient partials across its 64 pixels and stores them with plain stores as
-// the (pair, quadrant) row partials[slot][quadrant] (slot = the pair's emission slot), flagging the row in
-// row_flags[slot] (byte = quadrant; rows never written stay unflagged and are never read);
-// gstex_raster_setup_bwd sums each splat's flagged rows in (slot, quadrant) order -> bitwise reproducible,
-// no float atomics for splat gradients.  Texel gradients: segmented scan along each 8-pixel row, run tails
+// visited splat it reduces its 24 gradient partials across its 64 pixels and adds them into the splat's accumulator
+// row with one float-atomic instruction; in the deterministic mode (row_flags given) it stores them instead as the
+// (pair, quadrant) row partials[slot][quadrant] (slot = the pair's emission slot), flagging the row in
+// row_flags[slot] (byte = quadrant; rows never written stay unflagged and are never read), and
+// gstex_raster_setup_bwd sums each splat's flagged rows in (slot, quadrant) order -> bitwise reproducible.
+// Texel gradients: segmented scan along each 4-pixel half row, run tails
 // added to the splat's texel block staged in the wave's LDS as int32 fixed point (exact, order-independent),
 // and the block flushed to v_texture (global float atomics, non-zero entries only) right after the visit.
 //
@@ -1200,30 +995,12 @@ __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^
     return q;
 }
 constexpr int kTexFixBits = 30;
-#ifndef GSTEX_TEX_FIXED
-#define GSTEX_TEX_FIXED 1
-#endif
-// 1: run tails staged as int32 fixed point at the per-visit scale; 0: staged as fp32 (ds_add_f32; the wave's LDS
-// atomics apply in program order, so the staged sums are deterministic either way).  Measured: fp32 LDS atomics
-// make the backward 2x slower (3.2 vs 1.57 ms) although they save the conversions.
-constexpr bool kTexFixed = GSTEX_TEX_FIXED;
-using TexQ = std::conditional_t<kTexFixed, int, float>;
+// (fp32 staging with ds_add_f32 instead measured 2x slower: 3.2 vs 1.57 ms, round 2; 3.0 vs 1.4 ms, round 4)
 __device__ __forceinline__ void stage_add(int* a, float y) { atomicAdd(a, fixed_round(y)); }
-__device__ __forceinline__ void stage_add(float* a, float y) { atomicAdd(a, y); }
 #ifndef GSTEX_FLUSH_U
 #define GSTEX_FLUSH_U 4
 #endif
 constexpr int kFlushU = GSTEX_FLUSH_U;  // staging entries per lane per flush pass
-#ifndef GSTEX_TAIL_MIRROR
-#define GSTEX_TAIL_MIRROR 0  // 1: mirrored corner order (measured: LDS bank conflicts -47 %, VALU +3 %, bwd +25 us; off)
-#endif
-// Run tails of neighbouring half rows usually share their bilinear cell (a texel spans ~3 pixels at cfg3), and same-
-// address LDS atomics of one instruction serialise like bank conflicts.  So the corner order of the four staged adds
-// is mirrored per half row: the half rows of a pixel row alternate the column order (lane bit 2), the pixel rows
-// alternate the row order (lane bit 3), and four tails that share a cell add into four different texels in each
-// instruction.  The mirror is uniform inside a scan segment (a half row), so it is applied to the bilinear factors
-// before the scan (swapped operands, identical products) and to the corner addresses at the tails.
-constexpr bool kTailMirror = GSTEX_TAIL_MIRROR;
 static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging area");
 
 
@@ -1235,12 +1012,11 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
-    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux,
-    const double* __restrict__ rec_hp) {
+    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux) {
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
-    __shared__ TexQ s_texq[kTexStage];
+    __shared__ int s_texq[kTexStage];
 
     // unit = 4 slot + quadrant (see AuxPtrs), launched costliest first; a unit the forward never evaluated in is empty
     const int unit = aux.order[blockIdx.x] - 1;  // entries are unit + 1
@@ -1371,24 +1147,6 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
-            if (GSTEX_HP && r.hp && rec_hp) {
-                // a near-edge-on splat (wave-uniform): the gradient's inputs dx, dy, 1 / p.z, u, v from its fp64
-                // homography; the decisions above (alpha, depth, branch) stay the forward's fp32 ones
-                // read through vector loads (a lane-varying zero offset): nine scalar-loaded doubles would spill
-                // the scalar register file of this 94-SGPR kernel
-                int vz;
-                asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-                const double* q = rec_hp + (size_t)gid * kHpDoubles + vz;
-                const double dx = (double)px - q[7], dy = (double)py - q[8];
-                const double qx = __builtin_fma(dx, q[0], dy * q[3]), qy = __builtin_fma(dx, q[1], dy * q[4]);
-                const double qz = __builtin_fma(dy, q[5], __builtin_fma(dx, q[2], q[6]));
-                const double iq = 1.0 / qz;
-                h.dx = (float)dx;
-                h.dy = (float)dy;
-                h.ipz = (float)iq;
-                h.u = (float)(qx * iq);
-                h.v = (float)(qy * iq);
-            }
             GSTEX_STAT(1, 1);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
@@ -1472,7 +1230,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if (has_tex && !(GSTEX_ABLATE & 1)) {
                     tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
                     tw = w * tex_scale;  // d value / d stored texel
-                    if (kTexFixed) P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
+                    P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
                     tax = b.ax;
                     tay = b.ay;
                 }
@@ -1556,10 +1314,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 }
                 // take the bound out of the spare slot (kMBound) before the row is stored
                 constexpr int kML = GEO ? 48 : 56, kMI = GEO ? 3 : 0;  // its lane and index after the reduce-scatter
-                if (kTexFixed) {
-                    vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
-                    if (lane == kML) P[kMI] = 0.0f;
-                }
+                vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
+                if (lane == kML) P[kMI] = 0.0f;
                 // lanes 8k hold NP / 8 consecutive values each.  Deterministic mode (row_flags given): the
                 // (pair, quadrant) row, whose flag (1: 24-value row, 2: 32-value row) marks it written, summed by
                 // setup_bwd in a fixed order.  Otherwise: added with float atomics into the splat's NP-value
@@ -1604,19 +1360,15 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // are exact multiplies (what ldexp computed); S is clamped to [-126, 126] (denormal / zero bounds)
                 const uint32_t mbits = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(vis_M));
                 const int biased = (int)((mbits >> 23) & 0xFFu);
-                const int e_m = (kTexFixed && biased > 0) ? biased - 126 : 0;
-                const int tex_S = kTexFixed ? min(max(kTexFixBits - e_m, -126), 126) : 0;
+                const int e_m = biased > 0 ? biased - 126 : 0;
+                const int tex_S = min(max(kTexFixBits - e_m, -126), 126);
                 const float pow_S = __uint_as_float((uint32_t)(tex_S + 127) << 23);     // 2^S
                 const float pow_mS = __uint_as_float((uint32_t)(127 - tex_S) << 23);    // 2^-S
-                const float twq = kTexFixed ? tw * pow_S : tw;
+                const float twq = tw * pow_S;
                 float tg[4 * CM];
                 {
 #pragma clang fp contract(fast)
-                    // row / column factors of the slot order (kTailMirror: swapped in mirrored half rows)
-                    const bool mi = kTailMirror && (lane & 8), mj = kTailMirror && (lane & 4);
-                    const float ax0 = 1.0f - tax, ay0 = 1.0f - tay;
-                    const float fi0 = mi ? tax : ax0, fi1 = mi ? ax0 : tax;
-                    const float fj0 = mj ? tay : ay0, fj1 = mj ? ay0 : tay;
+                    const float fi0 = 1.0f - tax, fi1 = tax, fj0 = 1.0f - tay, fj1 = tay;
                     const float w00 = fi0 * fj0, w01 = fi0 * fj1;
                     const float w10 = fi1 * fj0, w11 = fi1 * fj1;
 #pragma unroll
@@ -1638,21 +1390,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
                 } else if (tail) {
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
-                    int c00, c01, c10, c11;
-                    if (kTailMirror) {  // slot (p, q) = corner (p ^ mi, q ^ mj)
-                        const int di = tdi * r.w, dj = tdj;
-                        const int b = t0 + ((lane & 8) ? di : 0) + ((lane & 4) ? dj : 0);
-                        const int si = (lane & 8) ? -di : di, sj = (lane & 4) ? -dj : dj;
-                        c00 = b * Cn;
-                        c01 = (b + sj) * Cn;
-                        c10 = (b + si) * Cn;
-                        c11 = (b + si + sj) * Cn;
-                    } else {
-                        c00 = t0 * Cn;
-                        c01 = (t0 + tdj) * Cn;
-                        c10 = (t0 + tdi * r.w) * Cn;
-                        c11 = (t0 + tdi * r.w + tdj) * Cn;
-                    }
+                    const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
+                    const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
                     if (staged) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
@@ -1666,7 +1405,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     } else {
                         // block larger than the staging area: straight to global, back in value units
                         float* base = v_texture + (size_t)r.off * Cn;
-                        auto val = [&](float y) { return kTexFixed ? y * pow_mS : y; };
+                        auto val = [&](float y) { return y * pow_mS; };
 #pragma unroll
                         for (int c = 0; c < CM; ++c) {
                             if (c < Cn) {
@@ -1685,7 +1424,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     // kFlushU entries per lane per pass, their LDS reads issued together (one wait per pass); entries
                     // past the block are zero (the staging area is kept zeroed) and kTexStage is a multiple of the pass
                     for (int e0 = lane; e0 < bsize; e0 += 64 * kFlushU) {
-                        TexQ v[kFlushU];
+                        int v[kFlushU];
                         GSTEX_STAT(4, 1);
 #pragma unroll
                         for (int k = 0; k < kFlushU; ++k) v[k] = s_texq[e0 + 64 * k];
@@ -1694,7 +1433,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                             GSTEX_STAT(6, __popcll(__ballot(v[k] != 0)));
                             if (v[k] == 0) continue;
                             s_texq[e0 + 64 * k] = 0;
-                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, kTexFixed ? (float)v[k] * pow_mS : (float)v[k]);
+                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, (float)v[k] * pow_mS);
                         }
                     }
                 }
@@ -1709,32 +1448,18 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 // ------------------------------------------------------------------------------------------
 // setup backward: sum partials per splat, chain to parameters
 // ------------------------------------------------------------------------------------------
-constexpr int kSetupBwdRows = 256 / kRowStride;  // 8 splats x 32 partial columns summed at once per 256-thread workgroup
-#ifndef GSTEX_SETUP_SPW
-#define GSTEX_SETUP_SPW 40
-#endif
-// splats per workgroup: phase 1 sums them kSetupBwdRows at a time, phase 2 chains them one per thread
-constexpr int kSetupBwdSplats = GSTEX_SETUP_SPW;
-#ifndef GSTEX_SETUP_INFLIGHT
-#define GSTEX_SETUP_INFLIGHT 4
-#endif
-constexpr int kSetupBwdInflight = GSTEX_SETUP_INFLIGHT;  // slots (x 4 quadrant rows) per group of loads
-static_assert(kSetupBwdSplats % kSetupBwdRows == 0 && kSetupBwdSplats <= 256, "setup_bwd splats per workgroup");
-// FOLD_AABB: the centres were produced by get_aabb_2d from these same means / scales / quats (training
-// path), so the AABB-centre chain (aabb_bwd_kernel's arithmetic) is applied here and added in, instead of
-// a separate launch plus autograd's accumulation kernels; the sums are the same two terms added once.
-#ifndef GSTEX_SETUP_SPLIT
-#define GSTEX_SETUP_SPLIT 1
-#endif
-// Split form (GSTEX_SETUP_SPLIT): setup_bwd_sum_kernel, 32 lanes per splat (lane c = column c), sums the splat's
-// flagged rows in the same (slot, quadrant) order and writes the 32 sums over the splat's first row (slot
-// offsets[g], quadrant 0), whose values it has already read -- no other splat reads that row; then
-// setup_bwd_chain_kernel, one thread per splat, chains the sums to the parameters.  (The fused kernel below keeps
-// 216 of its 256 threads idle through the chain and serialises its 5 splat groups' load chains.)
+constexpr int kSetupBwdRows = 8;  // splats summed per 256-thread workgroup (32 lanes each)
 #ifndef GSTEX_SUM_SLOTS
 #define GSTEX_SUM_SLOTS 8
 #endif
-constexpr int kSumSlots = GSTEX_SUM_SLOTS;  // slots whose rows one lane group has in flight at once
+constexpr int kSumSlots = GSTEX_SUM_SLOTS;  // slots whose rows one lane group has in flight at once (16: equal; 4: slower)
+// Deterministic mode: setup_bwd_sum_kernel, 32 lanes per splat, sums the splat's flagged rows in (slot, quadrant)
+// order and writes the 32 sums over the splat's first row (slot offsets[g], quadrant 0), whose values it has already
+// read -- no other splat reads that row; then setup_bwd_chain_kernel, one thread per splat, chains the sums to the
+// parameters.  (One fused kernel, 40 splats per workgroup, measured 120 vs 102 us in round 2.)
+// Capacity mode (n_rows >= 0, gstex_bin_sort_capped): a total offsets[n] above the row capacity means the binning
+// left every tile empty and no row was written; both kernels then treat every splat as pair-free (zero gradients)
+// instead of addressing rows past the buffers.
 // 32 lanes per splat: lane 8 q + m reads float4 m (columns 4m .. 4m+3) of the quadrant-q rows, kSumSlots slots at a
 // time, and sums them in slot order; the 4 quadrant sums are then combined (q0 + q1) + (q2 + q3) across lanes.
 // Deterministic (fixed order), like the fused kernel's slot-major quadrant-minor order it replaces.
@@ -1744,10 +1469,11 @@ constexpr int kSumSlots = GSTEX_SUM_SLOTS;  // slots whose rows one lane group h
 __global__ __launch_bounds__(256) void setup_bwd_sum_kernel(int n, const int32_t* __restrict__ nth,
                                                            const int32_t* __restrict__ offsets,
                                                            float* __restrict__ partials,
-                                                           const uint32_t* __restrict__ row_flags, int rs) {
+                                                           const uint32_t* __restrict__ row_flags, int rs,
+                                                           int64_t n_rows) {
     const int l = threadIdx.x & 31, q = l >> 3, m = l & 7;
     const int g = blockIdx.x * 8 + (threadIdx.x >> 5);
-    const bool live = g < n;
+    const bool live = g < n && !(n_rows >= 0 && (int64_t)offsets[n] > n_rows);  // over capacity: no rows exist
     const int cnt = live ? nth[g] : 0;
     const size_t s0 = live ? (size_t)offsets[g] : 0;
     // columns 24.. exist only in 32-value rows (flag 2: backward with depth / normal gradients)
@@ -1797,13 +1523,15 @@ __global__ __launch_bounds__(256) void setup_bwd_chain_kernel(
     int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
     const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
     const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials, int rs,
-    bool per_splat, CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales,
+    bool per_splat, int64_t n_rows, CamArgs cam_args, float* __restrict__ v_means, float* __restrict__ v_scales,
     float* __restrict__ v_quats, float* __restrict__ v_rgbs, float* __restrict__ v_opac, float* __restrict__ v_centers,
     float* __restrict__ v_uv0) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     const Camera cam = load_camera(cam_args);
-    const int cnt = nth[g];
+    // deterministic mode over capacity (n_rows >= 0): the binning left every tile empty and no row exists
+    const bool over = !per_splat && n_rows >= 0 && (int64_t)offsets[n] > n_rows;
+    const int cnt = over ? 0 : nth[g];
     float S[kPartRowGeo];
     if (per_splat) {
         // the backward's (N, rs) accumulator rows (zero for a splat without pairs): all eight 16-B loads issued at
@@ -1831,64 +1559,6 @@ __global__ __launch_bounds__(256) void setup_bwd_chain_kernel(
         for (int i = 0; i < kPartRowGeo; ++i) S[i] = 0.f;
     }
     setup_bwd_chain<FOLD_AABB>(g, S, cnt, cam, means, scales, glob, quats, umap, vmap, v_means, v_scales, v_quats,
-                               v_rgbs, v_opac, v_centers, v_uv0);
-}
-
-template <bool FOLD_AABB>
-__global__ __launch_bounds__(256) void setup_bwd_kernel(
-    int n, const float* __restrict__ means, const float* __restrict__ scales, float glob,
-    const float* __restrict__ quats, const float* __restrict__ umap, const float* __restrict__ vmap,
-    const int32_t* __restrict__ nth, const int32_t* __restrict__ offsets, const float* __restrict__ partials,
-    const uint32_t* __restrict__ row_flags, int rs, CamArgs cam_args, float* __restrict__ v_means,
-    float* __restrict__ v_scales, float* __restrict__ v_quats, float* __restrict__ v_rgbs, float* __restrict__ v_opac,
-    float* __restrict__ v_centers, float* __restrict__ v_uv0) {
-    // phase 1: 32 lanes per splat, lane c sums column c of the splat's flagged (slot, quadrant) rows in slot-major,
-    // quadrant-minor order (a splat's slots are contiguous, so its rows and flag words are too); phase 2: one
-    // thread per splat chains the sums to the parameters
-    __shared__ float s_sum[kSetupBwdSplats][kRowStride];
-    const int t = threadIdx.x;
-    const int g0 = blockIdx.x * kSetupBwdSplats;
-    if (t < kSetupBwdRows * kRowStride) {
-        const int c = t % kRowStride;
-        // columns 24.. exist only in 32-value rows (flag 2: backward with depth / normal gradients)
-        const uint32_t need = c < kPartRow ? 0xFFu : 0x02u;
-        for (int j = t / kRowStride; j < kSetupBwdSplats; j += kSetupBwdRows) {
-            float acc = 0.f;
-            if (g0 + j < n) {
-                const int cnt = nth[g0 + j];
-                const size_t s0 = (size_t)offsets[g0 + j];
-                const float* src = partials + s0 * 4 * rs + c;
-                const uint32_t* fl = row_flags + s0;
-                // groups of kSetupBwdInflight slots: their flag words, then every flagged row of the group, are
-                // loaded before any is summed (most splats hit fewer tiles than one group holds)
-                for (int e = 0; e < cnt; e += kSetupBwdInflight) {
-                    uint32_t f[kSetupBwdInflight];
-#pragma unroll
-                    for (int u = 0; u < kSetupBwdInflight; ++u) f[u] = e + u < cnt ? fl[e + u] : 0u;
-                    float r[kSetupBwdInflight * 4];
-#pragma unroll
-                    for (int u = 0; u < kSetupBwdInflight; ++u)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            r[4 * u + q] = (f[u] >> (8 * q)) & need ? src[((size_t)(e + u) * 4 + q) * rs] : 0.f;
-#pragma unroll
-                    for (int u = 0; u < kSetupBwdInflight; ++u)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            if ((f[u] >> (8 * q)) & need) acc += r[4 * u + q];
-                }
-            }
-            s_sum[j][c] = acc;
-        }
-    }
-    __syncthreads();
-    const int g = g0 + t;
-    if (t >= kSetupBwdSplats || g >= n) return;
-    const Camera cam = load_camera(cam_args);
-    float S[kPartRowGeo];
-#pragma unroll
-    for (int i = 0; i < kPartRowGeo; ++i) S[i] = s_sum[t][i];
-    setup_bwd_chain<FOLD_AABB>(g, S, nth[g], cam, means, scales, glob, quats, umap, vmap, v_means, v_scales, v_quats,
                                v_rgbs, v_opac, v_centers, v_uv0);
 }
 
@@ -2069,15 +1739,6 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
                                   const float* centers, const float* uv0, const float* umap, const float* vmap,
                                   const int32_t* texture_dims, const int32_t* num_tiles_hit,
                                   const gstex_camera* cam, float* records, void* stream) {
-    return gstex_raster_setup_hp(n, means, scales, glob_scale, quats, rgbs, opacities, centers, uv0, umap, vmap,
-                                 texture_dims, num_tiles_hit, cam, records, nullptr, stream);
-}
-
-extern "C" int gstex_raster_setup_hp(int32_t n, const float* means, const float* scales, float glob_scale,
-                                     const float* quats, const float* rgbs, const float* opacities,
-                                     const float* centers, const float* uv0, const float* umap, const float* vmap,
-                                     const int32_t* texture_dims, const int32_t* num_tiles_hit,
-                                     const gstex_camera* cam, float* records, double* rec_hp, void* stream) {
     GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup: invalid arguments");
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(means && scales && quats && rgbs && opacities && centers && uv0 && umap && vmap &&
@@ -2085,7 +1746,7 @@ extern "C" int gstex_raster_setup_hp(int32_t n, const float* means, const float*
                   "gstex_raster_setup: null pointer");
     setup_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, means, scales, glob_scale, quats, rgbs, opacities,
                                                                  centers, uv0, umap, vmap, texture_dims,
-                                                                 num_tiles_hit, to_device_camera(*cam), records, rec_hp);
+                                                                 num_tiles_hit, to_device_camera(*cam), records);
     return launch_status("gstex_raster_setup");
 }
 
@@ -2137,18 +1798,10 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     zbuf.p[1] = zero_floats2 > 0 && !(GSTEX_ABLATE & 512) ? zero_buf2 : nullptr;
     zbuf.n[1] = zero_floats2;
 #define GSTEX_FWD(CC, GG)                                                                                      \
-    do {                                                                                                       \
-        if (GSTEX_FWD_WAVE)                                                                                    \
-            raster_fwd_kernel<CC, GG, true><<<(unsigned)(((nblk + 7) / 8) * 32), 64, 0, st>>>(                \
-                dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, \
-                tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth,       \
-                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf);                      \
-        else                                                                                                   \
-            raster_fwd_kernel<CC, GG, false><<<nblk, kThreads, 0, st>>>(                                      \
-                dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, \
-                tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth,       \
-                out_reg, out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf);                      \
-    } while (0)
+    raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(                                                      \
+        dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
+        tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg,     \
+        out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf)
     if (channels == 3 && geo) GSTEX_FWD(3, true);
     else if (channels == 3) GSTEX_FWD(3, false);
     else if (channels == 6 && geo) GSTEX_FWD(6, true);
@@ -2167,24 +1820,9 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
                                 float* v_texture, void* aux, void* stream) {
-    return gstex_raster_bwd_hp(cam, channels, settings, background, records, tile_ranges, sorted_ids, sorted_slots,
-                               texture, n_texels, tex_scale, tex_bias, state, v_img, v_depth, v_reg, v_alpha, v_tex,
-                               v_normal, n_isect, partials, row_flags, v_texture, aux, nullptr, stream);
-}
-
-extern "C" int gstex_raster_bwd_hp(const gstex_camera* cam, int32_t channels, int32_t settings,
-                                   const float* background, const float* records, const int32_t* tile_ranges,
-                                   const int32_t* sorted_ids, const int32_t* sorted_slots,
-                                   const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
-                                   const float* state, const float* v_img,
-                                   const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
-                                   const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
-                                   float* v_texture, void* aux, const double* rec_hp, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
-    const bool ordered = (settings & GSTEX_BWD_ORDERED) != 0;  // gstex_raster_bwd_order already ran on this aux
-    settings &= ~GSTEX_BWD_ORDERED;
     int rc = check_settings(settings);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && state && aux, "gstex_raster_bwd: null pointer (tile_ranges, state and the forward's aux)");
@@ -2202,18 +1840,15 @@ extern "C" int gstex_raster_bwd_hp(const gstex_camera* cam, int32_t channels, in
     if (n_isect > 0 && row_flags && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
     // costliest units first, from the histogram the forward built (order entries are unit + 1)
-    if (!ordered) {
-        rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
-        if (rc) return rc;
-    }
+    rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
+    if (rc) return rc;
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
 #define GSTEX_BWD(CC, GG)                                                                                      \
     raster_bwd_kernel<CC, GG><<<(unsigned)al.n_units, 64, 0, st>>>(                                            \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
-        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap,      \
-        rec_hp)
+        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
     else if (channels == 3) GSTEX_BWD(3, true);
     else if (channels == 6 && !geo) GSTEX_BWD(6, false);
@@ -2224,18 +1859,6 @@ extern "C" int gstex_raster_bwd_hp(const gstex_camera* cam, int32_t channels, in
     return launch_status("gstex_raster_bwd");
 }
 
-extern "C" int gstex_raster_bwd_order(const gstex_camera* cam, int32_t channels, int64_t n_isect, void* aux,
-                                      void* stream) {
-    GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0 && cam->block == kTile, "gstex_raster_bwd_order: invalid camera");
-    GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd_order: channels must be in [1, 8]");
-    GSTEX_REQUIRE(aux, "gstex_raster_bwd_order: null aux");
-    GSTEX_REQUIRE(n_isect >= 0 && n_isect < (int64_t)INT32_MAX, "gstex_raster_bwd_order: n_isect out of range");
-    const int tiles_x = (cam->W + kTile - 1) / kTile, tiles_y = (cam->H + kTile - 1) / kTile;
-    const AuxLayout al = aux_layout(n_isect, tiles_x * tiles_y, channels);
-    const AuxPtrs ap = aux_ptrs(aux, al);
-    return unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, as_stream(stream));
-}
-
 extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels) {
     if (n_isect < 0 || n_tiles < 0 || channels < 1 || channels > 8) return 0;
     return aux_layout(n_isect, n_tiles, channels).bytes;
@@ -2244,62 +1867,60 @@ extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32
 template <bool FOLD_AABB>
 int setup_bwd_launch(int32_t n, const float* means, const float* scales, float glob_scale, const float* quats,
                      const float* umap, const float* vmap, const int32_t* nth, const int32_t* offsets,
-                     float* partials, const uint32_t* row_flags, int32_t rs, const gstex_camera* cam, float* v_means,
-                     float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
-                     float* v_uv0, hipStream_t st, const char* name) {
-    if (GSTEX_SETUP_SPLIT || !row_flags) {
-        // no row_flags: the backward accumulated per splat (atomic mode), nothing to sum
-        if (row_flags)
-            setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags, rs);
-        setup_bwd_chain_kernel<FOLD_AABB><<<div_up(n, 256), 256, 0, st>>>(
-            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, rs, row_flags == nullptr,
-            to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
-    } else {
-        setup_bwd_kernel<FOLD_AABB><<<div_up(n, kSetupBwdSplats), 256, 0, st>>>(
-            n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, row_flags, rs,
-            to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
-    }
+                     float* partials, const uint32_t* row_flags, int32_t rs, int64_t n_rows, const gstex_camera* cam,
+                     float* v_means, float* v_scales, float* v_quats, float* v_rgbs, float* v_opacities,
+                     float* v_centers, float* v_uv0, hipStream_t st) {
+    // no row_flags: the backward accumulated per splat (atomic mode), nothing to sum
+    if (row_flags)
+        setup_bwd_sum_kernel<<<div_up(n, kSetupBwdRows), 256, 0, st>>>(n, nth, offsets, partials, row_flags, rs, n_rows);
+    setup_bwd_chain_kernel<FOLD_AABB><<<div_up(n, 256), 256, 0, st>>>(
+        n, means, scales, glob_scale, quats, umap, vmap, nth, offsets, partials, rs, row_flags == nullptr, n_rows,
+        to_device_camera(*cam), v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0);
+    return GSTEX_OK;
+}
+
+template <bool FOLD_AABB>
+int setup_bwd_entry(const char* name, int32_t n, const float* means, const float* scales, float glob_scale,
+                    const float* quats, const float* umap, const float* vmap, const int32_t* num_tiles_hit,
+                    const int32_t* offsets, float* partials, const uint32_t* row_flags, int32_t row_floats,
+                    int64_t n_rows, const gstex_camera* cam, float* v_means, float* v_scales, float* v_quats,
+                    float* v_rgbs, float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
+    GSTEX_REQUIRE(n >= 0 && cam, "%s: invalid arguments", name);
+    if (n == 0) return GSTEX_OK;
+    GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && partials && v_means &&
+                      v_scales && v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
+                  "%s: null pointer", name);
+    GSTEX_REQUIRE(row_floats == kPartRow || row_floats == kPartRowGeo, "%s: row_floats must be %d or %d (got %d)",
+                  name, kPartRow, kPartRowGeo, row_floats);
+    setup_bwd_launch<FOLD_AABB>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
+                                row_flags, row_floats, n_rows, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities,
+                                v_centers, v_uv0, as_stream(stream));
     return launch_status(name);
 }
 
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                                       const float* quats, const float* opacities, const float* umap,
                                       const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      float* partials, const uint32_t* row_flags, int32_t row_floats,
-                                      const gstex_camera* cam,
-                                      float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
-                                      float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
+                                      float* partials, const uint32_t* row_flags, int32_t row_floats, int64_t n_rows,
+                                      const gstex_camera* cam, float* v_means, float* v_scales, float* v_quats,
+                                      float* v_rgbs, float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
     (void)opacities;
-    GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup_bwd: invalid arguments");
-    if (n == 0) return GSTEX_OK;
-    GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
-                      v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
-                  "gstex_raster_setup_bwd: null pointer");
-    GSTEX_REQUIRE(row_floats == kPartRow || row_floats == kPartRowGeo,
-                  "gstex_raster_setup_bwd: row_floats must be %d or %d (got %d)", kPartRow, kPartRowGeo, row_floats);
-    return setup_bwd_launch<false>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
-                                   row_flags, row_floats, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
-                                   as_stream(stream), "gstex_raster_setup_bwd");
+    return setup_bwd_entry<false>("gstex_raster_setup_bwd", n, means, scales, glob_scale, quats, umap, vmap,
+                                  num_tiles_hit, offsets, partials, row_flags, row_floats, n_rows, cam, v_means,
+                                  v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0, stream);
 }
 
 extern "C" int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scales, float glob_scale,
-                                      const float* quats, const float* opacities, const float* umap,
-                                      const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
-                                      float* partials, const uint32_t* row_flags, int32_t row_floats,
-                                      const gstex_camera* cam,
-                                      float* v_means, float* v_scales, float* v_quats, float* v_rgbs,
-                                      float* v_opacities, float* v_centers, float* v_uv0, void* stream) {
+                                           const float* quats, const float* opacities, const float* umap,
+                                           const float* vmap, const int32_t* num_tiles_hit, const int32_t* offsets,
+                                           float* partials, const uint32_t* row_flags, int32_t row_floats,
+                                           int64_t n_rows, const gstex_camera* cam, float* v_means, float* v_scales,
+                                           float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
+                                           float* v_uv0, void* stream) {
     (void)opacities;
-    GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup_bwd_aabb: invalid arguments");
-    if (n == 0) return GSTEX_OK;
-    GSTEX_REQUIRE(means && scales && quats && umap && vmap && num_tiles_hit && offsets && v_means && v_scales &&
-                      v_quats && v_rgbs && v_opacities && v_centers && v_uv0,
-                  "gstex_raster_setup_bwd_aabb: null pointer");
-    GSTEX_REQUIRE(row_floats == kPartRow || row_floats == kPartRowGeo,
-                  "gstex_raster_setup_bwd_aabb: row_floats must be %d or %d (got %d)", kPartRow, kPartRowGeo, row_floats);
-    return setup_bwd_launch<true>(n, means, scales, glob_scale, quats, umap, vmap, num_tiles_hit, offsets, partials,
-                                   row_flags, row_floats, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0,
-                                   as_stream(stream), "gstex_raster_setup_bwd_aabb");
+    return setup_bwd_entry<true>("gstex_raster_setup_bwd_aabb", n, means, scales, glob_scale, quats, umap, vmap,
+                                 num_tiles_hit, offsets, partials, row_flags, row_floats, n_rows, cam, v_means,
+                                 v_scales, v_quats, v_rgbs, v_opacities, v_centers, v_uv0, stream);
 }
 
 extern "C" int gstex_texture_edit(const gstex_camera* cam, int32_t settings, const float* records,

@@ -180,8 +180,8 @@ class GradSync:
         if self.rebuild():
             return  # a new buffer is zero
         if getattr(self.trainer, "texture_grad_zeroed_by_update", False):
-            # the texel slice is zeroed by the trainer's texel Adam as it reads it (GSTEX_ADAM_ZERO_GRAD: a side-stream
-            # or deferred update, async_texture / defer_texture); filling it here would race or pre-empt that update
+            # the texel slice is zeroed by the next differentiable raster forward (gstex_raster_fwd_zero); filling it
+            # here would pre-empt the deferred texel update (defer_texture) still reading it
             self.flat[self._z0:self._tail_off].zero_()
         else:
             self.flat[self._z0:].zero_()

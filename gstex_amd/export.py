@@ -18,7 +18,7 @@ NPZ_KEYS = ("xyz", "features_rest", "opacity", "scaling", "rotation", "texture_d
 
 
 def export_npz(trainer, path) -> None:
-    if hasattr(trainer, "wait_texture"):  # async_texture: the side-stream texel update must land before the read
+    if hasattr(trainer, "wait_texture"):  # defer_texture: the pending texel update must run before the read
         trainer.wait_texture()
     params = {
         "xyz": trainer.means,

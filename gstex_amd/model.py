@@ -106,8 +106,7 @@ class GStexTrainer:
                  pixel_num: float | None = None, background=(1.0, 1.0, 1.0), fused_adam: bool = True,
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
-                 async_texture: bool = False, defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0,
-                 use_normal_loss: bool = False, defer_side_stream: bool | None = None,
+                 defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0, use_normal_loss: bool = False,
                  pair_capacity: bool | None = None):
         self.device = torch.device(device)
         d = self.device
@@ -162,33 +161,20 @@ class GStexTrainer:
         self.texture_grad_ready = None
         self.texture_grad_route = None  # GradSync: the per-render texel-gradient target (several renders per step)
         self.test_colors = None  # eval-render test colours (gstex.py:309)
-        # async_texture (not in the reference; fused Adam on a HIP device): the texel parameter's Adam update (73 % of
-        # the parameters at cfg3) runs on a side stream (its gradient is zeroed by the next raster forward); the next step's
-        # preprocessing and binning overlap it, and only its raster forward waits (texture_gaussians texture_ready).
-        # The gradient lives in a persistent buffer the raster backward accumulates into (texture_grad_sink), so
-        # no per-step zero fill remains.  Anything else reading texture_dc after optimizer_step() must call
-        # wait_texture() first (eval_render and recharge in this class do).
-        self.async_texture = bool(async_texture) and fused_adam and self.device.type == "cuda"
-        # defer_texture (not in the reference; fused Adam on a HIP device; exclusive with async_texture): the texel
-        # parameter's Adam update of step k runs inside step k+1's render, queued right after the binning's pair count
-        # is read back -- the device runs it while the host waits for that count and sizes the pair buffers (an idle
-        # gap of the device otherwise), and before the raster forward, the first reader of the texels.  Same updates
-        # in the same order on the same stream; the gradient is a persistent buffer the raster forward zeroes.
-        # Readers of texture_dc outside the step go through wait_texture() / texels(), which run a pending update.
-        self.defer_texture = bool(defer_texture) and not self.async_texture and fused_adam and self.device.type == "cuda"
+        # defer_texture (not in the reference; fused Adam on a HIP device): the texel parameter's Adam update of step k
+        # (73 % of the parameters at cfg3) runs inside step k+1's render, before the raster forward, the first reader of
+        # the texels -- at the pair-count read-back when there is one (the device runs it while the host waits), else
+        # right before the raster forward.  Same updates in the same order on the same stream; the gradient is a
+        # persistent buffer the raster forward zeroes (no per-step fill).  Readers of texture_dc outside the step go
+        # through wait_texture() / texels(), which run a pending update.  (A side-stream texel update, overlapping
+        # the next step's preprocessing and binning, measured no gain in rounds 2-3: the compute stream's kernels
+        # slow down under the streaming update by what the overlap saves; removed in round 5.)
+        self.defer_texture = bool(defer_texture) and fused_adam and self.device.type == "cuda"
         self._pending_tex = None
         self._pending_collective = False  # the pending update first waits for a GradSync collective
         # the texel-gradient sink is zeroed by the first differentiable raster forward after an optimizer step
         # (gstex_raster_fwd_zero), so several renders of one step still accumulate their texel gradients
         self._sink_fresh = True
-        # defer_side_stream (one GPU, defer_texture): the deferred update is enqueued at the pair-count read-back on a
-        # side stream instead, so it overlaps the binning's placement and sort (latency-bound kernels that leave HBM
-        # mostly idle); the raster forward waits for it.  Measured slower (+15 us median per step): off
-        # by default, GSTEX_DEFER_SIDE=1 turns it on.
-        if defer_side_stream is None:
-            defer_side_stream = os.environ.get("GSTEX_DEFER_SIDE", "0") != "0"
-        self.defer_side = bool(defer_side_stream) and self.defer_texture
-        self._tex_stream = torch.cuda.Stream(device=d) if (self.async_texture or self.defer_side) else None
         # pair_capacity (not in the reference; fused Adam on a HIP device): the training renders size their pair
         # buffers from an ops.PairCapacity instead of reading the pair total back to the host (gstex.py:1045-1052,
         # 1127), so a step has no host synchronisation.  Each step's renders write an overflow flag into
@@ -200,12 +186,8 @@ class GStexTrainer:
         self.pairs = ops.PairCapacity(d) if (pair_capacity and fused_adam and self.device.type == "cuda") else None
         self.step_control = torch.zeros(8, device=d, dtype=torch.float32)
         self.skipped_steps = []  # steps whose update the pair-capacity guard skipped (found by _poll_pairs)
-        self._tex_ready = None
         self._tex_grad = None
-        # the side-stream update's workgroup cap (GSTEX_TEX_ADAM_GRID; 0 = full grid).  Measured at cfg3: no cap, 512,
-        # 256, 128, 64 -- none gains over the compute-stream update
-        self._tex_grid = int(os.environ.get("GSTEX_TEX_ADAM_GRID", "0")) if self.async_texture else 0
-        if self.async_texture or self.defer_texture:
+        if self.defer_texture:
             self._own_texture_grad()
         self._build_optimizer()
 
@@ -219,8 +201,8 @@ class GStexTrainer:
     def texture_grad_zeroed_by_update(self) -> bool:
         """The texel gradient buffer handed to the raster (texture_grad_sink) is zeroed by the raster forward
         (gstex_raster_fwd_zero) before the backward accumulates into it: a gradient-buffer owner
-        (gstex_amd.dist.GradSync) must not fill that slice itself (with a side-stream or deferred texel update,
-        async_texture / defer_texture, that fill would also race or pre-empt the update still reading it)."""
+        (gstex_amd.dist.GradSync) must not fill that slice itself (with the deferred texel update, defer_texture, that
+        fill would also pre-empt the update still reading it)."""
         return True
 
     def reset_texture_grad(self):
@@ -251,36 +233,13 @@ class GStexTrainer:
         if fn is not None:
             fn()
 
-    def _launch_pending_texture_side(self):
-        """The deferred texel update on the side stream, after everything the current stream has enqueued (the
-        backward, the head update); the raster forward waits for its event (_wait_side_texture)."""
-        fn, self._pending_tex = self._pending_tex, None
-        if fn is None:
-            return
-        main = torch.cuda.current_stream(self.device)
-        self._tex_stream.wait_stream(main)
-        with torch.cuda.stream(self._tex_stream):
-            fn()
-            ev = torch.cuda.Event()
-            ev.record(self._tex_stream)
-        self._tex_ready = ev
-
-    def _wait_side_texture(self):
-        if self._tex_ready is not None:
-            torch.cuda.current_stream(self.device).wait_event(self._tex_ready)
-            self._tex_ready = None
-
     def wait_texture(self):
-        """Order the current stream after the pending texel update: a deferred one (defer_texture) is enqueued now,
-        a side-stream one (async_texture) is waited for."""
+        """Order the current stream after the pending texel update (defer_texture): it is enqueued now."""
         self._run_pending_texture()
-        if self._tex_ready is not None:
-            torch.cuda.current_stream(self.device).wait_event(self._tex_ready)
-            self._tex_ready = None
 
     def texels(self) -> torch.Tensor:
-        """The texel store (SH-DC values) for readers outside the step (export, average_colors, viewers): waits for a
-        pending side-stream update first (async_texture), so no reader depends on remembering wait_texture()."""
+        """The texel store (SH-DC values) for readers outside the step (export, average_colors, viewers): runs a
+        pending deferred update first (defer_texture), so no reader depends on remembering wait_texture()."""
         self.wait_texture()
         return self.texture_dc.detach()
 
@@ -353,7 +312,6 @@ class GStexTrainer:
         if self.pairs is not None and torch.is_grad_enabled():
             self._poll_pairs()
             guard = (self.pairs, self._skip_flag(), self._sink_fresh, self.step)
-        side = pend and not late and self.defer_side
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
             uv0, umap, vmap, texture, view.viewmat, view.c2w, view.fx, view.fy, view.cx, view.cy, view.H, view.W,
@@ -361,11 +319,9 @@ class GStexTrainer:
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs if geometry is None else geometry,
             texture_grad_sink=sink, zero_texture_grad_sink=zero_sink, on_texture_grad=on_grad,
-            texture_ready=(self._run_pending_texture if late else self._wait_side_texture if side else self._tex_ready),
-            before_pair_wait=(self._launch_pending_texture_side if side else
-                              self._run_pending_texture if pend and not late else None),
+            texture_ready=self._run_pending_texture if late else None,
+            before_pair_wait=self._run_pending_texture if pend and not late else None,
             pair_guard=guard)
-        self._tex_ready = None  # the raster forward (enqueued above) is ordered after the texel update
         if torch.is_grad_enabled():
             self._sink_fresh = False  # zeroed by this forward: further renders before the step accumulate on top
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
@@ -489,7 +445,7 @@ class GStexTrainer:
                 self._pending_collective = False
             self.step += 1
             return
-        if sync is not None and self.fused_adam and not self.async_texture:
+        if sync is not None and self.fused_adam:
             tex = {id(self.texture_dc)}
             sync.all_reduce_and_step(lambda s: self.optimizer.step(only=tex, grad_scale=s, skip_flag=sf),
                                      lambda s: self.optimizer.step(skip=tex, grad_scale=s, skip_flag=sf))
@@ -497,26 +453,7 @@ class GStexTrainer:
             return
         if sync is not None:
             sync.all_reduce()
-        if not self.async_texture:
-            self._step(skip_flag=sf)
-            self.step += 1
-            return
-        # the texel update on the side stream, after everything enqueued so far (the backward, and a GradSync
-        # all-reduce of the gradient); the other groups on the current stream
-        main = torch.cuda.current_stream(self.device)
-        self.wait_texture()  # (a step without a render in between)
-        tex = {id(self.texture_dc)}
-        self._step(skip=tex, skip_flag=sf)
-        # recorded after the other groups' update: that one runs alone at full bandwidth, and the texel update then
-        # overlaps the next step's latency-bound kernels (preprocessing, binning) instead of contending with it
-        grads_ready = torch.cuda.Event()
-        grads_ready.record(main)
-        self._tex_stream.wait_event(grads_ready)
-        with torch.cuda.stream(self._tex_stream):
-            self.optimizer.step(only=tex, grid=self._tex_grid, skip_flag=sf)
-            ev = torch.cuda.Event()
-            ev.record(self._tex_stream)
-        self._tex_ready = ev
+        self._step(skip_flag=sf)
         self.step += 1
 
     def _step(self, **kw):
@@ -530,9 +467,9 @@ class GStexTrainer:
         """Optimizers.zero_grad_all (engine/optimizers.py): torch's default set_to_none=True, so backward
         writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
         when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead).  With
-        async_texture / defer_texture the texel gradient buffer is kept (the raster forward zeroes it)."""
+        defer_texture the texel gradient buffer is kept (the raster forward zeroes it)."""
         self.reset_texture_grad()
-        if self.async_texture or self.defer_texture:
+        if self.defer_texture:
             keep = self.texture_dc.grad
             self.optimizer.zero_grad(set_to_none=set_to_none)
             self.texture_dc.grad = keep
@@ -570,7 +507,7 @@ class GStexTrainer:
                     "exp_avg": torch.zeros_like(self.texture_dc),
                     "exp_avg_sq": torch.zeros_like(self.texture_dc),
                 }
-            if self.async_texture or self.defer_texture:  # a fresh persistent gradient buffer (GradSync replaces it)
+            if self.defer_texture:  # a fresh persistent gradient buffer (GradSync replaces it)
                 self._own_texture_grad()
         else:
             st = self.optimizer.state.get(old)

@@ -8,7 +8,6 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 from __future__ import annotations
 
 import ctypes
-import os
 import time
 from typing import NamedTuple, Tuple
 
@@ -27,8 +26,6 @@ _TIMING: dict | None = None
 
 _TIMED_DEFAULT = ("gstex_raster_fwd", "gstex_raster_bwd")  # the roofline kernels
 _TIMED = set(_TIMED_DEFAULT)
-HP_DOUBLES = 10  # raster.hip kHpDoubles
-_HP_RECORD = os.environ.get("GSTEX_HP_RECORD", "0") != "0"
 
 
 def set_kernel_timing(enabled: bool, names=None) -> None:
@@ -53,8 +50,8 @@ def _TIMING_EVENTS(name: str) -> list:
 
 
 def _launch(name: str, *args) -> None:
-    # gstex_raster_fwd_zero times as the forward, gstex_raster_bwd_hp as the backward
-    key = name[:-len("_zero")] if name.endswith("_zero") else name[:-len("_hp")] if name.endswith("_hp") else name
+    # gstex_raster_fwd_zero times as the forward
+    key = name[:-len("_zero")] if name.endswith("_zero") else name
     if _TIMING is None or key not in _TIMED:
         call(name, *args)
         return
@@ -118,22 +115,6 @@ def _c2w(c2w) -> torch.Tensor | None:
 
 def _stream(t: torch.Tensor) -> int:
     return _lib.stream_of(t.device)
-
-
-_ORDER_STREAMS: dict = {}
-# 1: the backward's unit ordering on a side stream right after the forward, overlapping the loss kernels (round 3:
-# 10-20 us faster); round 4, with the lighter timing events, the cross-stream fork / join costs what the overlap saves
-# (A/B, three interleaved 60-step triples: in stream 2.353-2.361 ms mean vs 2.362-2.364 on the side stream), so the
-# backward orders its units itself by default
-_ORDER_SIDE = os.environ.get("GSTEX_ORDER_SIDE", "0") != "0"
-
-
-def _order_stream(dev: torch.device) -> torch.cuda.Stream:
-    """The side stream the backward's unit ordering runs on (one per device)."""
-    s = _ORDER_STREAMS.get(dev.index)
-    if s is None:
-        s = _ORDER_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
-    return s
 
 
 # ----------------------------------------------------------------------------------------
@@ -524,15 +505,9 @@ class _TextureGaussians(torch.autograd.Function):
         # backward-only buffers only when a backward can follow: not under torch.no_grad() (eval renders of
         # trainable parameters), where apply() records no graph whatever the inputs' requires_grad
         needs_bwd = bool(grad_enabled) and any(ctx.needs_input_grad)
-        # the near-edge-on splats' fp64 pair-evaluation inputs for the backward (gstex_raster_setup_hp; rows written
-        # only for the flagged splats): off unless GSTEX_HP_RECORD=1 -- measured not to close the fp32-record floor
-        # and to cost backward time, so the training path passes none
-        rec_hp = (torch.empty((n, HP_DOUBLES), device=dev, dtype=torch.float64) if needs_bwd and _HP_RECORD
-                  else None)
-        _launch("gstex_raster_setup_hp", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
+        _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
                 ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam,
-                ptr(records), ptr(rec_hp), st)
-        ctx.rec_hp = rec_hp
+                ptr(records), st)
         ctx.v_texture = None
         ctx.sink = texture_grad_sink is not None
         ctx.on_texture_grad = on_texture_grad
@@ -602,21 +577,6 @@ class _TextureGaussians(torch.autograd.Function):
              ptr(state), n_isect, ptr(aux), ptr(zbuf), 0 if zbuf is None else zbuf.numel(), ptr(ctx.partials),
              0 if ctx.partials is None else ctx.partials.numel(), st)
         ctx.aux = aux
-        ctx.order_ready = None
-        if aux is not None and n_isect > 0 and _ORDER_SIDE:
-            # the backward's unit launch order (a scan and a scatter over the forward's per-unit costs, ~18 us of
-            # latency-bound launches) on a side stream, overlapping the loss kernels that run before the backward
-            # (fork and join by device-scope ordering events: a default event's system-scope release writes the
-            # caches back at each of these points)
-            main = torch.cuda.current_stream(dev)
-            side = _order_stream(dev)
-            fork = _lib.OrderEvent()
-            fork.record(stream=main.cuda_stream)
-            fork.wait(stream=side.cuda_stream)
-            _launch("gstex_raster_bwd_order", cam, C, n_isect, ptr(aux), side.cuda_stream)
-            ctx.order_ready = _lib.OrderEvent()
-            ctx.order_ready.record(stream=side.cuda_stream)
-            aux.record_stream(side)
         ctx.save_for_backward(means, scales, quats, opacities, umap, vmap, texture, nth, offsets, tile_ranges,
                               order, sorted_ids, sorted_slots, records, state, vm, cw if cw is not None else vm,
                               bg if bg is not None else vm)
@@ -668,18 +628,11 @@ class _TextureGaussians(torch.autograd.Function):
             row_flags = None
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
-        if ctx.order_ready is not None:  # the unit order was computed on the side stream after the forward
-            ctx.order_ready.wait(stream=torch.cuda.current_stream(dev).cuda_stream)
-            settings_b = int(settings) | _lib.BWD_ORDERED
-        else:
-            settings_b = settings
-        _launch("gstex_raster_bwd_hp", cam, C, settings_b, ptr(bg), ptr(records), ptr(tile_ranges),
+        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
-                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux),
-                ptr(ctx.rec_hp), st)
+                ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)
         ctx.aux = None
-        ctx.rec_hp = None
         if ctx.sink:
             if ctx.on_texture_grad is not None:
                 ctx.on_texture_grad()  # the texel gradient is complete in stream order
@@ -693,7 +646,7 @@ class _TextureGaussians(torch.autograd.Function):
         v_uv0 = torch.empty((n, 1, 2), device=dev, dtype=torch.float32)
         _launch("gstex_raster_setup_bwd_aabb" if ctx.fold_aabb else "gstex_raster_setup_bwd", n, ptr(means),
                 ptr(scales), glob, ptr(quats), ptr(opacities), ptr(umap), ptr(vmap), ptr(nth), ptr(offsets), ptr(partials),
-                ptr(row_flags), row_floats, cam,
+                ptr(row_flags), row_floats, n_isect if row_flags is not None else -1, cam,
                 ptr(v_means), ptr(v_scales), ptr(v_quats), ptr(v_rgbs), ptr(v_opac), ptr(v_centers), ptr(v_uv0), st)
         v_bg = None
         if ctx.needs_input_grad[26]:

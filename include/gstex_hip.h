@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 14
+#define GSTEX_ABI_VERSION 15
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -51,10 +51,6 @@ extern "C" {
 #define GSTEX_SETTING_DIST_REG (1 << 10) /* 2DGS NDC depth-distortion output */
 #define GSTEX_SETTING_EDIT (1 << 13)     /* texture_edit request (gstex.py:599) */
 #define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198): normal output unit-length, forward only */
-/* gstex_raster_bwd only (ABI 12): the backward's unit launch order was already computed on this aux by
- * gstex_raster_bwd_order (e.g. on a side stream while the loss kernels run): the backward skips it. */
-#define GSTEX_BWD_ORDERED (1 << 30)
-
 typedef enum {
     GSTEX_OK = 0,
     GSTEX_ERR_INVALID_ARG = 1,
@@ -188,15 +184,6 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
                        const float* vmap, const int32_t* texture_dims,
                        const int32_t* num_tiles_hit, const gstex_camera* cam, float* records,
                        void* stream);
-/* gstex_raster_setup that also writes, for every near-edge-on splat (|normal . view direction| < 0.05 at its
- * centre), the fp64 inputs of its pair evaluation into rec_hp[n][10] (A.xyz, B.xyz, Pz, anchor x, y; caller-owned,
- * only flagged rows written) and flags its record; gstex_raster_bwd_hp then takes that splat's gradient inputs (dx,
- * dy, 1 / p.z, u, v) from them, fp64-evaluated, with the pair decisions unchanged.  ABI 13. */
-int gstex_raster_setup_hp(int32_t n, const float* means, const float* scales, float glob_scale,
-                          const float* quats, const float* rgbs, const float* opacities, const float* centers,
-                          const float* uv0, const float* umap, const float* vmap, const int32_t* texture_dims,
-                          const int32_t* num_tiles_hit, const gstex_camera* cam, float* records, double* rec_hp,
-                          void* stream);
 /* Texel values: the texels are read as tex_scale * texture + tex_bias (1, 0 = as stored), so a caller
  * that keeps SH-DC coefficients (gstex.py:1119 passes SH2RGB(texture_dc) = 0.28209 x + 0.5) can pass the
  * store itself; the backward's v_texture is then the gradient w.r.t. the stored values. */
@@ -257,27 +244,19 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const float* v_img, const float* v_depth, const float* v_reg, const float* v_alpha,
                      const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
                      uint32_t* row_flags, float* v_texture, void* aux, void* stream);
-/* gstex_raster_bwd with the near-edge-on splats' fp64 inputs from gstex_raster_setup_hp (rec_hp; NULL = none). */
-int gstex_raster_bwd_hp(const gstex_camera* cam, int32_t channels, int32_t settings, const float* background,
-                        const float* records, const int32_t* tile_ranges, const int32_t* sorted_ids,
-                        const int32_t* sorted_slots, const float* texture, int64_t n_texels, float tex_scale,
-                        float tex_bias, const float* state, const float* v_img, const float* v_depth,
-                        const float* v_reg, const float* v_alpha, const float* v_tex, const float* v_normal,
-                        int64_t n_isect, float* partials, uint32_t* row_flags, float* v_texture, void* aux,
-                        const double* rec_hp, void* stream);
-/* The backward's unit launch order alone (ABI 12): computed from the forward's aux (its per-unit costs and
- * histogram) into the same aux; a gstex_raster_bwd whose settings carry GSTEX_BWD_ORDERED then skips it.  Lets
- * the ordering run on another stream between the forward and the backward. */
-int gstex_raster_bwd_order(const gstex_camera* cam, int32_t channels, int64_t n_isect, void* aux, void* stream);
 /* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
  * them to the splat parameters. Outputs are overwritten.  partials is consumed: each splat's sums are written
  * over its first row (the rows are backward scratch, not read again).  row_flags == NULL: partials is the
- * backward's (n, row_floats) per-splat accumulator (gstex_raster_bwd without row_flags), chained directly. */
+ * backward's (n, row_floats) per-splat accumulator (gstex_raster_bwd without row_flags), chained directly.
+ * n_rows (ABI 15): the pair capacity the rows were allocated for (n_rows * 4 rows), or -1 when offsets[n] is
+ * known to fit; with capacity-sized pair buffers (gstex_bin_sort_capped) a total offsets[n] > n_rows means the
+ * binning left every tile empty, and every splat is then chained as pair-free (zero gradients) without reading
+ * rows past the allocation. */
 int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,
                            const float* quats, const float* opacities, const float* umap,
                            const float* vmap, const int32_t* num_tiles_hit,
                            const int32_t* offsets, float* partials, const uint32_t* row_flags,
-                           int32_t row_floats, const gstex_camera* cam, float* v_means, float* v_scales,
+                           int32_t row_floats, int64_t n_rows, const gstex_camera* cam, float* v_means, float* v_scales,
                            float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                            float* v_uv0, void* stream);
 /* gstex_raster_setup_bwd with gstex_aabb_2d_bwd folded in: for callers whose centres came from
@@ -288,7 +267,8 @@ int gstex_raster_setup_bwd_aabb(int32_t n, const float* means, const float* scal
                                 const float* quats, const float* opacities, const float* umap,
                                 const float* vmap, const int32_t* num_tiles_hit,
                                 const int32_t* offsets, float* partials, const uint32_t* row_flags,
-                                int32_t row_floats, const gstex_camera* cam, float* v_means, float* v_scales,
+                                int32_t row_floats, int64_t n_rows, const gstex_camera* cam, float* v_means,
+                                float* v_scales,
                                 float* v_quats, float* v_rgbs, float* v_opacities, float* v_centers,
                                 float* v_uv0, void* stream);
 

@@ -320,25 +320,6 @@ def test_outputs_independent_of_launch_order(monkeypatch, deterministic):
     assert float((t1 - t2).abs().max()) <= 1e-6 * float(t1.abs().max())
 
 
-@pytest.mark.parametrize("side", [False, True])
-def test_backward_unit_order_on_a_side_stream(monkeypatch, deterministic, side):
-    """GSTEX_ORDER_SIDE: the backward's unit ordering launched on a side stream right after the forward (device-scope
-    ordering events, ABI 14) or inside the backward (the default): the same outputs and gradients."""
-    from gstex_amd import ops
-
-    case = make_case(n=400, n_texels=20000, H=80, W=96, seed=14)
-    monkeypatch.setattr(ops, "_ORDER_SIDE", False)
-    f1, g1 = gpu_run(case, grads=True)
-    monkeypatch.setattr(ops, "_ORDER_SIDE", side)
-    f2, g2 = gpu_run(case, grads=True)
-    for k in f1:
-        assert torch.equal(f1[k], f2[k]), k
-    for k in ["rgbs", "opacities", "means", "scales", "quats", "centers", "uv0"]:
-        assert torch.equal(g1[k], g2[k]), k
-    t1, t2 = g1["texture"].double(), g2["texture"].double()
-    assert float((t1 - t2).abs().max()) <= 1e-6 * float(t1.abs().max())
-
-
 # ---------------------------------------------------------------- SH / texture_sample
 @pytest.mark.parametrize("K", [25, 30])  # LDS-staged kernels up to K = 25, direct kernels above
 @pytest.mark.parametrize("degree", [0, 1, 2, 3, 4])

@@ -83,10 +83,10 @@ def test_synced_step_matches_unsynced_across_rechart():
         dist.destroy_process_group()
 
 
-def test_async_texture_update_matches_sync_step():
-    """async_texture: the texel Adam update on a side stream (its gradient buffer zeroed by the next raster forward), overlapped with the
-    next step's preprocessing; alone and under GradSync (world 1), across an in-place rechart and an eval render,
-    it must train like the plain step."""
+def test_deferred_texture_update_across_rechart_and_eval():
+    """defer_texture: the texel Adam update of step k run inside step k+1's render (its gradient buffer zeroed by the
+    next raster forward); alone and with GradSync's flat buffer (world 1), across an in-place rechart and an eval
+    render, it must train like the plain step."""
     from gstex_amd.dist import GradSync
     from gstex_amd.model import GStexTrainer
     from gstex_amd.scene import make_scene, sphere_view
@@ -100,9 +100,9 @@ def test_async_texture_update_matches_sync_step():
         g = torch.Generator().manual_seed(1)
         gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(3)]
         plain = GStexTrainer(sc, dev, start_step=3000)
-        alone = GStexTrainer(sc, dev, start_step=3000, async_texture=True)
-        synced = GStexTrainer(sc, dev, start_step=3000, async_texture=True)
-        assert alone.async_texture and synced.async_texture
+        alone = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+        synced = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+        assert alone.defer_texture and synced.defer_texture
         sync = GradSync(synced, 1)
         for step in range(5):
             for tr in (plain, alone):
@@ -132,7 +132,7 @@ def test_async_texture_update_matches_sync_step():
         assert float(sync.flat[sync._tail_off:].abs().max()) == 0.0
         for other in (alone, synced):
             for (name, a), b in zip(plain.param_groups().items(), other.param_groups().values()):
-                _assert_trains_alike(name, a[0], b[0], "async texel update")
+                _assert_trains_alike(name, a[0], b[0], "deferred texel update")
     finally:
         dist.destroy_process_group()
 
@@ -327,10 +327,14 @@ def test_pair_capacity_step_trains_like_the_readback_step():
         _assert_trains_alike(name, a[0], b[0], "capacity-mode step")
 
 
-def test_pair_capacity_overflow_skips_the_update_and_grows():
+@pytest.mark.parametrize("det", [False, True])
+def test_pair_capacity_overflow_skips_the_update_and_grows(request, det):
     """A capacity below the pair total: the render comes out empty, every Adam launch of the step (the deferred texel
     update included) leaves parameters and moments untouched, the host finds the overflow from the totals it polls,
-    grows the capacity, and the next step trains."""
+    grows the capacity, and the next step trains.  det: under torch.use_deterministic_algorithms(True) (per-pair rows
+    sized by the capacity, ADVICE r04: setup_bwd must not address rows past them when the total overflows)."""
+    if det:
+        request.getfixturevalue("deterministic")
     from gstex_amd import ops
     from gstex_amd.loss import photometric_loss
     from gstex_amd.model import GStexTrainer
