@@ -5,6 +5,7 @@ os.exec*), gloo carrying the collectives between ranks that share the box's one 
 check (the all-reduced gradient every Adam launch consumes vs the single-rank mean gradient) to pass:
   * cfg4's step at cfg3 size: 200k splats, 1e7 texels, 800x800, world 2, the deferred texel update with the
     head-first exchange and the tail in 4 pieces (~30 MB each), deterministic splat sums (bit-exact splat groups);
+    and the same at world 8, cfg4's eight views per step;
   * cfg5's step: world 4 at 1600x1200 with depth / distortion / normal rendered and regularised (the geometry backward
     under the exchange), 200k splats, 1e7 texels.
 The only part of cfg4 / cfg5 these do not run is RCCL across physical GPUs (the driver's multi-GPU bench).
@@ -51,6 +52,16 @@ def _rehearse(name, world, *args, timeout=240):
 def test_cfg4_step_world2_at_cfg3_size():
     _rehearse("cfg4_w2", 2, "--n-splats", "200000", "--n-texels", "1e7", "--size", "800", "--defer-texture",
               "--deterministic")
+
+
+@pytest.mark.timeout(600)
+def test_cfg4_step_world8_at_cfg3_size():
+    """cfg4 as the driver's 8-GPU node runs it: eight ranks, one camera pose each per step (poses 0-7), 200k splats, 1e7
+    texels, 800x800, the deferred texel update with the head-first exchange and the tail in 4 pieces; every group's
+    all-reduced gradient within 1e-5 of the single-rank mean of the same eight views.  All eight
+    ranks share the box's one GPU (gloo collectives); RCCL across GPUs is the driver's."""
+    _rehearse("cfg4_w8", 8, "--n-splats", "200000", "--n-texels", "1e7", "--size", "800", "--defer-texture",
+              timeout=540)
 
 
 @pytest.mark.timeout(300)
