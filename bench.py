@@ -305,7 +305,10 @@ def main():
             transient = torch.cuda.max_memory_allocated(dev) - torch.cuda.memory_allocated(dev)
             torch.empty(2 * transient, dtype=torch.uint8, device=dev)
         step()
-    trainer.wait_texture()  # the last warmup step's deferred texel update, outside the timed region
+    # the last warmup step's deferred texel update stays pending: it is the first kernel of the first timed step (as
+    # every step starts with the previous step's texel update), and the last timed step's update runs after the timed
+    # region -- K steps, K texel updates, and the first timed step starts with ~90 us of device work queued instead of
+    # an idle device waiting for the host's first launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -327,11 +330,11 @@ def main():
         step()
         bound[k + 1].record()
         host_s.append(time.perf_counter() - h0)
-    trainer.wait_texture()  # the last timed step's deferred texel update, inside: K steps = K texel updates
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    trainer.wait_texture()  # the last timed step's deferred texel update (the first timed step ran the warmup's)
     peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20
     raster_ev = {n: ops._TIMING_EVENTS(n) for n in ("gstex_raster_fwd", "gstex_raster_bwd")}
     kt = ops.kernel_times()
@@ -487,8 +490,9 @@ def main():
             "pair_buffers": ("capacity-sized, pair total kept on the device: no host read-back or synchronisation in "
                              "the step (ops.PairCapacity, capacity %d)" % trainer.pairs.capacity
                              if trainer.pairs is not None else "sized by a host read-back of the pair total"),
-            "texture_update": ("deferred: step k's texel Adam update runs in step k+1's render (same stream, "
-                                    "before the raster forward); the timed region holds exactly K texel updates"
+            "texture_update": ("deferred: step k's texel Adam update is the first kernel of step k+1 (same stream, "
+                                    "before the raster forward); the timed region holds exactly K texel updates "
+                                    "(the last warmup step's and those of timed steps 1..K-1)"
                                if trainer.defer_texture
                                else "compute stream"),
         },

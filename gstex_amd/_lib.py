@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.a
 
 ABI_VERSION = 15
 REC_FLOATS = 32
+BWD_SPLIT = 1 << 29  # GSTEX_BWD_SPLIT: gstex_raster_bwd's split (texel-only pixel-major + splat-parallel) backward
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
 SETTING_AA_BLUR = 1 << 9

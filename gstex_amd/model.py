@@ -271,6 +271,12 @@ class GStexTrainer:
         the trainer's geometry_outputs)."""
         means = self.means
         deg = self.sh_degree if sh_degree_now is None else sh_degree_now
+        if self._pending_tex is not None and not self._pending_collective and self.pairs is not None:
+            # the deferred texel update first (read-back-free step: there is no pair-count wait to fill): ~90 us of
+            # streaming work the device starts on while the host enqueues the step's short preprocessing and binning
+            # launches, instead of idling through them after a synchronisation (the bench's first timed step); it only
+            # has to land before the raster forward, the first reader of the texels
+            self._run_pending_texture()
         if self.fused_activations:  # one HIP launch each way (gstex_amd.activations)
             quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
                 means, self.quats, self.scales, self.opacities, self.mappings, view.campos)

@@ -8,6 +8,7 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 from typing import NamedTuple, Tuple
 
@@ -17,6 +18,9 @@ from . import _lib
 from ._lib import PARTIAL_FLOATS, PARTIAL_FLOATS_PHOTO, REC_FLOATS, call, ptr
 
 BLOCK_WIDTH = 16
+# GSTEX_BWD_SPLIT=1: the photometric backward as the split pair (gstex_raster_bwd with GSTEX_BWD_SPLIT, ABI 15) -- an
+# experiment, off by default (measured slower than the single pixel-major kernel)
+BWD_SPLIT = os.environ.get("GSTEX_BWD_SPLIT", "0") != "0"
 
 # ----------------------------------------------------------------------------------------
 # optional per-kernel timing: HIP events recorded on the stream each kernel is launched on
@@ -628,7 +632,8 @@ class _TextureGaussians(torch.autograd.Function):
             row_flags = None
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
-        _launch("gstex_raster_bwd", cam, C, settings, ptr(bg), ptr(records), ptr(tile_ranges),
+        _launch("gstex_raster_bwd", cam, C, int(settings) | (_lib.BWD_SPLIT if BWD_SPLIT else 0), ptr(bg), ptr(records),
+                ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
                 ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)

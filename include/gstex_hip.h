@@ -51,6 +51,12 @@ extern "C" {
 #define GSTEX_SETTING_DIST_REG (1 << 10) /* 2DGS NDC depth-distortion output */
 #define GSTEX_SETTING_EDIT (1 << 13)     /* texture_edit request (gstex.py:599) */
 #define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198): normal output unit-length, forward only */
+/* gstex_raster_bwd only (ABI 15): the split backward for the photometric C = 3 case with float-atomic splat sums
+ * (row_flags NULL, no depth / normal / distortion gradient) -- texel gradients by the pixel-major kernel alone, splat
+ * gradients by a splat-parallel kernel (one splat per lane, lane scans for transmittance and colour behind).  Same
+ * results within fp32 rounding; an experiment kept off by default.  Ignored in every other case. */
+#define GSTEX_BWD_SPLIT (1 << 29)
+
 typedef enum {
     GSTEX_OK = 0,
     GSTEX_ERR_INVALID_ARG = 1,

@@ -78,7 +78,7 @@ class OracleTrainer:
         sim = 1 - ssim(gt.permute(2, 0, 1)[None], rgb.permute(2, 0, 1)[None])
         loss = 0.8 * l1 + 0.2 * sim
         loss.backward()
-        return float(loss)
+        return float(loss.detach())
 
     def zero_grad(self):
         self.optimizer.zero_grad(set_to_none=True)
