@@ -309,6 +309,7 @@ def main():
     # every step starts with the previous step's texel update), and the last timed step's update runs after the timed
     # region -- K steps, K texel updates, and the first timed step starts with ~90 us of device work queued instead of
     # an idle device waiting for the host's first launches
+    carried = trainer._pending_tex is not None  # the first timed step runs the last warmup step's texel update
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -383,7 +384,10 @@ def main():
     exchange = None
     if sync is not None and sync.phase_events and kt.get("gstex_raster_bwd") and kt.get("gstex_raster_fwd"):
         # per step k: raster bwd end -> head landed -> tail landed (in step k+1's render) -> next raster fwd start
-        pe = sync.phase_events
+        pe = dict(sync.phase_events)
+        if carried and pe.get("tail"):
+            # the first timed step's deferred update (and its tail landing) belongs to the last warmup step
+            pe["tail"] = pe["tail"][1:]
         bwd, fwd = raster_ev["gstex_raster_bwd"], raster_ev["gstex_raster_fwd"]
         rows = []
         for k in range(min(len(bwd), len(pe.get("head", [])), len(pe.get("tail", [])))):
