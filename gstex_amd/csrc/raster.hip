@@ -69,8 +69,12 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #define GSTEX_STAT(i, v) do { } while (0)
 #define GSTEX_STATW(i, v) do { } while (0)
 #endif
+#ifndef GSTEX_FWD_PREFETCH
+#define GSTEX_FWD_PREFETCH 0  // forward: next visit's record planes 0-3 read from LDS one visit ahead
+#endif
 #ifndef GSTEX_FWD_OCC
-#define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower)
+#define GSTEX_FWD_OCC (GSTEX_FWD_PREFETCH ? 5 : 6)  // forward waves per SIMD the register allocation targets (measured:
+                                                   // 8 at 64 VGPRs is slower)
 #endif
 #ifndef GSTEX_XCD_MB
 #define GSTEX_XCD_MB 2  // backward units of one 2x2-tile macro-block dispatched to one XCD (unit_order groups)
@@ -382,11 +386,43 @@ __device__ __forceinline__ int wave_max_i(int v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return __builtin_amdgcn_readfirstlane(v);
 }
-// sum over the wave, wave-uniform result (a bound, not a parity value: any summation order)
+// inclusive prefix product / sum over the 64 lanes (lane 0 first): in-row Hillis-Steele steps (row_shr 1, 2, 4, 8; a
+// lane whose source lies before its row start is not written, i.e. multiplied by 1 / added 0), then rows 1, 3 take
+// lane 15 of the row before and rows 2, 3 lane 31 (row_bcast).  s_nop 1 covers each VALU-write -> DPP-read hazard.
+__device__ __forceinline__ float lane_scan_mul(float v) {
+    asm volatile("s_nop 1\n"
+                 "v_mul_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_mul_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_mul_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_mul_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_mul_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
+                 "v_mul_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n s_nop 1"
+                 : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ float lane_scan_add(float v) {
+    asm volatile("s_nop 1\n"
+                 "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
+                 "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n s_nop 1"
+                 : "+v"(v));
+    return v;
+}
+// lane l - 1's value (0 in lane 0): the exclusive scan from the inclusive one
+__device__ __forceinline__ float lane_shift_up(float v) {
+    float r;
+    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 1"
+                 : "=v"(r) : "v"(v));
+    return r;
+}
+
+// sum over the wave, wave-uniform result (a bound, not a parity value: any summation order): the DPP lane scan's
+// last lane, no LDS round trips (ds_bpermute shuffles would put six serial LDS latencies on the visit's chain)
 __device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lane_scan_add(v)), 63));
 }
 
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
@@ -716,11 +752,29 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         bool all_done = __all(GSTEX_FWD_DONE);
         for (int hb = 0; hb < kWords && !all_done; ++hb) {
           unsigned long long m = todo[hb];
+#if GSTEX_FWD_PREFETCH
+          // the cull / evaluation planes (0-3) of the next visited record are read from LDS one visit ahead, so their
+          // latency overlaps the current visit instead of opening it
+          int jc = hb * 64 + (m ? __builtin_ctzll(m) : 0);
+          float4 q0 = s_rec[0 * kFwdBatch + jc], q1 = s_rec[1 * kFwdBatch + jc];
+          float4 q2 = s_rec[2 * kFwdBatch + jc], q3 = s_rec[3 * kFwdBatch + jc];
+#endif
           while (m) {
+#if GSTEX_FWD_PREFETCH
+            const int j = jc;
+            m &= m - 1;
+            jc = m ? hb * 64 + __builtin_ctzll(m) : jc;
+            const float4 n0 = s_rec[0 * kFwdBatch + jc], n1 = s_rec[1 * kFwdBatch + jc];
+            const float4 n2 = s_rec[2 * kFwdBatch + jc], n3 = s_rec[3 * kFwdBatch + jc];
+            const Rec r = rec_from_planes(q0, q1, q2, q3, s_rec[4 * kFwdBatch + j], s_rec[5 * kFwdBatch + j],
+                                          s_rec[6 * kFwdBatch + j], s_rec[7 * kFwdBatch + j]);
+            q0 = n0; q1 = n1; q2 = n2; q3 = n3;
+#else
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
-            ++seg_visits;
             const Rec r = read_rec<kFwdBatch>(s_rec, j);
+#endif
+            ++seg_visits;
             Hit h;
             const bool ok = eval_hit(r, px, py, aa, h) && alive != 0.0f;
             const float test_T = T * (1.0f - h.alpha);
@@ -1488,39 +1542,6 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 #define GSTEX_SPLAT_WAVES 4
 #endif
 constexpr int kPxF = 12;  // per-pixel LDS record: T_end, S_end, last (bits), Ga, Gimg[3], Gtex[3], tex_bias term, pad
-
-// inclusive prefix product / sum over the 64 lanes (lane 0 first): in-row Hillis-Steele steps (row_shr 1, 2, 4, 8; a
-// lane whose source lies before its row start is not written, i.e. multiplied by 1 / added 0), then rows 1, 3 take
-// lane 15 of the row before and rows 2, 3 lane 31 (row_bcast).  s_nop 1 covers each VALU-write -> DPP-read hazard.
-__device__ __forceinline__ float lane_scan_mul(float v) {
-    asm volatile("s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n s_nop 1"
-                 : "+v"(v));
-    return v;
-}
-__device__ __forceinline__ float lane_scan_add(float v) {
-    asm volatile("s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n s_nop 1"
-                 : "+v"(v));
-    return v;
-}
-// lane l - 1's value (0 in lane 0): the exclusive scan from the inclusive one
-__device__ __forceinline__ float lane_shift_up(float v) {
-    float r;
-    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 1"
-                 : "=v"(r) : "v"(v));
-    return r;
-}
 
 __global__ __launch_bounds__(64) void lane_scan_probe_kernel(const float* in, float* out) {
     const float v = in[threadIdx.x];

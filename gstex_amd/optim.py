@@ -28,8 +28,13 @@ class FusedAdam(torch.optim.Optimizer):
         multiplies every gradient as it is read (gstex_adam_step_scaled: a data-parallel step's 1 / world, applied to the
         all-reduced sums -- bit-identical to averaging the buffer first); `skip_flag` (a 1-element device fp32 tensor)
         makes the launch a no-op on the device when the value is non-zero (gstex_adam_step_guarded: the pair-capacity
-        guard of the step's renders, ops.PairCapacity) -- the step counts still advance.  The launch goes to the
-        current stream."""
+        guard of the step's renders, ops.PairCapacity) -- the step counts still advance, deliberately: the host learns
+        of a skipped step only after the fact (no read-back in the step), so unlike GradScaler-style skipping (which
+        does not call step() at all) the next real update applies the bias corrections of step t + 1 to moments last
+        updated at step t - 1.  The moments themselves are untouched; the difference is a factor
+        (1 - beta^t) / (1 - beta^(t+1)) on each correction, which tends to 1 as t grows (< 1e-3 for beta1 = 0.9 once
+        t > 60, for beta2 = 0.999 once t > 7000), and an overflow grows the capacity, so it recurs only if the pair
+        total keeps jumping.  The launch goes to the current stream."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
