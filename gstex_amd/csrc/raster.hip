@@ -72,6 +72,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_FWD_PREFETCH
 #define GSTEX_FWD_PREFETCH 0  // forward: next visit's record planes 0-3 read from LDS one visit ahead
 #endif
+#ifndef GSTEX_FWD_HOIST
+#define GSTEX_FWD_HOIST 0  // forward: the contributing branch's record planes read with the evaluation's (experiment)
+#endif
 #ifndef GSTEX_FWD_OCC
 #define GSTEX_FWD_OCC (GSTEX_FWD_PREFETCH ? 5 : 6)  // forward waves per SIMD the register allocation targets (measured:
                                                    // 8 at 64 VGPRs is slower)
@@ -783,10 +786,20 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             GSTEX_STAT(11, __ballot(ok) ? 1 : 0);                 // ... with a contributing lane
             GSTEX_STAT(12, __popcll(__ballot(ok && !stop)));      // contributing lanes
             alive = stop ? 0.0f : alive;
+#if GSTEX_FWD_HOIST
+            // the contributing branch's record fields (planes 3-7) consumed here, ahead of the branch, so their LDS
+            // reads issue with the evaluation's and their latency hides behind it instead of opening the branch
+            const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
+            const int boff = __builtin_amdgcn_readfirstlane(r.off);
+            asm volatile("" ::"v"(r.rgb[0]), "v"(r.rgb[1]), "v"(r.rgb[2]), "v"(r.tu0), "v"(r.auu), "v"(r.auv),
+                         "v"(r.tv0), "v"(r.avu), "v"(r.avv), "v"(r.hm1), "v"(r.wm1));
+#endif
             if (ok && !stop) {
                 const float w = h.alpha * T;
+#if !GSTEX_FWD_HOIST
                 const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
                 const int boff = __builtin_amdgcn_readfirstlane(r.off);
+#endif
                 const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels && !(GSTEX_ABLATE & 4);
                 if (kDefer) {
                     // (computed whether or not the splat has texels: used only when it has)

@@ -1,10 +1,10 @@
 #!/bin/bash
 # GPU-box side of an A/B run: raster-only cfg3 loop (photometric upstream grads) for every
-# scratch/<variant>/libgstex_hip.so given on the command line, then (optional) stall-counter passes.
+# scratch/<variant>/libgstex_hip.so given on the command line (the bench's variant: no geometry outputs), then (optional) stall-counter passes.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/ablate; mkdir -p $OUT
 for v in "$@"; do
-  GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 120 python3 tools/raster_loop.py --photometric --iters 20 > $OUT/$v.log 2>&1 || { echo "FAIL $v"; exit 1; }
+  GSTEX_LIB=scratch/$v/libgstex_hip.so timeout -k 10 120 python3 tools/raster_loop.py --photometric --no-geometry --iters 20 > $OUT/$v.log 2>&1 || { echo "FAIL $v"; exit 1; }
   echo "$v: $(tail -2 $OUT/$v.log | tr '\n' ' ')"
 done
 if [ -n "$PMC" ]; then
