@@ -72,6 +72,13 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_FWD_PREFETCH
 #define GSTEX_FWD_PREFETCH 0  // forward: next visit's record planes 0-3 read from LDS one visit ahead
 #endif
+#ifndef GSTEX_FWD_ORDER
+#define GSTEX_FWD_ORDER 0  // forward tile launch order (experiment): 0 the binning's largest-first order, 1 row-major,
+                           // 2 XCD macro-blocks (GSTEX_FWD_MB^2 tiles dealt to one XCD back to back, row-major)
+#endif
+#ifndef GSTEX_FWD_MB
+#define GSTEX_FWD_MB 4
+#endif
 #ifndef GSTEX_FWD_HOIST
 #define GSTEX_FWD_HOIST 0  // forward: the contributing branch's record planes read with the evaluation's (experiment)
 #endif
@@ -228,6 +235,32 @@ __device__ __forceinline__ WaveBlock wave_block(int tx, int ty, int tid) {
     b.wx1 = b.wx0 + 7.0f;
     b.wy1 = b.wy0 + 7.0f;
     return b;
+}
+
+// Experimental forward launch orders (GSTEX_FWD_ORDER 1, 2).  Mode 2: workgroups b and b + 8 share an XCD (blocks are
+// dealt round-robin over the 8 XCDs); position p = 8 r + g runs the r-th tile of XCD group g, whose tiles are the
+// MB x MB macro-blocks m = 8 k + g (row-major), each walked tile by tile -- a macro-block's tiles share splats and run
+// back to back on one XCD's L2.  Holes (-1): positions past the last macro-block or outside the tile grid.
+__host__ __device__ __forceinline__ int fwd_grid(int tiles_x, int tiles_y) {
+#if GSTEX_FWD_ORDER == 2
+    const int mbx = (tiles_x + GSTEX_FWD_MB - 1) / GSTEX_FWD_MB, mby = (tiles_y + GSTEX_FWD_MB - 1) / GSTEX_FWD_MB;
+    return 8 * GSTEX_FWD_MB * GSTEX_FWD_MB * ((mbx * mby + 7) / 8);
+#else
+    return tiles_x * tiles_y;
+#endif
+}
+__device__ __forceinline__ int fwd_xcd_tile(int p, int tiles_x, int tiles_y) {
+#if GSTEX_FWD_ORDER == 2
+    constexpr int MB = GSTEX_FWD_MB;
+    const int g = p & 7, r = p >> 3;
+    const int m = 8 * (r / (MB * MB)) + g, q = r % (MB * MB);
+    const int mbx = (tiles_x + MB - 1) / MB, mby = (tiles_y + MB - 1) / MB;
+    if (m >= mbx * mby) return -1;
+    const int tx = (m % mbx) * MB + q % MB, ty = (m / mbx) * MB + q / MB;
+    return (tx < tiles_x && ty < tiles_y) ? ty * tiles_x + tx : -1;
+#else
+    return p;
+#endif
 }
 
 // Record j of a batch staged in LDS as [plane][splat] float4
@@ -632,7 +665,12 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
     const int ti = (int)blockIdx.x;
+#if GSTEX_FWD_ORDER == 0
     const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
+#else
+    const int tile = fwd_xcd_tile(ti, tiles_x, n_tiles / tiles_x);
+    if (tile < 0) return;  // a hole of the macro-block layout (whole workgroup, before any barrier)
+#endif
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = (int)threadIdx.x;
     const WaveBlock wb = wave_block(tx, ty, tid);
@@ -2092,7 +2130,7 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     zbuf.p[1] = zero_floats2 > 0 && !(GSTEX_ABLATE & 512) ? zero_buf2 : nullptr;
     zbuf.n[1] = zero_floats2;
 #define GSTEX_FWD(CC, GG)                                                                                      \
-    raster_fwd_kernel<CC, GG><<<nblk, kThreads, 0, st>>>(                                                      \
+    raster_fwd_kernel<CC, GG><<<fwd_grid(tiles_x, tiles_y), kThreads, 0, st>>>(                               \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg,     \
         out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf)
