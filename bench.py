@@ -75,6 +75,8 @@ def parse():
                    help="run the texel Adam update inside optimizer_step instead of deferring it into the next "
                         "step's render (GStexTrainer defer_texture)")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
+    p.add_argument("--no-graph", action="store_true",
+                   help="N = 1: enqueue every step eagerly instead of replaying it as a hipGraph (gstex_amd.graphs)")
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="diagnostics only: no HIP events around the raster launches (no roofline figures)")
     return p.parse_args()
@@ -269,11 +271,9 @@ def main():
     setup_s = time.perf_counter() - t_scene
     step_no = [0]
 
-    def step():
+    def body(pose):
         with torch.no_grad():  # stationary workload: same geometry every step (8.8 MB, one copy, timed)
             trainer.geometry_flat.copy_(geom0)
-        pose = (rank + step_no[0] * world) % N_POSES
-        step_no[0] += 1
         if sync is not None:
             sync.zero()  # one fill of the flat gradient buffer the .grad views live in
         else:
@@ -281,6 +281,33 @@ def main():
         trainer.forward_backward(views[pose], gts[pose])
         # N > 1: the collectives inside the step (texel group updated while the head's collective runs)
         trainer.optimizer_step(sync=sync)
+
+    # N = 1: each pose's step captured once as a hipGraph and replayed (one launch per step instead of ~40 launches
+    # and ~1 ms of Python; gstex_amd.graphs.StepGraphs): the same kernels, the same Adam scalars per step
+    timed = {"gstex_raster_bwd"} if world == 1 else {"gstex_raster_fwd", "gstex_raster_bwd"}
+    graphs = None
+    if world == 1 and not args.no_graph and args.warmup >= 1 and trainer.pairs is not None and trainer.defer_texture:
+        from gstex_amd.graphs import StepGraphs
+
+        graphs = StepGraphs(trainer, body, N_POSES, timed=() if args.no_kernel_timing else timed)
+
+    graph_error = [None]
+
+    def step(eager=False):
+        nonlocal graphs
+        pose = (rank + step_no[0] * world) % N_POSES
+        step_no[0] += 1
+        if graphs is not None and not eager and (graphs.stale or not graphs.slots):
+            try:
+                graphs.capture()
+            except Exception as ex:  # noqa: BLE001  (the eager step is the fallback; the line records why)
+                graph_error[0] = repr(ex)[:300]
+                graphs.slots, graphs = [], None
+                torch.cuda.synchronize()
+        if graphs is not None and not eager:
+            graphs.replay(pose)
+        else:
+            body(pose)
 
     # counted quantities for the roofline (every pose of this rank's cycle; the geometry is stationary), before the
     # warmup: host work between the warmup and the timed steps would idle the device and let its clock drop
@@ -304,7 +331,14 @@ def main():
             torch.cuda.synchronize()
             transient = torch.cuda.max_memory_allocated(dev) - torch.cuda.memory_allocated(dev)
             torch.empty(2 * transient, dtype=torch.uint8, device=dev)
-        step()
+        # the graphs are captured after two eager steps (the first sizes the pair capacity)
+        step(eager=w < 2)
+    if graphs is not None and (graphs.stale or not graphs.slots):
+        try:
+            graphs.capture()  # (--warmup < 3: captured here, outside the timed region)
+        except Exception as ex:  # noqa: BLE001
+            graph_error[0] = repr(ex)[:300]
+            graphs = None
     # the last warmup step's deferred texel update stays pending: it is the first kernel of the first timed step (as
     # every step starts with the previous step's texel update), and the last timed step's update runs after the timed
     # region -- K steps, K texel updates, and the first timed step starts with ~90 us of device work queued instead of
@@ -318,7 +352,6 @@ def main():
     # every event recorded into the stream is a marker packet the device waits on (≈ 4 us each, A/B measured), so the
     # timed loop records only what the line needs: one event per step boundary (K + 1, not 2 K) and, at N = 1, the
     # dominant kernel's pair (the raster backward); at N > 1 also the forward's, for the exchange's phase record
-    timed = {"gstex_raster_bwd"} if world == 1 else {"gstex_raster_fwd", "gstex_raster_bwd"}
     ops.set_kernel_timing(not args.no_kernel_timing, names=timed)
     if sync is not None and not args.no_kernel_timing:
         sync.phase_events = {}  # when the head / tail collectives land, on rank 0's compute stream
@@ -345,7 +378,7 @@ def main():
         # the raster forward's launch time from a few untimed steps right after the timed region (same workload)
         ops.set_kernel_timing(True, names={"gstex_raster_fwd"})
         for _ in range(6):
-            step()
+            step(eager=True)  # (the graphs time only the backward)
         trainer.wait_texture()
         kt.update(ops.kernel_times())
         ops.set_kernel_timing(False)
@@ -494,6 +527,11 @@ def main():
             "pair_buffers": ("capacity-sized, pair total kept on the device: no host read-back or synchronisation in "
                              "the step (ops.PairCapacity, capacity %d)" % trainer.pairs.capacity
                              if trainer.pairs is not None else "sized by a host read-back of the pair total"),
+            "step_launch": ("hipGraph replay: each pose's whole step (geometry restore, render, loss, backward, "
+                            "Adam) captured once and replayed, Adam bias corrections per step from device tables "
+                            "(gstex_amd.graphs.StepGraphs, gstex_adam_step_scheduled)" if graphs is not None
+                            else "eager: every launch enqueued by the host each step" +
+                            (f" (graph capture failed: {graph_error[0]})" if graph_error[0] else "")),
             "texture_update": ("deferred: step k's texel Adam update is the first kernel of step k+1 (same stream, "
                                     "before the raster forward); the timed region holds exactly K texel updates "
                                     "(the last warmup step's and those of timed steps 1..K-1)"

@@ -74,7 +74,8 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #endif
 #ifndef GSTEX_FWD_ORDER
 #define GSTEX_FWD_ORDER 0  // forward tile launch order (experiment): 0 the binning's largest-first order, 1 row-major,
-                           // 2 XCD macro-blocks (GSTEX_FWD_MB^2 tiles dealt to one XCD back to back, row-major)
+                           // 2 XCD macro-blocks (GSTEX_FWD_MB^2 tiles dealt to one XCD back to back, row-major),
+                           // 3 largest-first within XCD groups of MB x MB macro-blocks
 #endif
 #ifndef GSTEX_FWD_MB
 #define GSTEX_FWD_MB 4
@@ -120,7 +121,8 @@ constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
                         // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
-                        // 256 = no partial-row / flag stores, 512 = forward without the gradient-buffer zeroing
+                        // 256 = no partial-row / flag stores, 512 = forward without the gradient-buffer zeroing,
+                        // 1024 = forward texel gathers replaced by register values (addresses and arithmetic kept)
                         // (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
@@ -261,6 +263,30 @@ __device__ __forceinline__ int fwd_xcd_tile(int p, int tiles_x, int tiles_y) {
 #else
     return p;
 #endif
+}
+
+// GSTEX_FWD_ORDER 3 (experiment): largest-first inside XCD groups -- tile t belongs to group g(t) of its MB x MB
+// macro-block and runs at position 8 * (its rank by pair count within the group) + g(t); holes stay -1.
+__host__ __device__ __forceinline__ int fwd_group_of(int t, int tiles_x) {
+    const int mbw = (tiles_x + GSTEX_FWD_MB - 1) / GSTEX_FWD_MB;
+    return ((t % tiles_x) / GSTEX_FWD_MB + ((t / tiles_x) / GSTEX_FWD_MB) * mbw) & 7;
+}
+__global__ __launch_bounds__(256) void fwd_group_order_kernel(int n_tiles, int tiles_x,
+                                                              const int2* __restrict__ tile_ranges,
+                                                              int32_t* __restrict__ order) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= n_tiles) return;
+    const int g = fwd_group_of(t, tiles_x);
+    const int2 rt = tile_ranges[t];
+    const int c = rt.y - rt.x;
+    int r = 0;
+    for (int u = 0; u < n_tiles; ++u) {
+        if (fwd_group_of(u, tiles_x) != g) continue;
+        const int2 ru = tile_ranges[u];
+        const int cu = ru.y - ru.x;
+        r += (cu > c || (cu == c && u < t)) ? 1 : 0;
+    }
+    order[8 * r + g] = t;
 }
 
 // Record j of a batch staged in LDS as [plane][splat] float4
@@ -665,8 +691,9 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
     const int ti = (int)blockIdx.x;
-#if GSTEX_FWD_ORDER == 0
+#if GSTEX_FWD_ORDER == 0 || GSTEX_FWD_ORDER == 3
     const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
+    if (GSTEX_FWD_ORDER == 3 && tile < 0) return;
 #else
     const int tile = fwd_xcd_tile(ti, tiles_x, n_tiles / tiles_x);
     if (tile < 0) return;  // a hole of the macro-block layout (whole workgroup, before any barrier)
@@ -847,7 +874,16 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                     fold_pending();
                     if (has_tex) {
                         const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
-                        if constexpr (CM == 3) load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
+                        if constexpr (CM == 3) {
+                            if (GSTEX_ABLATE & 1024) {  // diagnostic: the gathers' values from the registers instead
+#pragma unroll
+                                for (int c = 0; c < 3; ++c) {
+                                    p00[c] = b.ax + c; p01[c] = b.ay + c; p10[c] = b.ax * c; p11[c] = b.ay * c;
+                                }
+                            } else {
+                                load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
+                            }
+                        }
                         else load_texel_quad<CM>(rs, b, bw, Cn, p00, p01, p10, p11);
                         pax = b.ax;
                         pay = b.ay;
@@ -2129,8 +2165,28 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     zbuf.n[0] = zero_floats;
     zbuf.p[1] = zero_floats2 > 0 && !(GSTEX_ABLATE & 512) ? zero_buf2 : nullptr;
     zbuf.n[1] = zero_floats2;
+    int fgrid = fwd_grid(tiles_x, tiles_y);
+#if GSTEX_FWD_ORDER == 3
+    {
+        static int32_t* s_order = nullptr;
+        static int s_cap = 0;
+        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int t = 0; t < nblk; ++t) ++cnt[fwd_group_of(t, tiles_x)];
+        int mx = 0;
+        for (int g = 0; g < 8; ++g) mx = cnt[g] > mx ? cnt[g] : mx;
+        fgrid = 8 * mx;
+        if (fgrid > s_cap) {
+            if (s_order) (void)hipFree(s_order);
+            if (hipMalloc(&s_order, (size_t)fgrid * 4) != hipSuccess) return launch_status("gstex_raster_fwd (order)");
+            s_cap = fgrid;
+        }
+        if (hipMemsetAsync(s_order, 0xFF, (size_t)fgrid * 4, st) != hipSuccess) return launch_status("gstex_raster_fwd");
+        fwd_group_order_kernel<<<(nblk + 255) / 256, 256, 0, st>>>(nblk, tiles_x, (const int2*)tile_ranges, s_order);
+        tile_order = s_order;
+    }
+#endif
 #define GSTEX_FWD(CC, GG)                                                                                      \
-    raster_fwd_kernel<CC, GG><<<fwd_grid(tiles_x, tiles_y), kThreads, 0, st>>>(                               \
+    raster_fwd_kernel<CC, GG><<<fgrid, kThreads, 0, st>>>(                                                    \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg,     \
         out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf)

@@ -316,7 +316,8 @@ class GStexTrainer:
             sink, zero_sink, on_grad = self.texture_grad_sink, self._sink_fresh, self.texture_grad_ready
         guard = None
         if self.pairs is not None and torch.is_grad_enabled():
-            self._poll_pairs()
+            if not torch.cuda.is_current_stream_capturing():  # (a captured step's owner polls between replays)
+                self._poll_pairs()
             guard = (self.pairs, self._skip_flag(), self._sink_fresh, self.step)
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,

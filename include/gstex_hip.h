@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 15
+#define GSTEX_ABI_VERSION 16
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -167,6 +167,19 @@ int gstex_event_record(void* event, void* stream);
 int gstex_event_elapsed(void* start, void* end, float* ms);
 int gstex_stream_wait_event(void* stream, void* event);
 int gstex_event_destroy(void* event);
+/* HIP-graph support (ABI 16; not in the reference, which has no graph capture).  A training step captured into a
+ * hipGraph (gstex_amd.graphs.StepGraphs) times its raster kernels with event-record nodes:
+ *   gstex_event_record_external: hipEventRecordWithFlags(hipEventRecordExternal) -- on a capturing stream it adds an
+ *     event-record node to the graph (a plain record there only orders the capture);
+ *   gstex_graph_event_nodes: nodes[i] = the event-record node of `graph` (a hipGraph_t) recording events[i]; an event no
+ *     node records is an error;
+ *   gstex_graph_exec_set_event: point that node of the instantiated graph `exec` (a hipGraphExec_t) at another event
+ *     (a fresh timing pair per replay). */
+int gstex_event_record_external(void* event, void* stream);
+int gstex_graph_event_nodes(void* graph, void* const* events, int32_t n, void** nodes);
+int gstex_graph_exec_set_event(void* exec, void* node, void* event);
+/* hipGraphUpload of an instantiated graph on `stream` (its first launch then pays no upload). */
+int gstex_graph_upload(void* exec, void* stream);
 int gstex_scan_offsets_guarded(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
                                size_t workspace_bytes, const gstex_pair_guard* guard, void* stream);
 int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* centers, const float* extents,
@@ -380,6 +393,21 @@ int gstex_adam_step_scaled(int32_t n_tensors, const gstex_adam_tensor* tensors, 
  * data-parallel training so that every rank skips the same steps.  ABI 13. */
 int gstex_adam_step_guarded(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                             double eps, int32_t flags, float grad_scale, const float* skip, void* stream);
+/* gstex_adam_step_guarded whose per-tensor step_size and bias_correction2_sqrt are read on the device (ABI 16): for
+ * tensor i, row base[i] + *counter of table[i] (float pairs (step_size, bias_correction2_sqrt), rows[i] of them, the
+ * row index clamped to the table).  For a hipGraph replayed many times (gstex_amd.graphs.StepGraphs): the host keeps
+ * the tables (the same python-double bias corrections the per-call entry points take, one row per step t) and the
+ * graph advances *counter once per replay, so replay r applies the bias corrections of step t0 + r.  The tensors'
+ * step_size / bias_correction2_sqrt fields are ignored. */
+typedef struct gstex_adam_schedule {
+    const int32_t* counter;
+    const float* table[GSTEX_ADAM_MAX_TENSORS];
+    int32_t base[GSTEX_ADAM_MAX_TENSORS];
+    int32_t rows[GSTEX_ADAM_MAX_TENSORS];
+} gstex_adam_schedule;
+int gstex_adam_step_scheduled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
+                              double eps, int32_t flags, float grad_scale, const float* skip,
+                              const gstex_adam_schedule* schedule, void* stream);
 
 #ifdef __cplusplus
 }

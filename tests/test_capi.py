@@ -37,7 +37,7 @@ def test_every_header_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.gstex_abi_version() == _lib.ABI_VERSION == 15
+    assert lib.gstex_abi_version() == _lib.ABI_VERSION == 16
 
 
 def test_workspace_size_queries(lib):
