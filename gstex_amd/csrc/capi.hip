@@ -116,10 +116,30 @@ extern "C" int gstex_event_destroy(void* event) {
 }
 
 // HIP-graph support (ABI 16, see gstex_hip.h)
+// On a capturing stream: an event-record node appended after the capture's current dependencies, which then become
+// that node (what hipEventRecordWithFlags(hipEventRecordExternal) is specified to do; that call fails on this runtime
+// during capture); otherwise a plain record.
 extern "C" int gstex_event_record_external(void* event, void* stream) {
-    if (!event || hipEventRecordWithFlags((hipEvent_t)event, gstex::as_stream(stream), hipEventRecordExternal) !=
-                      hipSuccess) {
-        gstex::set_error("gstex_event_record_external: hipEventRecordWithFlags failed");
+    if (!event) {
+        gstex::set_error("gstex_event_record_external: null event");
+        return GSTEX_ERR_INVALID_ARG;
+    }
+    const hipStream_t st = gstex::as_stream(stream);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t n_deps = 0;
+    hipError_t e = hipStreamGetCaptureInfo_v2(st, &cs, nullptr, &graph, &deps, &n_deps);
+    if (e != hipSuccess) {
+        gstex::set_error("gstex_event_record_external: hipStreamGetCaptureInfo_v2: %s", hipGetErrorString(e));
+        return GSTEX_ERR_LAUNCH;
+    }
+    if (cs != hipStreamCaptureStatusActive) return gstex_event_record(event, stream);
+    hipGraphNode_t node = nullptr;
+    e = hipGraphAddEventRecordNode(&node, graph, deps, n_deps, (hipEvent_t)event);
+    if (e == hipSuccess) e = hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
+    if (e != hipSuccess) {
+        gstex::set_error("gstex_event_record_external: event-record node: %s", hipGetErrorString(e));
         return GSTEX_ERR_LAUNCH;
     }
     return GSTEX_OK;
@@ -158,10 +178,13 @@ extern "C" int gstex_graph_event_nodes(void* graph, void* const* events, int32_t
 }
 
 extern "C" int gstex_graph_exec_set_event(void* exec, void* node, void* event) {
-    if (!exec || !node || !event ||
-        hipGraphExecEventRecordNodeSetEvent((hipGraphExec_t)exec, (hipGraphNode_t)node, (hipEvent_t)event) !=
-            hipSuccess) {
-        gstex::set_error("gstex_graph_exec_set_event: hipGraphExecEventRecordNodeSetEvent failed");
+    if (!exec || !node || !event) {
+        gstex::set_error("gstex_graph_exec_set_event: null argument");
+        return GSTEX_ERR_INVALID_ARG;
+    }
+    const hipError_t e = hipGraphExecEventRecordNodeSetEvent((hipGraphExec_t)exec, (hipGraphNode_t)node, (hipEvent_t)event);
+    if (e != hipSuccess) {
+        gstex::set_error("gstex_graph_exec_set_event: hipGraphExecEventRecordNodeSetEvent: %s", hipGetErrorString(e));
         return GSTEX_ERR_LAUNCH;
     }
     return GSTEX_OK;

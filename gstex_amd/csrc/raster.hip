@@ -80,11 +80,14 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #ifndef GSTEX_FWD_MB
 #define GSTEX_FWD_MB 4
 #endif
+#ifndef GSTEX_FWD_DEFER2
+#define GSTEX_FWD_DEFER2 0  // forward: texel gathers folded two visits later (two pending sets; experiment, C = 3 only)
+#endif
 #ifndef GSTEX_FWD_HOIST
 #define GSTEX_FWD_HOIST 0  // forward: the contributing branch's record planes read with the evaluation's (experiment)
 #endif
 #ifndef GSTEX_FWD_OCC
-#define GSTEX_FWD_OCC (GSTEX_FWD_PREFETCH ? 5 : 6)  // forward waves per SIMD the register allocation targets (measured:
+#define GSTEX_FWD_OCC ((GSTEX_FWD_PREFETCH || GSTEX_FWD_DEFER2) ? 5 : 6)  // forward waves per SIMD the register allocation targets (measured:
                                                    // 8 at 64 VGPRs is slower)
 #endif
 #ifndef GSTEX_XCD_MB
@@ -733,20 +736,40 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     // is applied once, by tex_value(): sum_k w_k (s m_k + b) = s sum_k w_k m_k + b sum_k w_k (9 + 4 C VALU per visit
     // instead of 8 C; no decision depends on a texel value)
     float texw = 0.0f;
-    auto fold_pending = [&]() {
-        if (kDefer && pend != 0.0f) {
-            const float c1 = pw * pax, c0 = pw * (1.0f - pax), qy = 1.0f - pay;
-            const float w00 = c0 * qy, w01 = c0 * pay, w10 = c1 * qy, w11 = c1 * pay;
+    auto fold_set = [&](float (&a00)[CM], float (&a01)[CM], float (&a10)[CM], float (&a11)[CM], float ax, float ay,
+                        float aw, float& apend) {
+        if (kDefer && apend != 0.0f) {
+            const float c1 = aw * ax, c0 = aw * (1.0f - ax), qy = 1.0f - ay;
+            const float w00 = c0 * qy, w01 = c0 * ay, w10 = c1 * qy, w11 = c1 * ay;
 #pragma unroll
             for (int c = 0; c < CM; ++c) {
                 if (c < Cn)
-                    tex[c] = __builtin_fmaf(p11[c], w11, __builtin_fmaf(p10[c], w10, __builtin_fmaf(p01[c], w01,
-                             __builtin_fmaf(p00[c], w00, tex[c]))));
+                    tex[c] = __builtin_fmaf(a11[c], w11, __builtin_fmaf(a10[c], w10, __builtin_fmaf(a01[c], w01,
+                             __builtin_fmaf(a00[c], w00, tex[c]))));
             }
-            texw = texw + pw;
-            pend = 0.0f;
+            texw = texw + aw;
+            apend = 0.0f;
         }
     };
+#if GSTEX_FWD_DEFER2
+    // two pending sets (experiment): the gathers of wave visit v land in set v & 1 and are folded at visit v + 2 (every
+    // lane holding one, contributing or not), i.e. still in visit order; `par` = the parity of the next visit, whose set
+    // holds the older pending gathers
+    float qpend = 0.0f;
+    float q00[CM], q01[CM], q10[CM], q11[CM], qax = 0.f, qay = 0.f, qw = 0.f;
+    int par = 0;
+    auto fold_pending = [&]() {  // both sets, older first
+        if (par) {
+            fold_set(q00, q01, q10, q11, qax, qay, qw, qpend);
+            fold_set(p00, p01, p10, p11, pax, pay, pw, pend);
+        } else {
+            fold_set(p00, p01, p10, p11, pax, pay, pw, pend);
+            fold_set(q00, q01, q10, q11, qax, qay, qw, qpend);
+        }
+    };
+#else
+    auto fold_pending = [&]() { fold_set(p00, p01, p10, p11, pax, pay, pw, pend); };
+#endif
     auto tex_value = [&](int c) {  // the texture output of channel c so far
         return kDefer ? __builtin_fmaf(tex[c], tex_scale, tex_bias * texw) : tex[c];
     };
@@ -851,6 +874,11 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             GSTEX_STAT(11, __ballot(ok) ? 1 : 0);                 // ... with a contributing lane
             GSTEX_STAT(12, __popcll(__ballot(ok && !stop)));      // contributing lanes
             alive = stop ? 0.0f : alive;
+#if GSTEX_FWD_DEFER2
+            // this visit's set: its gathers of two visits ago are folded first (all lanes holding one)
+            if (par) fold_set(q00, q01, q10, q11, qax, qay, qw, qpend);
+            else fold_set(p00, p01, p10, p11, pax, pay, pw, pend);
+#endif
 #if GSTEX_FWD_HOIST
             // the contributing branch's record fields (planes 3-7) consumed here, ahead of the branch, so their LDS
             // reads issue with the evaluation's and their latency hides behind it instead of opening the branch
@@ -871,6 +899,20 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
                     const Bilerp b = bilerp_xy(tu, tv, bh, bw, r.hm1, r.wm1);
+#if GSTEX_FWD_DEFER2
+                    if constexpr (CM != 3) {
+                        fold_pending();  // (two sets only for C = 3; kDefer is false otherwise)
+                    } else if (has_tex) {
+                        const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
+                        if (par) {
+                            load_texel_quad_unclamped(rs, b, bw, q00, q01, q10, q11);
+                            qax = b.ax; qay = b.ay; qw = w; qpend = 1.0f;
+                        } else {
+                            load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
+                            pax = b.ax; pay = b.ay; pw = w; pend = 1.0f;
+                        }
+                    }
+#else
                     fold_pending();
                     if (has_tex) {
                         const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
@@ -890,6 +932,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                         pw = w;
                         pend = 1.0f;
                     }
+#endif
                 } else if (has_tex) {
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
@@ -920,6 +963,9 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                 T = test_T;
                 last = b0 - rng.x + j;
             }
+#if GSTEX_FWD_DEFER2
+            par ^= 1;
+#endif
             if (__builtin_amdgcn_ballot_w64(alive != 0.0f) == 0) {
                 all_done = true;
                 break;

@@ -24,6 +24,7 @@ parameter tensors needs capture() again.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -31,8 +32,11 @@ from . import _lib, ops
 from .optim import AdamSchedule, FusedAdam
 
 
+_UPLOAD = os.environ.get("GSTEX_GRAPH_UPLOAD", "current")  # hipGraphUpload after instantiation: none | capture | current
+
+
 class _Slot:
-    __slots__ = ("graph", "exec_ptr", "timing", "current", "pending", "capacity")
+    __slots__ = ("graph", "exec_ptr", "timing", "current", "pending", "capacity", "updated")
 
 
 class StepGraphs:
@@ -115,13 +119,20 @@ class StepGraphs:
                     self.schedule.counter.add_(1)  # the next replay reads the next table row
                 timing = ops._CAPTURE_TIMING
                 ops._CAPTURE_TIMED = ops._CAPTURE_TIMING = None
-                if len(self.schedule.updates) != n_params or set(self.schedule.updates.values()) != {1}:
-                    raise RuntimeError("StepGraphs: the captured step must update every parameter exactly once "
+                if not self.schedule.updates or set(self.schedule.updates.values()) != {1}:
+                    raise RuntimeError("StepGraphs: the captured step must update each parameter at most once "
                                        f"(got {sorted(self.schedule.updates.values())} over {n_params} parameters)")
+                updated = set(self.schedule.updates)  # (parameters without a gradient, e.g. features_dc, are not)
+                if self.slots and updated != self.slots[0].updated:
+                    raise RuntimeError("StepGraphs: the slots' steps update different parameters")
                 if pool is None:
                     pool = g.pool()  # one memory pool for all slots (replayed one at a time on one stream)
                 g.instantiate()
-                _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(), stream.cuda_stream)
+                if _UPLOAD == "capture":
+                    _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(), stream.cuda_stream)
+                elif _UPLOAD == "current":  # the stream the replays will run on
+                    _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(),
+                              torch.cuda.current_stream(dev).cuda_stream)
                 s = _Slot()
                 s.graph, s.exec_ptr = g, g.raw_cuda_graph_exec()
                 s.timing = []
@@ -133,6 +144,7 @@ class StepGraphs:
                 s.current = None  # the timing events the nodes record into now (None: the capture's own pair)
                 s.pending = tr._pending_tex  # the step's deferred texel update, run eagerly if no replay follows
                 s.capacity = tr.pairs.capacity
+                s.updated = updated
                 self.slots.append(s)
         finally:
             tr.optimizer.schedule = None
@@ -179,9 +191,8 @@ class StepGraphs:
         self.replays += 1
         tr._pending_tex, tr._pending_collective, tr._sink_fresh = s.pending, False, True
         for p in self._params():
-            st = opt.state.get(p)
-            if st is not None and "step" in st:
-                st["step"] += 1
+            if id(p) in s.updated:
+                opt.state[p]["step"] += 1
         self._unpolled.append((k, tr.step))
         tr.step += 1
         self._expected_step = tr.step

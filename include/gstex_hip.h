@@ -169,8 +169,9 @@ int gstex_stream_wait_event(void* stream, void* event);
 int gstex_event_destroy(void* event);
 /* HIP-graph support (ABI 16; not in the reference, which has no graph capture).  A training step captured into a
  * hipGraph (gstex_amd.graphs.StepGraphs) times its raster kernels with event-record nodes:
- *   gstex_event_record_external: hipEventRecordWithFlags(hipEventRecordExternal) -- on a capturing stream it adds an
- *     event-record node to the graph (a plain record there only orders the capture);
+ *   gstex_event_record_external: on a capturing stream, an event-record node appended to the graph after the
+ *     capture's current dependencies (what hipEventRecordExternal specifies; a plain record there only orders the
+ *     capture); on any other stream a plain record;
  *   gstex_graph_event_nodes: nodes[i] = the event-record node of `graph` (a hipGraph_t) recording events[i]; an event no
  *     node records is an error;
  *   gstex_graph_exec_set_event: point that node of the instantiated graph `exec` (a hipGraphExec_t) at another event

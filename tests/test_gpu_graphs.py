@@ -47,7 +47,10 @@ def _assert_same(a, b):
     for (name, pa), pb in zip(a.param_groups().items(), b.parameters()):
         pa = pa[0]
         assert torch.equal(pa, pb), f"{name}: parameters differ (max {float((pa - pb).abs().max()):.3e})"
-        sa, sb = a.optimizer.state[pa], b.optimizer.state[pb]
+        sa, sb = a.optimizer.state.get(pa, {}), b.optimizer.state.get(pb, {})
+        assert sa.keys() == sb.keys(), name
+        if not sa:  # never updated (no gradient: features_dc)
+            continue
         assert sa["step"] == sb["step"], f"{name}: Adam step {sa['step']} vs {sb['step']}"
         if name == "texture_dc":  # float-atomic gradients: the moments agree within their noise
             for key in ("exp_avg", "exp_avg_sq"):
