@@ -277,17 +277,20 @@ __host__ __device__ __forceinline__ int fwd_group_of(int t, int tiles_x) {
 __global__ __launch_bounds__(256) void fwd_group_order_kernel(int n_tiles, int tiles_x,
                                                               const int2* __restrict__ tile_ranges,
                                                               int32_t* __restrict__ order) {
+    // (experiment only: every tile's count and group staged in LDS, n_tiles <= 4096)
+    __shared__ int s_cnt[4096];
+    for (int u = threadIdx.x; u < n_tiles && u < 4096; u += 256) {
+        const int2 ru = tile_ranges[u];
+        s_cnt[u] = ((ru.y - ru.x) << 3) | fwd_group_of(u, tiles_x);
+    }
+    __syncthreads();
     const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= n_tiles) return;
-    const int g = fwd_group_of(t, tiles_x);
-    const int2 rt = tile_ranges[t];
-    const int c = rt.y - rt.x;
+    if (t >= n_tiles || n_tiles > 4096) return;
+    const int g = s_cnt[t] & 7, c = s_cnt[t] >> 3;
     int r = 0;
     for (int u = 0; u < n_tiles; ++u) {
-        if (fwd_group_of(u, tiles_x) != g) continue;
-        const int2 ru = tile_ranges[u];
-        const int cu = ru.y - ru.x;
-        r += (cu > c || (cu == c && u < t)) ? 1 : 0;
+        const int k = s_cnt[u];
+        r += ((k & 7) == g && ((k >> 3) > c || ((k >> 3) == c && u < t))) ? 1 : 0;
     }
     order[8 * r + g] = t;
 }

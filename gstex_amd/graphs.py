@@ -47,17 +47,23 @@ class StepGraphs:
 
     def __init__(self, trainer, step_fn, n_slots: int, timed=(), rows: int = 8192):
         self.tr = trainer
+        # one pair-capacity flag slot for every step (gstex_amd.model: step k's flag is read by its head update and, at
+        # the top of step k + 1, by its deferred texel update, before step k + 1's scan overwrites it): a captured
+        # step then reads the flag of whichever step (eager or replayed) ran before it
+        trainer.single_flag = True
         self.step_fn = step_fn
         self.n = int(n_slots)
         self.timed = set(timed)
         self.rows = int(rows)
-        self.slots: list[_Slot] = []
+        self.slots: list = [None] * self.n
         self.schedule = None
+        self._pool = None
+        self._stream = None
         self.replays = 0
         self._row0 = 0  # replays taken off the schedule's counter by AdamSchedule.shift
         self._polls = []  # (event, [(slot, trainer step), ...]) of replays whose pair totals have not been read
         self._unpolled = []  # replays since the last poll event
-        self._expected_step = None  # trainer.step after the last capture / replay (an eager step in between: stale)
+        self._expected_step = None  # trainer.step after the last capture / replay (eager steps since: catch_up)
         self.stale = False
         self._host_words = self._dev_words = None
 
@@ -82,7 +88,7 @@ class StepGraphs:
                 opt.state[p]["step"] = s["steps"][id(p)]
 
     # ------------------------------------------------------------------ capture
-    def capture(self):
+    def _check(self):
         tr = self.tr
         if not (isinstance(tr.optimizer, FusedAdam) and tr.defer_texture and tr.pairs is not None):
             raise RuntimeError("StepGraphs: needs a read-back-free trainer (fused Adam, defer_texture, pair_capacity)")
@@ -90,70 +96,92 @@ class StepGraphs:
             raise RuntimeError("StepGraphs: single-GPU steps only (a GradSync step has collectives)")
         if tr.pairs.capacity <= 0:
             raise RuntimeError("StepGraphs: run one eager step first (it sizes the pair capacity)")
-        dev = tr.device
+
+    def _reset(self):
+        """Drop every slot and start a new schedule (after a device synchronisation: replays of the old graphs may be
+        in flight, and their memory pool goes with them)."""
+        dev = self.tr.device
         torch.cuda.synchronize(dev)
         self._poll_all()
-        self.slots = []
+        self.slots = [None] * self.n
+        self._pool = None
         if self._host_words is None:
             h, d = ctypes.c_void_p(), ctypes.c_void_p()
             _lib.call("gstex_host_words_alloc", self.n, ctypes.byref(h), ctypes.byref(d))
             self._host_words, self._dev_words = h.value, d.value
             self._words = (ctypes.c_int32 * self.n).from_address(self._host_words)
-        self.schedule = AdamSchedule(tr.optimizer, dev, self.rows)
+        self.schedule = AdamSchedule(self.tr.optimizer, dev, self.rows)
         self.replays, self._row0 = 0, 0
+        self.stale = False
+        self._expected_step = self.tr.step
+
+    def capture(self, slots=None):
+        """Capture the steps of `slots` (default: every slot; replay() captures a missing slot itself, at its first
+        replay).  Each capture synchronises the device (torch.cuda.graph), which then idles for the few ms of the
+        capture: its clock takes several steps to ramp back up, so capture early (bench.py: after the first warmup
+        step)."""
+        self._check()
+        self.catch_up()
+        if self.schedule is None or self.stale:
+            self._reset()
+        for k in (range(self.n) if slots is None else slots):
+            if self.slots[k] is None:
+                self._capture_slot(k)
+
+    def _capture_slot(self, k: int):
+        tr = self.tr
+        dev = tr.device
         snap = self._snapshot()
         n_params = len(self._params())
-        stream = torch.cuda.Stream(dev)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(dev)
+        stream = self._stream
         stream.wait_stream(torch.cuda.current_stream(dev))
-        pool = None
         tr.optimizer.schedule = self.schedule
+        # the device counter reads replays - row0 when this slot's first replay runs
+        self.schedule.capture_offset = self.replays - self._row0
         try:
-            for k in range(self.n):
-                self._restore(snap)
-                tr.pairs.graph_word = self._dev_words + 4 * k
-                ops._CAPTURE_TIMED, ops._CAPTURE_TIMING = set(self.timed), []
-                self.schedule.reset_updates()
-                g = torch.cuda.CUDAGraph(keep_graph=True)
-                with torch.cuda.graph(g, pool=pool, stream=stream):
-                    self.step_fn(k)
-                    self.schedule.counter.add_(1)  # the next replay reads the next table row
-                timing = ops._CAPTURE_TIMING
-                ops._CAPTURE_TIMED = ops._CAPTURE_TIMING = None
-                if not self.schedule.updates or set(self.schedule.updates.values()) != {1}:
-                    raise RuntimeError("StepGraphs: the captured step must update each parameter at most once "
-                                       f"(got {sorted(self.schedule.updates.values())} over {n_params} parameters)")
-                updated = set(self.schedule.updates)  # (parameters without a gradient, e.g. features_dc, are not)
-                if self.slots and updated != self.slots[0].updated:
-                    raise RuntimeError("StepGraphs: the slots' steps update different parameters")
-                if pool is None:
-                    pool = g.pool()  # one memory pool for all slots (replayed one at a time on one stream)
-                g.instantiate()
-                if _UPLOAD == "capture":
-                    _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(), stream.cuda_stream)
-                elif _UPLOAD == "current":  # the stream the replays will run on
-                    _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(),
-                              torch.cuda.current_stream(dev).cuda_stream)
-                s = _Slot()
-                s.graph, s.exec_ptr = g, g.raw_cuda_graph_exec()
-                s.timing = []
-                for key, a, b in timing:
-                    evs = (ctypes.c_void_p * 2)(a.handle, b.handle)
-                    nodes = (ctypes.c_void_p * 2)()
-                    _lib.call("gstex_graph_event_nodes", g.raw_cuda_graph(), evs, 2, nodes)
-                    s.timing.append((key, a, b, nodes[0], nodes[1]))
-                s.current = None  # the timing events the nodes record into now (None: the capture's own pair)
-                s.pending = tr._pending_tex  # the step's deferred texel update, run eagerly if no replay follows
-                s.capacity = tr.pairs.capacity
-                s.updated = updated
-                self.slots.append(s)
+            tr.pairs.graph_word = self._dev_words + 4 * k
+            ops._CAPTURE_TIMED, ops._CAPTURE_TIMING = set(self.timed), []
+            self.schedule.reset_updates()
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            # (torch.cuda.graph: the device synchronised and the caches emptied first; one pool for all slots, which
+            # are replayed one at a time on one stream)
+            with torch.cuda.graph(g, pool=self._pool, stream=stream):
+                self.step_fn(k)
+                self.schedule.counter.add_(1)  # the next replay reads the next table row
+            timing = ops._CAPTURE_TIMING
+            ops._CAPTURE_TIMED = ops._CAPTURE_TIMING = None
+            if not self.schedule.updates or set(self.schedule.updates.values()) != {1}:
+                raise RuntimeError("StepGraphs: the captured step must update each parameter at most once "
+                                   f"(got {sorted(self.schedule.updates.values())} over {n_params} parameters)")
+            updated = set(self.schedule.updates)  # (parameters without a gradient, e.g. features_dc, are not)
+            if self._pool is None:
+                self._pool = g.pool()
+            g.instantiate()
+            if _UPLOAD == "capture":
+                _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(), stream.cuda_stream)
+            elif _UPLOAD == "current":  # the stream the replays will run on
+                _lib.call("gstex_graph_upload", g.raw_cuda_graph_exec(), torch.cuda.current_stream(dev).cuda_stream)
+            s = _Slot()
+            s.graph, s.exec_ptr = g, g.raw_cuda_graph_exec()
+            s.timing = []
+            for key, a, b in timing:
+                evs = (ctypes.c_void_p * 2)(a.handle, b.handle)
+                nodes = (ctypes.c_void_p * 2)()
+                _lib.call("gstex_graph_event_nodes", g.raw_cuda_graph(), evs, 2, nodes)
+                s.timing.append((key, a, b, nodes[0], nodes[1]))
+            s.current = None  # the timing events the nodes record into now (None: the capture's own pair)
+            s.pending = tr._pending_tex  # the step's deferred texel update, run eagerly if no replay follows
+            s.capacity = tr.pairs.capacity
+            s.updated = updated
+            self.slots[k] = s
         finally:
             tr.optimizer.schedule = None
             tr.pairs.graph_word = None
             ops._CAPTURE_TIMED = ops._CAPTURE_TIMING = None
             self._restore(snap)
         torch.cuda.current_stream(dev).wait_stream(stream)
-        self.stale = False
-        self._expected_step = tr.step
 
     # ------------------------------------------------------------------ replay
     def _point_timing(self, s: _Slot):
@@ -176,13 +204,12 @@ class StepGraphs:
 
     def replay(self, k: int):
         """Slot k's step, one hipGraphLaunch on the current stream; host state advanced as the eager step's."""
-        if self._expected_step is not None and self.tr.step != self._expected_step:
-            self.stale = True  # an eager step ran since: the tables' rows no longer match the replay count
-        if self.stale or not self.slots:
-            self.capture()
+        self.catch_up()
+        if self.stale or self.schedule is None or self.slots[k] is None:
+            self.capture([k])
         tr, opt = self.tr, self.tr.optimizer
         s = self.slots[k]
-        if self.replays - self._row0 >= self.rows - 1:  # slide the bias-correction tables before their rows run out
+        while self.replays - self._row0 >= self.rows - 1:  # slide the bias-correction tables before the rows run out
             n = self.rows // 2
             self.schedule.shift(n)
             self._row0 += n
@@ -202,6 +229,23 @@ class StepGraphs:
             self._polls.append((ev, self._unpolled))
             self._unpolled = []
         self.poll()
+
+    def catch_up(self):
+        """Account for eager steps run since the last capture / replay: the bias-correction row counter advances by
+        their number (one tiny launch on the current stream, so a caller can issue it ahead of a timed replay) --
+        eager steps and replays may then be mixed freely.  A grown pair capacity marks the graphs stale."""
+        if self.schedule is None or self.stale:
+            return
+        d = self.tr.step - self._expected_step
+        if d < 0:
+            self.stale = True
+            return
+        if d:
+            self.schedule.counter.add_(d)
+            self.replays += d
+            self._expected_step = self.tr.step
+        if any(sl is not None and self.tr.pairs.capacity > sl.capacity for sl in self.slots):
+            self.stale = True
 
     # ------------------------------------------------------------------ pair totals
     def _absorb(self, k: int, step: int):
@@ -234,12 +278,17 @@ class StepGraphs:
             self._absorb(k, step)
         self._polls, self._unpolled = [], []
 
+    @property
+    def captured(self) -> int:
+        return sum(s is not None for s in self.slots)
+
     def close(self):
         """Wait for the replays, read their pair totals and drop the graphs (their memory pool is released)."""
-        if self.slots:
+        if self.captured:
             torch.cuda.synchronize(self.tr.device)
             self._poll_all()
-        self.slots = []
+        self.slots = [None] * self.n
+        self.schedule = self._pool = None
         if self._host_words is not None:
             _lib.load().gstex_host_words_free(self._host_words)
             self._host_words = self._dev_words = None

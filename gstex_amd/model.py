@@ -185,6 +185,7 @@ class GStexTrainer:
             pair_capacity = os.environ.get("GSTEX_SYNC_PAIRS", "0") == "0"
         self.pairs = ops.PairCapacity(d) if (pair_capacity and fused_adam and self.device.type == "cuda") else None
         self.step_control = torch.zeros(8, device=d, dtype=torch.float32)
+        self.single_flag = False  # gstex_amd.graphs.StepGraphs: every step uses step_control[0]
         self.skipped_steps = []  # steps whose update the pair-capacity guard skipped (found by _poll_pairs)
         self._tex_grad = None
         if self.defer_texture:
@@ -215,7 +216,7 @@ class GStexTrainer:
         """The current step's guard flag (1-element view of step_control) for its Adam launches, or None."""
         if self.pairs is None:
             return None
-        k = self.step % 8
+        k = 0 if self.single_flag else self.step % 8
         return self.step_control[k:k + 1]
 
     def _poll_pairs(self):

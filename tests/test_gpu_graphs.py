@@ -5,8 +5,8 @@ fixed order); the texel gradients stay float-atomic sums (order varies run to ru
 lr = 0 here: its values then stay fixed and every other group's gradient is reproducible.  A trainer whose steps are
 graph replays must then hold exactly the parameters, Adam moments and step counts of an eager trainer after the same
 steps -- the device-side bias-correction tables (gstex_adam_step_scheduled) included, across two table shifts
-(rows = 16), an eager step between replays (the graphs are re-captured) and a final deferred texel update; the texel
-moments agree within the float-atomic noise."""
+(rows = 16), eager steps between replays (StepGraphs.catch_up advances the row counter) and a final deferred texel
+update; the texel moments agree within the float-atomic noise."""
 import pytest
 import torch
 
@@ -77,11 +77,13 @@ def test_graph_replays_match_eager_steps_bitwise():
             graphs.replay(s % 3)
         assert graphs.replays == 24 and graphs._row0 == 16 and not b.skipped_steps
         _assert_same(a, b)
-        ea(26 % 3)  # an eager step between replays: the graphs are re-captured at the next replay
-        eb(26 % 3)
-        for s in range(27, 31):
+        for s in range(26, 29):  # eager steps between replays: the row counter catches up, no re-capture
+            ea(s % 3)
+            eb(s % 3)
+        for s in range(29, 33):
             ea(s % 3)
             graphs.replay(s % 3)
+        assert graphs.replays == 31 and graphs.captured == 3
         _assert_same(a, b)
         graphs.close()
     finally:

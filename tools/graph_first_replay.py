@@ -4,6 +4,7 @@ synchronisations and timed with events, poses 0..7 three times over.  GSTEX_GRAP
 where hipGraphUpload runs after instantiation."""
 import os
 import sys
+import time
 
 import torch
 
@@ -30,19 +31,29 @@ body(0)
 body(1)
 graphs = StepGraphs(tr, body, 8)
 graphs.capture()
+if os.environ.get("BUSY_FIRST"):  # the device kept busy after the capture before the first replays (clock ramp?)
+    for k in range(6):
+        body(k % 8)
+    graphs.capture()  # (an eager step in between: re-captured; the capture itself idles the device again)
+    x = torch.empty((1 << 28,), device=dev)
+    for _ in range(200):
+        x.mul_(1.0001)  # ~0.3 s of streaming work right before the replays
 rows = []
+same = os.environ.get("ROUND0_SAME")  # round 0 replays pose 0 eight times: a per-graph first-launch cost or a ramp?
 for rnd in range(3):
-    t = []
+    t, h = [], []
     for k in range(8):
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        graphs.replay(k)
+        t0 = time.perf_counter()
+        graphs.replay(0 if (same and rnd == 0) else k)
+        h.append(round(1e3 * (time.perf_counter() - t0), 3))
         b.record()
         torch.cuda.synchronize()
         t.append(round(a.elapsed_time(b), 3))
     rows.append(t)
-    print(f"upload={_UPLOAD} round {rnd}: {t}", flush=True)
+    print(f"upload={_UPLOAD} round {rnd}: {t} host ms {h}", flush=True)
 for k in range(2):
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
