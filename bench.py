@@ -336,18 +336,22 @@ def main():
             torch.cuda.synchronize()
             transient = torch.cuda.max_memory_allocated(dev) - torch.cuda.memory_allocated(dev)
             torch.empty(2 * transient, dtype=torch.uint8, device=dev)
-        # the first step is eager (it sizes the pair capacity); the graphs are captured right after it, early in the
-        # warmup (a capture idles the device for a moment, and the clock takes several steps to ramp back up)
+        # the first step is eager (it sizes the pair capacity); --graph all: every pose's step captured right after
+        # it, early in the warmup (a capture idles the device for a moment and the clock takes several steps to ramp
+        # back up), the rest of the warmup replays them
         step(eager=w < 1 or args.graph == "first")
-        if w == 0 and graphs is not None:
+        if w == 0 and graphs is not None and args.graph == "all":
             try:
-                first_pose = (rank + args.warmup * world) % N_POSES
-                graphs.capture([first_pose] if args.graph == "first" else None)
+                graphs.capture()
             except Exception as ex:  # noqa: BLE001
                 graph_error[0] = repr(ex)[:300]
                 graphs = None
-    if graphs is not None:
-        graphs.catch_up()  # the row counter past the eager warmup steps (a tiny launch, before the timed region)
+    if graphs is not None and args.graph == "first":
+        try:  # the first timed step's pose, captured after the warmup's eager steps
+            graphs.capture([(rank + args.warmup * world) % N_POSES])
+        except Exception as ex:  # noqa: BLE001
+            graph_error[0] = repr(ex)[:300]
+            graphs = None
     # the last warmup step's deferred texel update stays pending: it is the first kernel of the first timed step (as
     # every step starts with the previous step's texel update), and the last timed step's update runs after the timed
     # region -- K steps, K texel updates, and the first timed step starts with ~90 us of device work queued instead of

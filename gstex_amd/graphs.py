@@ -63,7 +63,7 @@ class StepGraphs:
         self._row0 = 0  # replays taken off the schedule's counter by AdamSchedule.shift
         self._polls = []  # (event, [(slot, trainer step), ...]) of replays whose pair totals have not been read
         self._unpolled = []  # replays since the last poll event
-        self._expected_step = None  # trainer.step after the last capture / replay (eager steps since: catch_up)
+        self._expected_step = None  # trainer.step after the last capture / replay (eager steps since: stale)
         self.stale = False
         self._host_words = self._dev_words = None
 
@@ -116,17 +116,18 @@ class StepGraphs:
         self._expected_step = self.tr.step
 
     def capture(self, slots=None):
-        """Capture the steps of `slots` (default: every slot; replay() captures a missing slot itself, at its first
-        replay).  Each capture synchronises the device (torch.cuda.graph), which then idles for the few ms of the
-        capture: its clock takes several steps to ramp back up, so capture early (bench.py: after the first warmup
-        step)."""
+        """Capture the steps of `slots` (default: every slot) back to back, after dropping every graph captured before
+        (a device synchronisation, a fresh memory pool and a fresh schedule).  Captures are never interleaved with
+        replays of graphs that share their pool: that pattern (a slot captured lazily after other slots of the same
+        pool had been replayed) faulted the GPU on a later replay in round 5, while back-to-back captures replay
+        correctly.  The device idles for the few ms of a capture (its clock then takes several steps to ramp back
+        up): capture outside the timed region."""
         self._check()
-        self.catch_up()
-        if self.schedule is None or self.stale:
-            self._reset()
-        for k in (range(self.n) if slots is None else slots):
-            if self.slots[k] is None:
-                self._capture_slot(k)
+        want = sorted(set(range(self.n) if slots is None else slots) |
+                      {k for k, sl in enumerate(self.slots) if sl is not None})
+        self._reset()
+        for k in want:
+            self._capture_slot(k)
 
     def _capture_slot(self, k: int):
         tr = self.tr
@@ -138,8 +139,6 @@ class StepGraphs:
         stream = self._stream
         stream.wait_stream(torch.cuda.current_stream(dev))
         tr.optimizer.schedule = self.schedule
-        # the device counter reads replays - row0 when this slot's first replay runs
-        self.schedule.capture_offset = self.replays - self._row0
         try:
             tr.pairs.graph_word = self._dev_words + 4 * k
             ops._CAPTURE_TIMED, ops._CAPTURE_TIMING = set(self.timed), []
@@ -204,7 +203,8 @@ class StepGraphs:
 
     def replay(self, k: int):
         """Slot k's step, one hipGraphLaunch on the current stream; host state advanced as the eager step's."""
-        self.catch_up()
+        if self._expected_step is not None and self.tr.step != self._expected_step:
+            self.stale = True  # eager steps since the last capture / replay: re-captured (the rows follow the steps)
         if self.stale or self.schedule is None or self.slots[k] is None:
             self.capture([k])
         tr, opt = self.tr, self.tr.optimizer
@@ -229,23 +229,6 @@ class StepGraphs:
             self._polls.append((ev, self._unpolled))
             self._unpolled = []
         self.poll()
-
-    def catch_up(self):
-        """Account for eager steps run since the last capture / replay: the bias-correction row counter advances by
-        their number (one tiny launch on the current stream, so a caller can issue it ahead of a timed replay) --
-        eager steps and replays may then be mixed freely.  A grown pair capacity marks the graphs stale."""
-        if self.schedule is None or self.stale:
-            return
-        d = self.tr.step - self._expected_step
-        if d < 0:
-            self.stale = True
-            return
-        if d:
-            self.schedule.counter.add_(d)
-            self.replays += d
-            self._expected_step = self.tr.step
-        if any(sl is not None and self.tr.pairs.capacity > sl.capacity for sl in self.slots):
-            self.stale = True
 
     # ------------------------------------------------------------------ pair totals
     def _absorb(self, k: int, step: int):

@@ -33,7 +33,6 @@ class AdamSchedule:
         self.counter = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._t0, self._tables, self._groups = {}, {}, {}
         self.updates = {}  # id(param) -> updates registered since reset_updates() (one per parameter per step)
-        self.capture_offset = 0  # the counter's value at the first replay of the step being captured
         for group in optimizer.param_groups:
             for p in group["params"]:
                 t0 = int(optimizer.state[p].get("step", 0)) + 1 if p in optimizer.state else 1
@@ -57,7 +56,7 @@ class AdamSchedule:
         if key not in self._tables:
             raise RuntimeError("AdamSchedule: a parameter added after the schedule was built (re-capture the step)")
         self.updates[key] = self.updates.get(key, 0) + 1
-        return self._tables[key].data_ptr(), t - self._t0[key] - self.capture_offset
+        return self._tables[key].data_ptr(), t - self._t0[key]
 
     def reset_updates(self):
         self.updates = {}
