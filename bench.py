@@ -548,11 +548,7 @@ def main():
                             if graphs is not None
                             else "eager: every launch enqueued by the host each step" +
                             (f" (graph capture failed: {graph_error[0]})" if graph_error[0] else "")),
-            "texture_update": ("side stream: step k's texel Adam update launched on a second stream right after step "
-                               "k's raster backward (workgroups capped at %d, 0 = uncapped), step k+1's raster forward "
-                               "waits for it; the timed region holds exactly K updates" % trainer.texture_grid
-                               if trainer.texture_stream else
-                               "deferred: step k's texel Adam update is the first kernel of step k+1 (same stream, "
+            "texture_update": ("deferred: step k's texel Adam update is the first kernel of step k+1 (same stream, "
                                     "before the raster forward); the timed region holds exactly K texel updates "
                                     "(the last warmup step's and those of timed steps 1..K-1)"
                                if trainer.defer_texture

@@ -107,7 +107,7 @@ class GStexTrainer:
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
                  defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0, use_normal_loss: bool = False,
-                 pair_capacity: bool | None = None, texture_stream: bool | None = None, texture_grid: int | None = None):
+                 pair_capacity: bool | None = None):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -170,19 +170,6 @@ class GStexTrainer:
         # the next step's preprocessing and binning, measured no gain in rounds 2-3: the compute stream's kernels
         # slow down under the streaming update by what the overlap saves; removed in round 5.)
         self.defer_texture = bool(defer_texture) and fused_adam and self.device.type == "cuda"
-        # texture_stream (with defer_texture, single GPU; GSTEX_TEX_STREAM=1): the texel update is launched on a side
-        # stream as soon as the raster backward that produces its gradient is enqueued (the texel-gradient hook), so it
-        # runs beside the rest of the backward (splat-gradient chain, SH / activation backward, the head's Adam) and
-        # the next step's preprocessing and binning -- latency-bound kernels that leave HBM mostly idle -- instead of
-        # between them and the next raster forward, which waits for it (an event).  texture_grid caps its workgroups
-        # (GSTEX_TEX_GRID; 0 = one per 1024 elements), leaving CUs to the compute stream.
-        if texture_stream is None:
-            texture_stream = os.environ.get("GSTEX_TEX_STREAM", "0") == "1"
-        self.texture_stream = bool(texture_stream) and self.defer_texture
-        self.texture_grid = int(os.environ.get("GSTEX_TEX_GRID", "0") if texture_grid is None else texture_grid)
-        self._tex_side = torch.cuda.Stream(d) if self.texture_stream else None
-        self._tex_done = None  # OrderEvent recorded after the side-stream texel update in flight
-        self._tex_launched = None  # trainer step whose texel update the side stream has been given
         self._pending_tex = None
         self._pending_collective = False  # the pending update first waits for a GradSync collective
         # the texel-gradient sink is zeroed by the first differentiable raster forward after an optimizer step
@@ -248,30 +235,8 @@ class GStexTrainer:
             fn()
 
     def wait_texture(self):
-        """Order the current stream after the pending texel update (defer_texture): it is enqueued now (or, with
-        texture_stream, waited for on the device)."""
+        """Order the current stream after the pending texel update (defer_texture): it is enqueued now."""
         self._run_pending_texture()
-        if self._tex_done is not None:
-            self._tex_done.wait(self.device)
-
-    def _launch_texture_side(self):
-        """texture_stream: the texel update of this step on the side stream, after the texel gradient (everything
-        enqueued on the compute stream so far: this is called right after the raster backward's launch)."""
-        if self._tex_launched == self.step:
-            return
-        from ._lib import OrderEvent
-
-        grad_done = OrderEvent()
-        grad_done.record(self.device)
-        side = self._tex_side
-        grad_done.wait(stream=side.cuda_stream)
-        sf = self._skip_flag()
-        with torch.cuda.stream(side):
-            self._step(only={id(self.texture_dc)}, skip_flag=sf, grid=self.texture_grid)
-        done = OrderEvent()
-        done.record(stream=side.cuda_stream)
-        self._tex_done = done
-        self._tex_launched = self.step
 
     def texels(self) -> torch.Tensor:
         """The texel store (SH-DC values) for readers outside the step (export, average_colors, viewers): runs a
@@ -307,8 +272,7 @@ class GStexTrainer:
         the trainer's geometry_outputs)."""
         means = self.means
         deg = self.sh_degree if sh_degree_now is None else sh_degree_now
-        if (self._pending_tex is not None and not self._pending_collective and self.pairs is not None
-                and not self.texture_stream):
+        if self._pending_tex is not None and not self._pending_collective and self.pairs is not None:
             # the deferred texel update first (read-back-free step: there is no pair-count wait to fill): ~90 us of
             # streaming work the device starts on while the host enqueues the step's short preprocessing and binning
             # launches, instead of idling through them after a synchronisation (the bench's first timed step); it only
@@ -351,11 +315,6 @@ class GStexTrainer:
             sink, zero_sink, on_grad = self.texture_grad_route(self._sink_fresh)
         else:
             sink, zero_sink, on_grad = self.texture_grad_sink, self._sink_fresh, self.texture_grad_ready
-        side = self.texture_stream and self.texture_grad_route is None and self.texture_grad_ready is None
-        if side:
-            on_grad = self._launch_texture_side
-            done = self._tex_done  # the raster forward (first reader of the texels) waits for the update in flight
-            late, pend = False, False
         guard = None
         if self.pairs is not None and torch.is_grad_enabled():
             if not torch.cuda.is_current_stream_capturing():  # (a captured step's owner polls between replays)
@@ -368,8 +327,7 @@ class GStexTrainer:
             texture_transform=(SH_C0, 0.5), fold_aabb=True,  # centers come from get_aabb_2d just above
             geometry_outputs=self.geometry_outputs if geometry is None else geometry,
             texture_grad_sink=sink, zero_texture_grad_sink=zero_sink, on_texture_grad=on_grad,
-            texture_ready=(lambda: done.wait(self.device)) if side and done is not None else
-            (self._run_pending_texture if late else None),
+            texture_ready=self._run_pending_texture if late else None,
             before_pair_wait=self._run_pending_texture if pend and not late else None,
             pair_guard=guard)
         if torch.is_grad_enabled():
@@ -476,14 +434,6 @@ class GStexTrainer:
         sync.all_reduce() before this."""
         self._sink_fresh = True  # the next step's first render zeroes the texel-gradient sink
         sf = self._skip_flag()  # this step's pair-capacity guard (None without pair_capacity)
-        if self.defer_texture and self.texture_stream and sync is None and self.texture_grad_ready is None:
-            # the texel update went to the side stream from the backward's hook (launched here if no render of
-            # this step produced a texel gradient); the head's update on the compute stream
-            if self._tex_launched != self.step:
-                self._launch_texture_side()
-            self._step(skip={id(self.texture_dc)}, skip_flag=sf)
-            self.step += 1
-            return
         if self.defer_texture:
             self._run_pending_texture()  # (two steps without a render in between)
             tex = {id(self.texture_dc)}

@@ -411,40 +411,3 @@ def test_two_renders_per_step_under_overlapped_gradsync():
             _assert_trains_alike(name, a[0], b[0], "two renders per step under GradSync")
     finally:
         dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("grid", [0, 128])
-def test_texture_stream_trains_like_the_deferred_step(grid):
-    """texture_stream: the texel update launched on a side stream from the raster backward's texel-gradient hook (the
-    next raster forward waits for it on the device); across an in-place rechart and an eval render it must train like
-    the deferred step on one stream.  grid: the update's capped workgroup count (GSTEX_TEX_GRID)."""
-    from gstex_amd.model import GStexTrainer
-    from gstex_amd.scene import make_scene, sphere_view
-
-    dev = torch.device("cuda", 0)
-    sc = make_scene(4000, 80_000, seed=5)
-    views = [sphere_view(i, 96, 96).to(dev) for i in range(3)]
-    g = torch.Generator().manual_seed(1)
-    gts = [torch.rand((96, 96, 3), generator=g).to(dev) for _ in range(3)]
-    ref = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, texture_stream=False)
-    side = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, texture_stream=True, texture_grid=grid)
-    assert side.texture_stream and not ref.texture_stream
-    for step in range(6):
-        for tr in (ref, side):
-            tr.zero_grad()
-            tr.forward_backward(views[step % 3], gts[step % 3])
-            tr.optimizer_step()
-        assert side._tex_launched == side.step - 1 and side._pending_tex is None
-        if step == 1:
-            for tr in (ref, side):
-                tr.recharge()
-        if step == 3:
-            ev = [tr.eval_render(views[0])["rgb"] for tr in (ref, side)]
-            assert float((ev[0] - ev[1]).abs().max()) < 1e-4
-    for tr in (ref, side):
-        tr.wait_texture()
-    torch.cuda.synchronize()
-    for (name, a), b in zip(ref.param_groups().items(), side.parameters()):
-        _assert_trains_alike(name, a[0], b, "texture_stream step")
-        sa, sb = ref.optimizer.state.get(a[0], {}), side.optimizer.state.get(b, {})
-        assert sa.get("step") == sb.get("step"), name
