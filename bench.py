@@ -357,19 +357,22 @@ def main():
     # region -- K steps, K texel updates, and the first timed step starts with ~90 us of device work queued instead of
     # an idle device waiting for the host's first launches
     carried = trainer._pending_tex is not None  # the first timed step runs the last warmup step's texel update
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    base_mb = torch.cuda.memory_allocated(dev) / 2**20  # parameters, Adam state, scene, views, targets
-    torch.cuda.reset_peak_memory_stats(dev)
     # every event recorded into the stream is a marker packet the device waits on (≈ 4 us each, A/B measured), so the
     # timed loop records only what the line needs: one event per step boundary (K + 1, not 2 K) and, at N = 1, the
-    # dominant kernel's pair (the raster backward); at N > 1 also the forward's, for the exchange's phase record
+    # dominant kernel's pair (the raster backward); at N > 1 also the forward's, for the exchange's phase record.
+    # The host-side preparation (event creation: ~K hipEventCreate calls) happens here, while the device still runs
+    # the warmup's last steps, not after the synchronisation, where the idle device would drop its clock before the
+    # timed region
     ops.set_kernel_timing(not args.no_kernel_timing, names=timed)
     if sync is not None and not args.no_kernel_timing:
         sync.phase_events = {}  # when the head / tail collectives land, on rank 0's compute stream
     bound = [_lib.TimingEvent() for _ in range(args.steps + 1)]  # fence-free timing events (`value` is the wall clock)
     host_s = []  # host time to enqueue each step (the device runs behind it when the step is not host-bound)
+    base_mb = torch.cuda.memory_allocated(dev) / 2**20  # parameters, Adam state, scene, views, targets
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     bound[0].record()
     for k in range(args.steps):
