@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 REC_FLOATS = 32
 BWD_SPLIT = 1 << 29  # GSTEX_BWD_SPLIT: gstex_raster_bwd's split (texel-only pixel-major + splat-parallel) backward
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
@@ -73,6 +73,19 @@ class GstexAdamSchedule(ctypes.Structure):
         ("base", c_int32 * 16),
         ("rows", c_int32 * 16),
     ]
+
+
+class GstexTrainPrologueArgs(ctypes.Structure):
+    """gstex_train_prologue_args (ABI 17): the launches of a training render before its raster forward."""
+    _fields_ = [("n", c_int32), ("sh_degree", c_int32), ("n_rest", c_int32), ("map_cols", c_int32),
+                ("capacity", c_int64), ("cam", GstexCamera), ("guard", GstexPairGuard)] + [
+        (name, c_void_p) for name in (
+            "means", "quats", "log_scales", "opac_logits", "mappings", "campos", "features_rest", "texture_dims",
+            "quats_n", "scales", "opacities", "uv0", "umap", "vmap", "viewdirs", "depths", "centers", "extents",
+            "num_tiles_hit", "rgbs", "offsets", "scan_workspace")] + [("scan_workspace_bytes", c_size_t)] + [
+        (name, c_void_p) for name in (
+            "records", "tile_ranges", "sorted_ids", "sorted_slots", "tile_order", "bin_workspace")] + [
+        ("bin_workspace_bytes", c_size_t)]
 
 
 ADAM_ZERO_GRAD = 1  # GSTEX_ADAM_ZERO_GRAD
@@ -170,6 +183,7 @@ SIGNATURES = {
                                          c_float, _P]),
     "gstex_adam_step_guarded": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32,
                                           c_float, _P, _P]),
+    "gstex_train_prologue": (c_int32, [POINTER(GstexTrainPrologueArgs), _P]),
     "gstex_adam_step_scheduled": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double,
                                             c_int32, c_float, _P, POINTER(GstexAdamSchedule), _P]),
 }

@@ -107,7 +107,7 @@ class GStexTrainer:
                  fused_loss: bool = True, fused_activations: bool = True, geometry_outputs: bool = False,
                  sh_degree_interval: int = 1000, fix_init: bool = False, start_step: int = 0,
                  defer_texture: bool = False, lambda_normal=0.0, lambda_reg=0.0, use_normal_loss: bool = False,
-                 pair_capacity: bool | None = None):
+                 pair_capacity: bool | None = None, fused_step: bool | None = None):
         self.device = torch.device(device)
         d = self.device
         P = lambda t: torch.nn.Parameter(t.detach().to(d).contiguous())  # noqa: E731
@@ -187,6 +187,11 @@ class GStexTrainer:
         self.step_control = torch.zeros(8, device=d, dtype=torch.float32)
         self.single_flag = False  # gstex_amd.graphs.StepGraphs: every step uses step_control[0]
         self.skipped_steps = []  # steps whose update the pair-capacity guard skipped (found by _poll_pairs)
+        # fused_step (not in the reference): the photometric training render as one C prologue call and one autograd
+        # node (gstex_amd.fused) -- the same launches with less host time between them; GSTEX_FUSED_STEP=1 enables it
+        if fused_step is None:
+            fused_step = os.environ.get("GSTEX_FUSED_STEP", "0") != "0"
+        self.fused_step = bool(fused_step)
         self._tex_grad = None
         if self.defer_texture:
             self._own_texture_grad()
@@ -278,6 +283,8 @@ class GStexTrainer:
             # launches, instead of idling through them after a synchronisation (the bench's first timed step); it only
             # has to land before the raster forward, the first reader of the texels
             self._run_pending_texture()
+        if self._fused_ok(composite, geometry):
+            return self._render_fused(view, deg)
         if self.fused_activations:  # one HIP launch each way (gstex_amd.activations)
             quats, scales, opacities, uv0, umap, vmap, viewdirs = activate(
                 means, self.quats, self.scales, self.opacities, self.mappings, view.campos)
@@ -337,6 +344,27 @@ class GStexTrainer:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
                                      0.0, 1.0)
         return out
+
+    def _fused_ok(self, composite: bool, geometry) -> bool:
+        """Whether render() takes gstex_amd.fused's path (see its docstring for why each condition is there)."""
+        return (self.fused_step and not composite and not (self.geometry_outputs if geometry is None else geometry)
+                and self.fused_activations and self.sh_degree > 0 and not self.fix_init
+                and self.pairs is not None and self.pairs.capacity > 0 and self.texture_grad_route is None
+                and self.texture_grad_sink is not None and self.texture_grad_ready is None
+                and self._pending_tex is None and torch.is_grad_enabled()
+                and not torch.are_deterministic_algorithms_enabled()
+                and not torch.cuda.is_current_stream_capturing())
+
+    def _render_fused(self, view: View, deg: int):
+        from . import fused
+
+        self._poll_pairs()
+        img, alpha, tex = fused.train_render(self, view, deg, self.texture_grad_sink, self._sink_fresh)
+        self._sink_fresh = False
+        z = ops._zero_scalar(self.device)  # not rendered: read-only zeros without gradient, as the per-op path
+        H, W = int(view.H), int(view.W)
+        return dict(img=img, tex=tex, depth=z.expand(H, W), reg=z.expand(H, W), alpha=alpha,
+                    normal=z.expand(H, W, 3))
 
     @torch.no_grad()
     def eval_render(self, view: View, edit_texture: torch.Tensor | None = None):

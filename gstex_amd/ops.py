@@ -423,26 +423,39 @@ class PairCapacity:
             call("gstex_scan_offsets_guarded", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), ctypes.byref(guard),
                  _stream(nth))
             return offsets, self.capacity
+        guard, k, cap = self.reserve(step_flag, first, tag, sized=False)
+        offsets = torch.empty((n + 1,), device=nth.device, dtype=torch.int32)
+        ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=nth.device, dtype=torch.uint8)
+        call("gstex_scan_offsets_guarded", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), ctypes.byref(guard),
+             _stream(nth))
+        return offsets, self.commit(k, cap, tag, nth.device)
+
+    def reserve(self, step_flag: torch.Tensor, first: bool, tag=None, sized: bool = True):
+        """The guard of one render's scan and its ring slot -> (GstexPairGuard, slot, capacity of the render).  The
+        caller launches the guarded scan, then commit()s the slot.  sized=True (gstex_amd.fused, which sizes its
+        buffers before the scan) requires the capacity to have been set by an earlier render."""
+        if sized and self.capacity <= 0:
+            raise RuntimeError("PairCapacity.reserve: no capacity yet (the first render sizes it through scan())")
         k = self._k % self.RING
         if self._events[k] is not None:  # the host is RING renders ahead: wait for that one (normally long done)
             self._events[k].synchronize()
             self._absorb(k)
         self._k += 1
-        offsets = torch.empty((n + 1,), device=nth.device, dtype=torch.int32)
-        ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=nth.device, dtype=torch.uint8)
+        cap = (1 << 62) if self.capacity <= 0 else self.capacity
+        return _lib.GstexPairGuard(cap, ptr(step_flag), self._dev_ptr + 4 * k, 1 if first else 0), k, cap
+
+    def commit(self, k: int, cap: int, tag, device) -> int:
+        """Record slot k's event after its scan (on the current stream); the first render reads its total back and
+        sizes the capacity.  -> the capacity."""
         first_use = self.capacity <= 0
-        cap = (1 << 62) if first_use else self.capacity
-        guard = _lib.GstexPairGuard(cap, ptr(step_flag), self._dev_ptr + 4 * k, 1 if first else 0)
-        call("gstex_scan_offsets_guarded", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), ctypes.byref(guard),
-             _stream(nth))
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(nth.device))
+        ev.record(torch.cuda.current_stream(device))
         self._events[k], self._caps[k], self._tags[k] = ev, cap, tag
         if first_use:  # the one read-back: the first render sizes the capacity
             ev.synchronize()
             self._absorb(k)
             self.capacity = max(self.capacity, int(self.headroom * self.last_total) + self.slack)
-        return offsets, self.capacity
+        return self.capacity
 
 
 def bin_capped(nth, offsets, capacity: int, centers, extents, depths, H: int, W: int, block_width: int = BLOCK_WIDTH):

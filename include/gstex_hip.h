@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 16
+#define GSTEX_ABI_VERSION 17
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -409,6 +409,54 @@ typedef struct gstex_adam_schedule {
 int gstex_adam_step_scheduled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                               double eps, int32_t flags, float grad_scale, const float* skip,
                               const gstex_adam_schedule* schedule, void* stream);
+
+/* ---- training-step prologue (ABI 17; not in the reference) ------------------------------------------------------
+ * One host call for the launches a photometric training render makes before its raster forward, in this order:
+ * gstex_activate_fwd, gstex_preprocess (the camera without c2w), gstex_sh_rest_fwd, gstex_scan_offsets_guarded,
+ * gstex_raster_setup (glob_scale 1), gstex_bin_sort_capped -- the same kernels with the same arguments as the
+ * per-op entry points (gstex_amd.fused: the trainer's render without ~0.3 ms of per-launch host overhead, which a
+ * step that starts on an idle device waits for).  All pointers are device pointers; the buffers are sized as the
+ * per-op entry points require (block = 16). */
+typedef struct gstex_train_prologue_args {
+    int32_t n;
+    int32_t sh_degree;
+    int32_t n_rest;
+    int32_t map_cols;
+    int64_t capacity;
+    gstex_camera cam;
+    gstex_pair_guard guard;
+    const float* means;
+    const float* quats;
+    const float* log_scales;
+    const float* opac_logits;
+    const float* mappings;
+    const float* campos;
+    const float* features_rest;
+    const int32_t* texture_dims;
+    float* quats_n;
+    float* scales;
+    float* opacities;
+    float* uv0;
+    float* umap;
+    float* vmap;
+    float* viewdirs;
+    float* depths;
+    float* centers;
+    float* extents;
+    int32_t* num_tiles_hit;
+    float* rgbs;
+    int32_t* offsets;
+    void* scan_workspace;
+    size_t scan_workspace_bytes;
+    float* records;
+    int32_t* tile_ranges;
+    int32_t* sorted_ids;
+    int32_t* sorted_slots;
+    int32_t* tile_order;
+    void* bin_workspace;
+    size_t bin_workspace_bytes;
+} gstex_train_prologue_args;
+int gstex_train_prologue(const gstex_train_prologue_args* args, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,7 @@ def test_every_header_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.gstex_abi_version() == _lib.ABI_VERSION == 16
+    assert lib.gstex_abi_version() == _lib.ABI_VERSION == 17
 
 
 def test_workspace_size_queries(lib):
@@ -162,3 +162,33 @@ def test_activate_and_sh_rest_reject_bad_args(lib):
     assert rc == 1 and "coefficients" in msg
     assert lib.gstex_activate_fwd(0, None, None, None, None, None, 2, None, None, None, None, None, None, None, None,
                                   None) == 0
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors in gstex_amd/_lib.py have the header's sizes and field offsets (gcc on the header)."""
+    import subprocess
+
+    structs = {"gstex_camera": _lib.GstexCamera, "gstex_pair_guard": _lib.GstexPairGuard,
+               "gstex_adam_tensor": _lib.GstexAdamTensor, "gstex_adam_schedule": _lib.GstexAdamSchedule,
+               "gstex_train_prologue_args": _lib.GstexTrainPrologueArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gstex_hip.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f in cls._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                        text=True).stdout.splitlines())
+    for cname, cls in structs.items():
+        assert int(got[f"{cname} size"]) == ctypes.sizeof(cls), cname
+        for f in cls._fields_:
+            assert int(got[f"{cname} {f[0]}"]) == getattr(cls, f[0]).offset, f"{cname}.{f[0]}"
+
+
+def test_train_prologue_rejects_null_args(lib):
+    rc, msg = _status(lib, "gstex_train_prologue", None, None)
+    assert rc != 0 and "null" in msg

@@ -1,0 +1,91 @@
+"""GStexTrainer(fused_step=True) (gstex_amd.fused: the photometric training render as one C prologue call and one
+autograd node) against the per-op path on the GPU: the same launches with the same arguments, so the rendered image,
+the loss and the forward's outputs are bit-identical, and the gradients agree up to the order of their float-atomic
+sums; a few training steps of each path train alike."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(n=4000, texels=80_000, res=96):
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    sc = make_scene(n, texels, seed=5)
+    views = [sphere_view(i, res, res).to(dev) for i in range(3)]
+    g = torch.Generator().manual_seed(2)
+    gts = [torch.rand((res, res, 3), generator=g).to(dev) for _ in range(3)]
+    return dev, sc, views, gts
+
+
+def _count_fused(monkeypatch):
+    from gstex_amd import fused
+
+    calls = [0]
+    inner = fused.train_render
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return inner(*a, **k)
+    monkeypatch.setattr(fused, "train_render", counted)
+    return calls
+
+
+def test_fused_render_matches_per_op(monkeypatch):
+    from gstex_amd.model import GStexTrainer
+
+    calls = _count_fused(monkeypatch)
+    dev, sc, views, gts = _setup()
+    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=True)
+    # the first render sizes the pair capacity (one read-back) through the per-op path
+    tr.zero_grad()
+    tr.forward_backward(views[0], gts[0])
+    tr.optimizer_step()
+    assert calls[0] == 0 and tr.pairs.capacity > 0
+    tr.wait_texture()
+    for k in range(3):
+        res = {}
+        for mode in (True, False):
+            tr.fused_step = mode
+            tr.zero_grad()
+            out = tr.forward_backward(views[k], gts[k])
+            torch.cuda.synchronize()
+            res[mode] = (out.loss.clone(), out.rgb.clone(),
+                         {name: ps[0].grad.detach().clone() for name, ps in tr.param_groups().items()
+                          if ps[0].grad is not None})
+        assert calls[0] == k + 1
+        (lf, rf, gf), (lp, rp, gp) = res[True], res[False]
+        assert torch.equal(rf, rp), "fused render differs from the per-op render"
+        assert torch.equal(lf, lp)
+        assert gf.keys() == gp.keys() and "texture_dc" in gf and "xyz" in gf
+        for name in gf:
+            a, b = gf[name].double(), gp[name].double()
+            scale = max(float(b.abs().max()), 1e-30)
+            err = float((a - b).abs().max()) / scale
+            assert err < 1e-4, f"{name}: fused gradient differs (max rel {err:.2e})"
+            assert float((a - b).abs().mean()) / scale < 1e-7, name
+    tr.fused_step = True
+
+
+def test_fused_step_trains_like_per_op(monkeypatch):
+    from gstex_amd.model import LRS, GStexTrainer
+
+    calls = _count_fused(monkeypatch)
+    dev, sc, views, gts = _setup()
+    a = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=False)
+    b = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=True)
+    for step in range(6):
+        for tr in (a, b):
+            tr.zero_grad()
+            tr.forward_backward(views[step % 3], gts[step % 3])
+            tr.optimizer_step()
+    assert calls[0] == 5  # every step after the capacity-sizing first one
+    assert a.skipped_steps == b.skipped_steps == []
+    for (name, pa), pb in zip(a.param_groups().items(), b.param_groups().values()):
+        x, y = pa[0].detach().double(), pb[0].detach().double()
+        if name == "texture_dc":
+            x, y = a.texels().double(), b.texels().double()
+        scale = max(float(x.abs().max()), 1e-30)
+        d = (x - y).abs()
+        assert float(d.max()) <= LRS[name] and float(d.mean()) / scale < 1e-6, name
