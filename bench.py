@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_TAG = "r05e"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+PROFILE_TAG = "r05g"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
 N_POSES = 8
 
 
@@ -550,6 +550,8 @@ def main():
                              "every step a hipGraph replay of its pose's captured step (gstex_amd.graphs.StepGraphs)")
                             if graphs is not None
                             else "eager: every launch enqueued by the host each step" +
+                            ("; the render's launches before the raster forward as one C call and the render as one "
+                             "autograd node (gstex_amd.fused)" if trainer.fused_step else "") +
                             (f" (graph capture failed: {graph_error[0]})" if graph_error[0] else "")),
             "texture_update": ("deferred: step k's texel Adam update is the first kernel of step k+1 (same stream, "
                                     "before the raster forward); the timed region holds exactly K texel updates "

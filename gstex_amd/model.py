@@ -188,9 +188,10 @@ class GStexTrainer:
         self.single_flag = False  # gstex_amd.graphs.StepGraphs: every step uses step_control[0]
         self.skipped_steps = []  # steps whose update the pair-capacity guard skipped (found by _poll_pairs)
         # fused_step (not in the reference): the photometric training render as one C prologue call and one autograd
-        # node (gstex_amd.fused) -- the same launches with less host time between them; GSTEX_FUSED_STEP=1 enables it
+        # node (gstex_amd.fused) -- the same launches with ~0.23 ms less host time before the raster forward (the
+        # device idles through that after a synchronisation); GSTEX_FUSED_STEP=0 restores the per-op render
         if fused_step is None:
-            fused_step = os.environ.get("GSTEX_FUSED_STEP", "0") != "0"
+            fused_step = os.environ.get("GSTEX_FUSED_STEP", "1") != "0"
         self.fused_step = bool(fused_step)
         self._tex_grad = None
         if self.defer_texture:
