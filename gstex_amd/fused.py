@@ -66,12 +66,12 @@ def _layout(n: int, n_rest: int, capacity: int, H: int, W: int, C: int):
     return hit
 
 
-def _view(arena: torch.Tensor, off: int, shape, dtype=torch.float32) -> torch.Tensor:
-    nb = 1
+def _view(arena: torch.Tensor, off: int, shape) -> torch.Tensor:
+    """fp32 view of arena bytes [off, off + 4 * prod(shape))."""
+    nb = 4
     for s in shape:
         nb *= s
-    item = torch.empty((), dtype=dtype).element_size()
-    return arena[off:off + nb * item].view(dtype).view(shape)
+    return arena[off:off + nb].view(torch.float32).view(shape)
 
 
 class _TrainRender(torch.autograd.Function):

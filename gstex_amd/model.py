@@ -162,7 +162,7 @@ class GStexTrainer:
         self.texture_grad_route = None  # GradSync: the per-render texel-gradient target (several renders per step)
         self.test_colors = None  # eval-render test colours (gstex.py:309)
         # defer_texture (not in the reference; fused Adam on a HIP device): the texel parameter's Adam update of step k
-        # (73 % of the parameters at cfg3) runs inside step k+1's render, before the raster forward, the first reader of
+        # (73 % of the parameters at cfg3) runs at step k+1's zero_grad() or render, before the raster forward, the first reader of
         # the texels -- at the pair-count read-back when there is one (the device runs it while the host waits), else
         # right before the raster forward.  Same updates in the same order on the same stream; the gradient is a
         # persistent buffer the raster forward zeroes (no per-step fill).  Readers of texture_dc outside the step go
@@ -504,7 +504,12 @@ class GStexTrainer:
         """Optimizers.zero_grad_all (engine/optimizers.py): torch's default set_to_none=True, so backward
         writes fresh gradients instead of accumulating into zero-filled ones.  Keep set_to_none=False
         when .grad tensors are views of a flat buffer (gstex_amd.dist.GradSync zeroes that instead).  With
-        defer_texture the texel gradient buffer is kept (the raster forward zeroes it)."""
+        defer_texture the texel gradient buffer is kept (the raster forward zeroes it), and the previous step's deferred
+        texel update is enqueued here, first: it reads that buffer (which set_to_none=False would otherwise zero under
+        it), and a step that starts on an idle device -- after a synchronisation -- gets its first long kernel without
+        waiting for the host to reach the render (the launch order on the stream is the same as from render())."""
+        if self._pending_tex is not None and not self._pending_collective:
+            self._run_pending_texture()
         self.reset_texture_grad()
         if self.defer_texture:
             keep = self.texture_dc.grad

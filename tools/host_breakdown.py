@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host time of the eager cfg3 train step by function (GPU box): the functions on the path to the raster forward are
 wrapped with perf_counter accumulators, 30 steps after 10 warm ones, each step started after a synchronisation (the
-bench's first timed step); prints mean us per step, inclusive, in call order, and the time to the raster forward."""
+bench's first timed step); prints the host time at which each C entry point is first called in the step, and mean us
+per step, inclusive, of the wrapped functions in call order."""
 import collections
 import os
 import sys
@@ -11,7 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from gstex_amd import _lib, activations, loss, model, ops  # noqa: E402
+from gstex_amd import _lib, activations, fused, loss, model, ops  # noqa: E402
 from gstex_amd.model import GStexTrainer  # noqa: E402
 from gstex_amd.scene import make_scene, sphere_view  # noqa: E402
 
@@ -58,7 +59,9 @@ def step():
 for _ in range(10):
     step()
 torch.cuda.synchronize()
+wrap(tr, "zero_grad", "trainer.zero_grad")
 wrap(tr, "render", "trainer.render")
+wrap(fused, "train_render", "fused.train_render")
 wrap(tr, "_run_pending_texture", "trainer._run_pending_texture")
 wrap(tr, "_poll_pairs", "trainer._poll_pairs")
 wrap(tr.pairs, "scan", "PairCapacity.scan")
@@ -68,29 +71,34 @@ wrap(ops, "preprocess")
 wrap(ops, "bin_capped")
 wrap(ops, "texture_gaussians")
 wrap(ops, "_launch")
-wrap(_lib, "call", "_lib.call")
-wrap(ops, "call", "ops.call")
 wrap(activations, "call", "activations.call")
 wrap(loss, "call", "loss.call")
 first_fwd = []
-inner = ops.call
+first_call = collections.defaultdict(list)  # C entry point -> host time of its first call in the step
+inner_ops, inner_lib = ops.call, _lib.call
 
 
 n = 30
 for _ in range(n):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    seen = [None]
+    seen = {}
 
-    def marker(name, *a):
-        if name.startswith("gstex_raster_fwd") and seen[0] is None:
-            seen[0] = time.perf_counter() - t0
-        return inner(name, *a)
-    ops.call = marker
+    def marker(inner):
+        def m(name, *a):
+            seen.setdefault(name, time.perf_counter() - t0)
+            return inner(name, *a)
+        return m
+    ops.call, _lib.call = marker(inner_ops), marker(inner_lib)
     step()
-    ops.call = inner
-    first_fwd.append(seen[0])
+    ops.call, _lib.call = inner_ops, inner_lib
+    for name, t in seen.items():
+        first_call[name].append(t)
 torch.cuda.synchronize()
-print(f"host time to the raster forward launch: median {1e6 * sorted(first_fwd)[n // 2]:.0f} us")
+fwd = [v for k, v in first_call.items() if k.startswith("gstex_raster_fwd")][0]
+print(f"host time to the raster forward launch: median {1e6 * sorted(fwd)[n // 2]:.0f} us")
+print("first call of each entry point in the step (median us after the step starts):")
+for name, v in sorted(first_call.items(), key=lambda kv: sorted(kv[1])[len(kv[1]) // 2]):
+    print(f"  {name:36s} {1e6 * sorted(v)[len(v) // 2]:8.0f}")
 for label in order:
     print(f"  {label:32s} {1e6 * acc[label] / n:8.1f} us/step  ({calls[label] / n:.1f} calls)")
