@@ -184,6 +184,7 @@ SIGNATURES = {
     "gstex_adam_step_guarded": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double, c_int32,
                                           c_float, _P, _P]),
     "gstex_train_prologue": (c_int32, [POINTER(GstexTrainPrologueArgs), _P]),
+    "gstex_train_prologue_scan_bytes": (c_size_t, [c_int32]),
     "gstex_adam_step_scheduled": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double,
                                             c_int32, c_float, _P, POINTER(GstexAdamSchedule), _P]),
 }

@@ -12,6 +12,7 @@
 //   (the third is detached), and the sigmoid.  Replaces ~40 small torch kernels per step.
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "splat_math.h"  // activate_splat
 
 using namespace gstex;
 
@@ -29,32 +30,11 @@ __global__ __launch_bounds__(256) void activate_fwd_kernel(
     float* __restrict__ viewdirs) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float4 q = reinterpret_cast<const float4*>(quats)[i];
-    const float nq = norm4(q.x, q.y, q.z, q.w);
-    const float w = q.x / nq, x = q.y / nq, y = q.z / nq, z = q.w / nq;
-    reinterpret_cast<float4*>(quats_n)[i] = make_float4(w, x, y, z);
-    const float s0 = fmaxf(expf(log_scales[3 * i]), 1e-9f), s1 = fmaxf(expf(log_scales[3 * i + 1]), 1e-9f);
-    scales[3 * i] = s0;
-    scales[3 * i + 1] = s1;
-    scales[3 * i + 2] = 1e-5f * ((s0 + s1) / 2.0f);
-    opacities[i] = 1.0f / (1.0f + expf(-opac_logits[i]));
-    // get_uv_mapping: rotation of the re-normalised quaternion (F.normalize, eps 1e-12)
-    const float n2 = fmaxf(norm4(w, x, y, z), 1e-12f);
-    const float rw = w / n2, rx = x / n2, ry = y / n2, rz = z / n2;
-    const float m0 = mappings[(size_t)map_stride * i], m1 = mappings[(size_t)map_stride * i + 1];
-    umap[3 * i] = m0 * (1.0f - 2.0f * (ry * ry + rz * rz));
-    umap[3 * i + 1] = m0 * (2.0f * (rx * ry + rw * rz));
-    umap[3 * i + 2] = m0 * (2.0f * (rx * rz - rw * ry));
-    vmap[3 * i] = m1 * (2.0f * (rx * ry - rw * rz));
-    vmap[3 * i + 1] = m1 * (1.0f - 2.0f * (rx * rx + rz * rz));
-    vmap[3 * i + 2] = m1 * (2.0f * (ry * rz + rw * rx));
-    uv0[2 * i] = 0.5f;
-    uv0[2 * i + 1] = 0.5f;
-    const float dx = means[3 * i] - campos[0], dy = means[3 * i + 1] - campos[1], dz = means[3 * i + 2] - campos[2];
-    const float nd = sqrtf((dx * dx + dy * dy) + dz * dz);
-    viewdirs[3 * i] = dx / nd;
-    viewdirs[3 * i + 1] = dy / nd;
-    viewdirs[3 * i + 2] = dz / nd;
+    const Activated a = activate_splat(reinterpret_cast<const float4*>(quats)[i], log_scales[3 * i],
+                                       log_scales[3 * i + 1], opac_logits[i], mappings[(size_t)map_stride * i],
+                                       mappings[(size_t)map_stride * i + 1], means[3 * i], means[3 * i + 1],
+                                       means[3 * i + 2], campos);
+    store_activated(i, a, quats_n, scales, opacities, uv0, umap, vmap, viewdirs);
 }
 
 __global__ __launch_bounds__(256) void activate_bwd_kernel(

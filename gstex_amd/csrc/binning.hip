@@ -14,6 +14,7 @@
 // Keys are unique (id is part of the key), so any correct sort yields the same, bit-exact order.
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "splat_math.h"
 
 using namespace gstex;
 
@@ -28,35 +29,6 @@ constexpr int kSortCap = 4096;  // keys per LDS sort (32 KiB)
 #define GSTEX_SORT_REGS 1
 #endif
 
-// Inclusive wave64 scan.
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
-
-// Exclusive scan of one 256-thread block's per-thread totals; returns the block total in *total.
-__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int incl = wave_incl_scan(v);
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    int wave_off = 0, sum = 0;
-#pragma unroll
-    for (int w = 0; w < kScanThreads / 64; ++w) {
-        int s = s_wave[w];
-        if (w < wave) wave_off += s;
-        sum += s;
-    }
-    __syncthreads();
-    *total = sum;
-    return wave_off + incl - v;
-}
-
 __global__ __launch_bounds__(kScanThreads) void scan_partials_kernel(int n, const int32_t* __restrict__ in,
                                                                      int32_t* __restrict__ block_sums) {
     __shared__ int s_wave[kScanThreads / 64];
@@ -65,7 +37,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_partials_kernel(int n, cons
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) v += (base + k < n) ? in[base + k] : 0;
     int total;
-    block_excl_scan(v, s_wave, &total);
+    block_excl_scan<kScanThreads>(v, s_wave, &total);
     if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
@@ -77,28 +49,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_block_sums_kernel(int nb, i
         int i = b0 + threadIdx.x;
         int v = (i < nb) ? sums[i] : 0;
         int total;
-        int ex = block_excl_scan(v, s_wave, &total);
+        int ex = block_excl_scan<kScanThreads>(v, s_wave, &total);
         if (i < nb) sums[i] = carry + ex;
         carry += total;
     }
-}
-
-// Pair-capacity guard (gstex_scan_offsets_guarded, ABI 13), applied by the thread that writes the total out[n]: the
-// step's overflow flag (1.0f when the total exceeds the pair buffers' capacity; the first render of a step writes it,
-// later ones OR into it) and, when given, the total in device-writable host memory (no copy, no synchronisation:
-// the host reads it once the stream has passed this kernel).  Plain vector stores.
-struct ScanGuard {
-    long long capacity;
-    float* flag;
-    int32_t* host_count;
-    int first;
-};
-__device__ __forceinline__ void apply_guard(const ScanGuard& g, int total) {
-    if (g.flag) {
-        const float over = (long long)total > g.capacity ? 1.0f : 0.0f;
-        *g.flag = g.first ? over : fmaxf(*g.flag, over);
-    }
-    if (g.host_count) *g.host_count = total;
 }
 
 __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(int n, const int32_t* __restrict__ in,
@@ -114,7 +68,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(int n, const i
         v += vals[k];
     }
     int total;
-    int ex = block_excl_scan(v, s_wave, &total) + block_offs[blockIdx.x];
+    int ex = block_excl_scan<kScanThreads>(v, s_wave, &total) + block_offs[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         if (base + k < n) out[base + k] = ex;
@@ -141,7 +95,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_single_kernel(int n, const 
             v += vals[k];
         }
         int total;
-        int ex = block_excl_scan(v, s_wave, &total) + carry;
+        int ex = block_excl_scan<kScanThreads>(v, s_wave, &total) + carry;
 #pragma unroll
         for (int k = 0; k < kScanItems; ++k) {
             if (base + k < n) out[base + k] = ex;

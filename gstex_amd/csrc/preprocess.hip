@@ -5,6 +5,7 @@
 // every array is SoA-contiguous fp32 so a wave reads 64 consecutive splats per load.
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "splat_math.h"  // preprocess_splat
 
 using namespace gstex;
 
@@ -152,19 +153,14 @@ __global__ __launch_bounds__(kBlock) void preprocess_kernel(int n, const float* 
     const Camera cam = load_camera(cam_args);
     int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    f3 mu = mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]);
-    depths[i] = vrow(cam, 2, mu) + cam.V[11];
-    Frame fr;
-    float su, sv;
-    Homog h = load_homog(i, means, scales, glob, quats, cam, fr, su, sv);
-    float cx = 0.0f, cy = 0.0f, ex = 0.0f, ey = 0.0f;
-    if (!aabb_from_homog(h, cx, cy, ex, ey)) { cx = cy = ex = ey = 0.0f; }
-    centers[2 * i] = cx;
-    centers[2 * i + 1] = cy;
-    extents[2 * i] = ex;
-    extents[2 * i + 1] = ey;
-    Rect r = tile_rect(cx, cy, ex, ey, tiles_x, tiles_y, block);
-    nth[i] = (r.x1 - r.x0) * (r.y1 - r.y0);
+    const Preprocessed p = preprocess_splat(cam, mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]), scales[3 * i],
+                                            scales[3 * i + 1], glob, quats + 4 * i, tiles_x, tiles_y, block);
+    depths[i] = p.depth;
+    centers[2 * i] = p.cx;
+    centers[2 * i + 1] = p.cy;
+    extents[2 * i] = p.ex;
+    extents[2 * i + 1] = p.ey;
+    nth[i] = p.nth;
 }
 
 }  // namespace

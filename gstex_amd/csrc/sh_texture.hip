@@ -11,57 +11,11 @@
 //                                       same sampler the rasterizer uses (gstex_common.h).
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "splat_math.h"  // sh_basis, sh_colour
 
 using namespace gstex;
 
 namespace {
-
-constexpr float SH_C0 = 0.28209479177387814f;
-constexpr float SH_C1 = 0.4886025119029199f;
-__constant__ float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
-                               -1.0925484305920792f, 0.5462742152960396f};
-__constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
-                               0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
-                               -0.5900435899266435f};
-__constant__ float SH_C4[9] = {2.5033429417967046f,  -1.7701307697799304f, 0.9461746957575601f,
-                               -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
-                               0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
-
-// basis[k] for k < (degree+1)^2
-__device__ __forceinline__ void sh_basis(int degree, float x, float y, float z, float* b) {
-    b[0] = SH_C0;
-    if (degree < 1) return;
-    float nrm = sqrtf((x * x + y * y) + z * z);
-    x = x / nrm; y = y / nrm; z = z / nrm;
-    b[1] = -SH_C1 * y;
-    b[2] = SH_C1 * z;
-    b[3] = -SH_C1 * x;
-    if (degree < 2) return;
-    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-    b[4] = SH_C2[0] * xy;
-    b[5] = SH_C2[1] * yz;
-    b[6] = SH_C2[2] * ((2.0f * zz - xx) - yy);
-    b[7] = SH_C2[3] * xz;
-    b[8] = SH_C2[4] * (xx - yy);
-    if (degree < 3) return;
-    b[9] = SH_C3[0] * y * (3.0f * xx - yy);
-    b[10] = SH_C3[1] * xy * z;
-    b[11] = SH_C3[2] * y * ((4.0f * zz - xx) - yy);
-    b[12] = SH_C3[3] * z * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
-    b[13] = SH_C3[4] * x * ((4.0f * zz - xx) - yy);
-    b[14] = SH_C3[5] * z * (xx - yy);
-    b[15] = SH_C3[6] * x * (xx - 3.0f * yy);
-    if (degree < 4) return;
-    b[16] = SH_C4[0] * xy * (xx - yy);
-    b[17] = SH_C4[1] * yz * (3.0f * xx - yy);
-    b[18] = SH_C4[2] * xy * (7.0f * zz - 1.0f);
-    b[19] = SH_C4[3] * yz * (7.0f * zz - 3.0f);
-    b[20] = SH_C4[4] * (zz * (35.0f * zz - 30.0f) + 3.0f);
-    b[21] = SH_C4[5] * xz * (7.0f * zz - 3.0f);
-    b[22] = SH_C4[6] * (xx - yy) * (7.0f * zz - 1.0f);
-    b[23] = SH_C4[7] * xz * (xx - 3.0f * yy);
-    b[24] = SH_C4[8] * (xx * (xx - 3.0f * yy) - yy * (3.0f * xx - yy));
-}
 
 // coeffs[i][k - k0] holds basis k (k0 = 1: the DC coefficient is implicitly zero, gstex.py:1100 zeroes it;
 // starting the sum at +0 without the zero DC product gives the same bits as with it)
@@ -109,19 +63,6 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int k0, 
 // thread, when it is 16-B aligned (the scalar copy with a division per word was the kernels' latency chain).
 constexpr int kShBlock = 128;
 constexpr int kShStagedMaxK = 25;
-__device__ __forceinline__ void sh_copy_span(float* __restrict__ dst, const float* __restrict__ src, int total) {
-    const int t = threadIdx.x;
-    int done = 0;
-    if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
-        const int n4 = total >> 2;
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        float4* d4 = reinterpret_cast<float4*>(dst);
-#pragma unroll 4
-        for (int q = t; q < n4; q += kShBlock) d4[q] = s4[q];
-        done = n4 << 2;
-    }
-    for (int q = done + t; q < total; q += kShBlock) dst[q] = src[q];
-}
 
 __global__ __launch_bounds__(kShBlock) void sh_fwd_staged_kernel(int n, int degree, int k0, int K,
                                                                 const float* __restrict__ dirs,
@@ -131,21 +72,13 @@ __global__ __launch_bounds__(kShBlock) void sh_fwd_staged_kernel(int n, int degr
     const int t = threadIdx.x;
     const int i0 = blockIdx.x * kShBlock;
     const int cnt = min(kShBlock, n - i0);
-    const int nb = (degree + 1) * (degree + 1);
     const int kw = K * 3;  // words per splat row
-    sh_copy_span(s_c, coeffs + (size_t)i0 * kw, cnt * kw);
+    sh_copy_span<kShBlock>(s_c, coeffs + (size_t)i0 * kw, cnt * kw);
     __syncthreads();
     if (t >= cnt) return;
     const int i = i0 + t;
-    float b[25];
-    sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
-    const float* c = s_c + t * kw - 3 * k0;
-    float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-    for (int k = k0; k < nb; ++k) {
-        r0 = r0 + b[k] * c[3 * k];
-        r1 = r1 + b[k] * c[3 * k + 1];
-        r2 = r2 + b[k] * c[3 * k + 2];
-    }
+    float r0, r1, r2;
+    sh_colour(degree, k0, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], s_c + t * kw - 3 * k0, r0, r1, r2);
     out[3 * i] = r0;
     out[3 * i + 1] = r1;
     out[3 * i + 2] = r2;
@@ -175,7 +108,7 @@ __global__ __launch_bounds__(kShBlock) void sh_bwd_staged_kernel(int n, int degr
         }
     }
     __syncthreads();
-    sh_copy_span(v_coeffs + (size_t)i0 * kw, s_c, cnt * kw);
+    sh_copy_span<kShBlock>(v_coeffs + (size_t)i0 * kw, s_c, cnt * kw);
 }
 
 // One thread per (query, channel-group): query q reads its 4 corner texels.

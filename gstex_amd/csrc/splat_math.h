@@ -1,0 +1,232 @@
+// splat_math.h — per-splat device functions shared by the per-op kernels and the training prologue's fused
+// kernels (trainstep.hip): the parameter activations (activations.hip), the preprocessing (preprocess.hip), the SH
+// colour (sh_texture.hip) and the block scans (binning.hip).  Each per-op kernel and the fused kernel call the same
+// function on the same fp32 values (-ffp-contract=off: every operation individually rounded), so their outputs are
+// bit-identical (tests/test_gpu_fused.py).
+#pragma once
+
+#include "gstex_common.h"
+
+namespace gstex {
+
+// ---- activations: gstex.py:1059-1066, 975-990, 1101-1104 (see activations.hip) ----------------------------------
+__device__ __forceinline__ float act_norm4(float a, float b, float c, float d) {
+    return sqrtf(((a * a + b * b) + c * c) + d * d);
+}
+
+struct Activated {
+    float q[4];          // quats / |quats|
+    float s0, s1, s2;    // scales (the third: 1e-5 * mean of the first two, detached)
+    float opacity;
+    float um[3], vm[3];  // umap, vmap (get_uv_mapping of the re-normalised quaternion)
+    float vd[3];         // viewdirs
+};
+
+__device__ __forceinline__ Activated activate_splat(float4 q, float ls0, float ls1, float logit, float m0, float m1,
+                                                    float mx, float my, float mz, const float* campos) {
+    Activated a;
+    const float nq = act_norm4(q.x, q.y, q.z, q.w);
+    const float w = q.x / nq, x = q.y / nq, y = q.z / nq, z = q.w / nq;
+    a.q[0] = w; a.q[1] = x; a.q[2] = y; a.q[3] = z;
+    a.s0 = fmaxf(expf(ls0), 1e-9f);
+    a.s1 = fmaxf(expf(ls1), 1e-9f);
+    a.s2 = 1e-5f * ((a.s0 + a.s1) / 2.0f);
+    a.opacity = 1.0f / (1.0f + expf(-logit));
+    // get_uv_mapping: rotation of the re-normalised quaternion (F.normalize, eps 1e-12)
+    const float n2 = fmaxf(act_norm4(w, x, y, z), 1e-12f);
+    const float rw = w / n2, rx = x / n2, ry = y / n2, rz = z / n2;
+    a.um[0] = m0 * (1.0f - 2.0f * (ry * ry + rz * rz));
+    a.um[1] = m0 * (2.0f * (rx * ry + rw * rz));
+    a.um[2] = m0 * (2.0f * (rx * rz - rw * ry));
+    a.vm[0] = m1 * (2.0f * (rx * ry - rw * rz));
+    a.vm[1] = m1 * (1.0f - 2.0f * (rx * rx + rz * rz));
+    a.vm[2] = m1 * (2.0f * (ry * rz + rw * rx));
+    const float dx = mx - campos[0], dy = my - campos[1], dz = mz - campos[2];
+    const float nd = sqrtf((dx * dx + dy * dy) + dz * dz);
+    a.vd[0] = dx / nd;
+    a.vd[1] = dy / nd;
+    a.vd[2] = dz / nd;
+    return a;
+}
+
+__device__ __forceinline__ void store_activated(int i, const Activated& a, float* quats_n, float* scales,
+                                                float* opacities, float* uv0, float* umap, float* vmap,
+                                                float* viewdirs) {
+    reinterpret_cast<float4*>(quats_n)[i] = make_float4(a.q[0], a.q[1], a.q[2], a.q[3]);
+    scales[3 * i] = a.s0;
+    scales[3 * i + 1] = a.s1;
+    scales[3 * i + 2] = a.s2;
+    opacities[i] = a.opacity;
+    umap[3 * i] = a.um[0];
+    umap[3 * i + 1] = a.um[1];
+    umap[3 * i + 2] = a.um[2];
+    vmap[3 * i] = a.vm[0];
+    vmap[3 * i + 1] = a.vm[1];
+    vmap[3 * i + 2] = a.vm[2];
+    uv0[2 * i] = 0.5f;
+    uv0[2 * i + 1] = 0.5f;
+    viewdirs[3 * i] = a.vd[0];
+    viewdirs[3 * i + 1] = a.vd[1];
+    viewdirs[3 * i + 2] = a.vd[2];
+}
+
+// ---- preprocessing: project_points' depth, get_aabb_2d, get_num_tiles_hit_2d (gstex.py:1077-1080) ---------------
+struct Preprocessed {
+    float depth, cx, cy, ex, ey;
+    int nth;
+};
+
+__device__ __forceinline__ Homog splat_homog(const Camera& cam, f3 mu, float s0, float s1, float glob, const float* q4,
+                                             Frame& fr, float& su, float& sv) {
+    fr = quat_frame(q4);
+    su = s0 * glob;
+    sv = s1 * glob;
+    return splat_homography(cam, mu, su, sv, fr);
+}
+
+__device__ __forceinline__ Preprocessed preprocess_splat(const Camera& cam, f3 mu, float s0, float s1, float glob,
+                                                         const float* q4, int tiles_x, int tiles_y, int block) {
+    Preprocessed p;
+    p.depth = vrow(cam, 2, mu) + cam.V[11];
+    Frame fr;
+    float su, sv;
+    Homog h = splat_homog(cam, mu, s0, s1, glob, q4, fr, su, sv);
+    p.cx = 0.0f; p.cy = 0.0f; p.ex = 0.0f; p.ey = 0.0f;
+    if (!aabb_from_homog(h, p.cx, p.cy, p.ex, p.ey)) { p.cx = p.cy = p.ex = p.ey = 0.0f; }
+    Rect r = tile_rect(p.cx, p.cy, p.ex, p.ey, tiles_x, tiles_y, block);
+    p.nth = (r.x1 - r.x0) * (r.y1 - r.y0);
+    return p;
+}
+
+// ---- SH colour of the gsplat-0.1 lineage, degree <= 4 (see sh_texture.hip) -----------------------------------------
+namespace {
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+__constant__ float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+__constant__ float SH_C4[9] = {2.5033429417967046f,  -1.7701307697799304f, 0.9461746957575601f,
+                               -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
+                               0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
+}  // namespace
+
+// basis[k] for k < (degree+1)^2
+__device__ __forceinline__ void sh_basis(int degree, float x, float y, float z, float* b) {
+    b[0] = SH_C0;
+    if (degree < 1) return;
+    float nrm = sqrtf((x * x + y * y) + z * z);
+    x = x / nrm; y = y / nrm; z = z / nrm;
+    b[1] = -SH_C1 * y;
+    b[2] = SH_C1 * z;
+    b[3] = -SH_C1 * x;
+    if (degree < 2) return;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    b[4] = SH_C2[0] * xy;
+    b[5] = SH_C2[1] * yz;
+    b[6] = SH_C2[2] * ((2.0f * zz - xx) - yy);
+    b[7] = SH_C2[3] * xz;
+    b[8] = SH_C2[4] * (xx - yy);
+    if (degree < 3) return;
+    b[9] = SH_C3[0] * y * (3.0f * xx - yy);
+    b[10] = SH_C3[1] * xy * z;
+    b[11] = SH_C3[2] * y * ((4.0f * zz - xx) - yy);
+    b[12] = SH_C3[3] * z * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
+    b[13] = SH_C3[4] * x * ((4.0f * zz - xx) - yy);
+    b[14] = SH_C3[5] * z * (xx - yy);
+    b[15] = SH_C3[6] * x * (xx - 3.0f * yy);
+    if (degree < 4) return;
+    b[16] = SH_C4[0] * xy * (xx - yy);
+    b[17] = SH_C4[1] * yz * (3.0f * xx - yy);
+    b[18] = SH_C4[2] * xy * (7.0f * zz - 1.0f);
+    b[19] = SH_C4[3] * yz * (7.0f * zz - 3.0f);
+    b[20] = SH_C4[4] * (zz * (35.0f * zz - 30.0f) + 3.0f);
+    b[21] = SH_C4[5] * xz * (7.0f * zz - 3.0f);
+    b[22] = SH_C4[6] * (xx - yy) * (7.0f * zz - 1.0f);
+    b[23] = SH_C4[7] * xz * (xx - 3.0f * yy);
+    b[24] = SH_C4[8] * (xx * (xx - 3.0f * yy) - yy * (3.0f * xx - yy));
+}
+
+// colour = sum_{k0 <= k < (degree+1)^2} basis[k] * c[k] (c: the splat's coefficient row, indexed from basis 0;
+// k0 = 1 for the rest coefficients, the DC term zeroed by the caller, gstex.py:1100)
+__device__ __forceinline__ void sh_colour(int degree, int k0, float dx, float dy, float dz, const float* c, float& r0,
+                                          float& r1, float& r2) {
+    float b[25];
+    sh_basis(degree, dx, dy, dz, b);
+    const int nb = (degree + 1) * (degree + 1);
+    r0 = 0.f; r1 = 0.f; r2 = 0.f;
+    for (int k = k0; k < nb; ++k) {
+        r0 = r0 + b[k] * c[3 * k];
+        r1 = r1 + b[k] * c[3 * k + 1];
+        r2 = r2 + b[k] * c[3 * k + 2];
+    }
+}
+
+// A workgroup's contiguous span of coefficient rows copied between global memory and LDS with consecutive lanes on
+// consecutive words (16-B vectors, several in flight per thread, when both sides are 16-B aligned).
+template <int kThreads>
+__device__ __forceinline__ void sh_copy_span(float* __restrict__ dst, const float* __restrict__ src, int total) {
+    const int t = threadIdx.x;
+    int done = 0;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+        const int n4 = total >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll 4
+        for (int q = t; q < n4; q += kThreads) d4[q] = s4[q];
+        done = n4 << 2;
+    }
+    for (int q = done + t; q < total; q += kThreads) dst[q] = src[q];
+}
+
+// ---- block scans (binning.hip) --------------------------------------------------------------------------------------
+// Inclusive wave64 scan.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// Exclusive scan of one kThreads-thread block's per-thread values; returns the block total in *total.
+template <int kThreads>
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = wave_incl_scan(v);
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    int wave_off = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+        int s = s_wave[w];
+        if (w < wave) wave_off += s;
+        sum += s;
+    }
+    __syncthreads();
+    *total = sum;
+    return wave_off + incl - v;
+}
+
+// Pair-capacity guard (gstex_scan_offsets_guarded, ABI 13), applied by the thread that writes the total out[n]: the
+// step's overflow flag (1.0f when the total exceeds the pair buffers' capacity; the first render of a step writes it,
+// later ones OR into it) and, when given, the total in device-writable host memory (no copy, no synchronisation:
+// the host reads it once the stream has passed this kernel).  Plain vector stores.
+struct ScanGuard {
+    long long capacity;
+    float* flag;
+    int32_t* host_count;
+    int first;
+};
+__device__ __forceinline__ void apply_guard(const ScanGuard& g, int total) {
+    if (g.flag) {
+        const float over = (long long)total > g.capacity ? 1.0f : 0.0f;
+        *g.flag = g.first ? over : fmaxf(*g.flag, over);
+    }
+    if (g.host_count) *g.host_count = total;
+}
+
+}  // namespace gstex

@@ -1,13 +1,15 @@
 """The photometric training render as one autograd node (not in the reference; GStexTrainer(fused_step=True)).
 
 GStexTrainer.render's training branch (gstex.py:992-1162 with the fused activations, the zeroed SH DC term and the
-read-back-free pair buffers) issues eight HIP launches before its raster forward -- activate, preprocess, sh_rest,
-the guarded scan, the splat records, the capped binning -- each behind its own Python wrapper, ctypes call, autograd
-node and a dozen tensor allocations.  Here the same launches are one C call (gstex_train_prologue, ABI 17) into one
-arena allocation, and the backward chains raster_bwd -> setup_bwd_aabb -> sh_rest_bwd -> activate_bwd in one node.
-The device work is identical, launch for launch and argument for argument (tests/test_gpu_fused.py compares both
-paths); what it removes is host time between the launches, which the device waits through whenever a step starts on
-an idle device -- the first step after a synchronisation (bench.py's first timed step).
+read-back-free pair buffers) issues eight C calls before its raster forward -- activate, preprocess, sh_rest, the
+guarded scan (three kernels), the splat records, the capped binning -- each behind its own Python wrapper, ctypes
+call, autograd node and a dozen tensor allocations.  Here they are one C call (gstex_train_prologue, ABI 17) into one
+arena allocation: activate + preprocess + sh_rest as one per-splat kernel and the scan as one launch (the same device
+functions on the same values, gstex_amd/csrc/splat_math.h: bit-identical outputs), then the records and the binning
+as before; the backward chains raster_bwd -> setup_bwd_aabb -> sh_rest_bwd -> activate_bwd in one node.
+tests/test_gpu_fused.py compares both paths.  What it removes is host time between the launches, which the device
+waits through whenever a step starts on an idle device -- the first step after a synchronisation (bench.py's first
+timed step) -- and four launches.
 
 Taken only where it applies (GStexTrainer._fused_ok): one process's own texel-gradient buffer (defer_texture, no
 GradSync route), a sized PairCapacity, SH degree > 0 without fix_init, no geometry outputs, non-deterministic
@@ -36,7 +38,7 @@ def _layout(n: int, n_rest: int, capacity: int, H: int, W: int, C: int):
     lib = _lib.load()
     n_tiles = ((W + ops.BLOCK_WIDTH - 1) // ops.BLOCK_WIDTH) * ((H + ops.BLOCK_WIDTH - 1) // ops.BLOCK_WIDTH)
     f4 = 4
-    scan_ws = max(int(lib.gstex_scan_workspace_size(n)), 1)
+    scan_ws = max(int(lib.gstex_train_prologue_scan_bytes(n)), 1)
     bin_ws = max(int(lib.gstex_bin_workspace_size(n, capacity, n_tiles)), 1)
     aux = int(lib.gstex_raster_aux_bytes(capacity, n_tiles, C))
     items = [  # forward: the prologue's outputs, the raster's outputs and its record for the backward

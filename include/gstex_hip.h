@@ -411,12 +411,13 @@ int gstex_adam_step_scheduled(int32_t n_tensors, const gstex_adam_tensor* tensor
                               const gstex_adam_schedule* schedule, void* stream);
 
 /* ---- training-step prologue (ABI 17; not in the reference) ------------------------------------------------------
- * One host call for the launches a photometric training render makes before its raster forward, in this order:
- * gstex_activate_fwd, gstex_preprocess (the camera without c2w), gstex_sh_rest_fwd, gstex_scan_offsets_guarded,
- * gstex_raster_setup (glob_scale 1), gstex_bin_sort_capped -- the same kernels with the same arguments as the
- * per-op entry points (gstex_amd.fused: the trainer's render without ~0.3 ms of per-launch host overhead, which a
- * step that starts on an idle device waits for).  All pointers are device pointers; the buffers are sized as the
- * per-op entry points require (block = 16). */
+ * One host call for the launches a photometric training render makes before its raster forward: the outputs of
+ * gstex_activate_fwd, gstex_preprocess (the camera without c2w), gstex_sh_rest_fwd and gstex_scan_offsets_guarded --
+ * bit-identical, computed by one per-splat kernel (the same device functions on the same values) and a one-launch
+ * scan -- then gstex_raster_setup (glob_scale 1) and gstex_bin_sort_capped as called per op (gstex_amd.fused: the
+ * trainer's render without ~0.2 ms of per-launch host overhead, which a step that starts on an idle device waits for,
+ * and four launches fewer).  All pointers are device pointers; the buffers are sized as the per-op entry points
+ * require (block = 16), scan_workspace as gstex_train_prologue_scan_bytes(n). */
 typedef struct gstex_train_prologue_args {
     int32_t n;
     int32_t sh_degree;
@@ -457,6 +458,9 @@ typedef struct gstex_train_prologue_args {
     size_t bin_workspace_bytes;
 } gstex_train_prologue_args;
 int gstex_train_prologue(const gstex_train_prologue_args* args, void* stream);
+/* Bytes of scan_workspace gstex_train_prologue needs for n splats (>= gstex_scan_workspace_size(n): the fused
+ * preprocessing kernel leaves one tile-count sum per 128 splats there for the one-launch offsets scan). */
+size_t gstex_train_prologue_scan_bytes(int32_t n);
 
 #ifdef __cplusplus
 }

@@ -189,6 +189,12 @@ def test_struct_layouts_match_header(tmp_path):
             assert int(got[f"{cname} {f[0]}"]) == getattr(cls, f[0]).offset, f"{cname}.{f[0]}"
 
 
+def test_train_prologue_scan_bytes(lib):
+    for n in (0, 1, 127, 128, 1025, 200_000):
+        b = lib.gstex_train_prologue_scan_bytes(n)
+        assert b >= lib.gstex_scan_workspace_size(n) and b >= 4 * ((n + 127) // 128)
+
+
 def test_train_prologue_rejects_null_args(lib):
     rc, msg = _status(lib, "gstex_train_prologue", None, None)
     assert rc != 0 and "null" in msg

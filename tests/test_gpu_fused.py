@@ -1,7 +1,8 @@
 """GStexTrainer(fused_step=True) (gstex_amd.fused: the photometric training render as one C prologue call and one
-autograd node) against the per-op path on the GPU: the same launches with the same arguments, so the rendered image,
-the loss and the forward's outputs are bit-identical, and the gradients agree up to the order of their float-atomic
-sums; a few training steps of each path train alike."""
+autograd node) against the per-op path on the GPU: the prologue's fused kernels compute the per-op outputs with the
+same device functions on the same values (gstex_amd/csrc/splat_math.h) and the rest are the same launches, so the
+rendered image and the loss are bit-identical, and the gradients agree up to the order of their float-atomic sums; a
+few training steps of each path train alike."""
 import pytest
 import torch
 
@@ -32,11 +33,14 @@ def _count_fused(monkeypatch):
     return calls
 
 
-def test_fused_render_matches_per_op(monkeypatch):
+@pytest.mark.parametrize("n,texels", [(4000, 80_000), (1500, 30_000), (300, 6_000)])
+def test_fused_render_matches_per_op(monkeypatch, n, texels):
+    """n = 4000: several scan tiles with a partial last one; 1500: one full tile and a partial one; 300: a single
+    partial 128-splat block of the fused preprocessing kernel and a single scan tile."""
     from gstex_amd.model import GStexTrainer
 
     calls = _count_fused(monkeypatch)
-    dev, sc, views, gts = _setup()
+    dev, sc, views, gts = _setup(n, texels)
     tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=True)
     # the first render sizes the pair capacity (one read-back) through the per-op path
     tr.zero_grad()
