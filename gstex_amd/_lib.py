@@ -25,6 +25,7 @@ SETTING_AA_BLUR = 1 << 9
 SETTING_DIST_REG = 1 << 10
 SETTING_EDIT = 1 << 13
 SETTING_EVAL_NORMAL = 1 << 15
+SETTING_AUX_ZEROED = 1 << 28  # GSTEX_SETTING_AUX_ZEROED: the prologue zeroed the forward's accumulated aux span
 
 
 class GstexCamera(ctypes.Structure):
@@ -85,7 +86,8 @@ class GstexTrainPrologueArgs(ctypes.Structure):
             "num_tiles_hit", "rgbs", "offsets", "scan_workspace")] + [("scan_workspace_bytes", c_size_t)] + [
         (name, c_void_p) for name in (
             "records", "tile_ranges", "sorted_ids", "sorted_slots", "tile_order", "bin_workspace")] + [
-        ("bin_workspace_bytes", c_size_t)]
+        ("bin_workspace_bytes", c_size_t), ("raster_aux", c_void_p), ("raster_aux_bytes", c_size_t),
+        ("raster_channels", c_int32)]
 
 
 ADAM_ZERO_GRAD = 1  # GSTEX_ADAM_ZERO_GRAD

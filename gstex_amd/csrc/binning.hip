@@ -14,6 +14,7 @@
 // Keys are unique (id is part of the key), so any correct sort yields the same, bit-exact order.
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "gstex_internal.h"
 #include "splat_math.h"
 
 using namespace gstex;
@@ -590,7 +591,7 @@ namespace {
 int bin_sort_impl(int32_t n, int64_t n_isect, const float* centers, const float* extents, const float* depths,
                   const int32_t* offsets, int32_t H, int32_t W, int32_t block, int32_t* tile_ranges,
                   int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order_out, void* workspace,
-                  size_t workspace_bytes, void* stream, bool capped = false) {
+                  size_t workspace_bytes, void* stream, bool capped = false, bool count_zeroed = false) {
     GSTEX_REQUIRE(n >= 0 && n_isect >= 0 && n_isect < (1ll << 31) && H > 0 && W > 0 && block > 0,
                   "gstex_bin_sort: invalid sizes (n=%d, n_isect=%lld, H=%d, W=%d, block=%d)", n,
                   (long long)n_isect, H, W, block);
@@ -613,7 +614,7 @@ int bin_sort_impl(int32_t n, int64_t n_isect, const float* centers, const float*
     BinWorkspace ws;
     bin_layout(n_tiles, n_isect, (char*)workspace, &ws);
     // (the whole 256-B-aligned slot: a size that is not a multiple of 16 B costs the runtime a second fill kernel)
-    (void)hipMemsetAsync(ws.tile_count, 0, align256((size_t)(n_tiles + 1) * sizeof(int32_t)), st);
+    if (!count_zeroed) (void)hipMemsetAsync(ws.tile_count, 0, align256((size_t)(n_tiles + 1) * sizeof(int32_t)), st);
     if (n_tiles <= kCountLdsTiles)
         count_lds_kernel<<<div_up(n, 256 * kCountSplatsPerThread), 256, 0, st>>>(
             n, centers, extents, offsets, tiles_x, tiles_y, block, ws.tile_count, ws.rank, cap);
@@ -668,6 +669,24 @@ extern "C" int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* c
     return bin_sort_impl(n, capacity, centers, extents, depths, offsets, H, W, block, tile_ranges, sorted_ids,
                          sorted_slots, tile_order, workspace, workspace_bytes, stream, true);
 }
+
+namespace gstex {
+ZeroSpan bin_count_span(void* workspace, int32_t n_tiles, int64_t n_isect) {
+    BinWorkspace ws;
+    bin_layout(n_tiles, n_isect, (char*)workspace, &ws);
+    return ZeroSpan{ws.tile_count, align256((size_t)(n_tiles + 1) * sizeof(int32_t))};
+}
+
+int bin_sort_capped_prezeroed(int32_t n, int64_t capacity, const float* centers, const float* extents,
+                              const float* depths, const int32_t* offsets, int32_t H, int32_t W, int32_t block,
+                              int32_t* tile_ranges, int32_t* sorted_ids, int32_t* sorted_slots, int32_t* tile_order,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+    GSTEX_REQUIRE(tile_order, "gstex_bin_sort_capped: null tile_order");
+    GSTEX_REQUIRE(capacity >= 0, "gstex_bin_sort_capped: capacity < 0");
+    return bin_sort_impl(n, capacity, centers, extents, depths, offsets, H, W, block, tile_ranges, sorted_ids,
+                         sorted_slots, tile_order, workspace, workspace_bytes, stream, true, true);
+}
+}  // namespace gstex
 
 extern "C" int gstex_scan_offsets_guarded(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
                                           size_t workspace_bytes, const gstex_pair_guard* guard, void* stream) {

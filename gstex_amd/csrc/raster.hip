@@ -20,6 +20,7 @@
 //     atomics.
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "gstex_internal.h"
 
 using namespace gstex;
 
@@ -2151,6 +2152,13 @@ int check_settings(int settings) {
 
 }  // namespace
 
+namespace gstex {
+ZeroSpan raster_aux_zero_span(void* aux, int64_t n_isect, int32_t n_tiles, int32_t channels) {
+    const AuxLayout al = aux_layout(n_isect, n_tiles, channels);
+    return ZeroSpan{aux ? (char*)aux + al.cost : nullptr, al.order_ws - al.cost + (size_t)kUnitBins * 4};
+}
+}  // namespace gstex
+
 extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* scales, float glob_scale,
                                   const float* quats, const float* rgbs, const float* opacities,
                                   const float* centers, const float* uv0, const float* umap, const float* vmap,
@@ -2192,7 +2200,7 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
                   channels);
     GSTEX_REQUIRE(n_texels >= 0 && n_texels * channels < (int64_t)INT32_MAX, "gstex_raster_fwd: n_texels out of range");
     GSTEX_REQUIRE(n_texels == 0 || texture, "gstex_raster_fwd: null texture");
-    int rc = check_settings(settings);
+    int rc = check_settings(settings & ~GSTEX_SETTING_AUX_ZEROED);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && out_img && out_alpha && out_tex && state, "gstex_raster_fwd: null pointer");
     const bool geo = out_depth || out_reg || out_normal;
@@ -2207,8 +2215,10 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     const AuxPtrs ap = aux_ptrs(aux, al);
     // one fill: unit costs (units the forward never reaches keep 0; the backward skips them), the launch order
     // (0 = no unit at that position) and the unit-order histogram the forward builds (contiguous in the layout)
-    if (aux && hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
+    if (aux && !(settings & GSTEX_SETTING_AUX_ZEROED) &&
+        hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
         return launch_status("gstex_raster_fwd (aux)");
+    settings &= ~GSTEX_SETTING_AUX_ZEROED;
     ZeroBufs zbuf;
     zbuf.p[0] = zero_floats > 0 && !(GSTEX_ABLATE & 512) ? zero_buf : nullptr;
     zbuf.n[0] = zero_floats;

@@ -9,10 +9,13 @@
 //   train_scan_kernel   the offsets scan in one launch: each 1024-splat scan tile starts from the sum of the block
 //                       sums before it (8 per tile; at most n / 128 L2-resident words), then scans its tile as
 //                       binning.hip's scan_final_kernel does (same integers, same guard);
-// then gstex_raster_setup and gstex_bin_sort_capped unchanged.  Four launches fewer and no host time between the
-// launches (the device waits through that whenever a step starts on an idle device, after a synchronisation).
+//                       its grid also zeroes the binning's tile counters and the raster forward's accumulated aux span
+//                       (args.raster_aux), so neither needs its fill launch (GSTEX_SETTING_AUX_ZEROED);
+// then gstex_raster_setup and the capped binning.  Six launches fewer and no host time between the launches (the
+// device waits through that whenever a step starts on an idle device, after a synchronisation).
 #include "gstex_common.h"
 #include "gstex_error.h"
+#include "gstex_internal.h"
 #include "splat_math.h"
 
 using namespace gstex;
@@ -73,8 +76,15 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
 
 __global__ __launch_bounds__(kScanBlock) void train_scan_kernel(int n, const int32_t* __restrict__ in,
                                                                 const int32_t* __restrict__ block_sums,
-                                                                int32_t* __restrict__ out, const ScanGuard guard) {
+                                                                int32_t* __restrict__ out, const ScanGuard guard,
+                                                                uint4* __restrict__ z0, int z0n,
+                                                                uint4* __restrict__ z1, int z1n) {
     __shared__ int s_wave[kScanBlock / 64];
+    // side job: the binning's tile counters and the raster forward's accumulated aux span (their fill launches)
+    for (int k = blockIdx.x * kScanBlock + threadIdx.x; k < z0n + z1n; k += gridDim.x * kScanBlock) {
+        if (k < z0n) z0[k] = make_uint4(0u, 0u, 0u, 0u);
+        else z1[k - z0n] = make_uint4(0u, 0u, 0u, 0u);
+    }
     const int tile = blockIdx.x;
     int pre = 0;
     for (int j = threadIdx.x; j < tile * kBlocksPerTile; j += kScanBlock) pre += block_sums[j];
@@ -119,6 +129,17 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
                   gstex_train_prologue_scan_bytes(a->n));
     gstex_camera pre = a->cam;  // preprocessing takes the view without c2w (as gstex_amd.ops.preprocess)
     pre.c2w = nullptr;
+    GSTEX_REQUIRE(pre.block > 0 && pre.H > 0 && pre.W > 0, "gstex_train_prologue: invalid camera");
+    {  // the spans zeroed below lie inside the buffers the caller sized
+        const int n_tiles = ((pre.W + pre.block - 1) / pre.block) * ((pre.H + pre.block - 1) / pre.block);
+        GSTEX_REQUIRE(a->bin_workspace &&
+                          a->bin_workspace_bytes >= gstex_bin_workspace_size(a->n, a->capacity, n_tiles),
+                      "gstex_train_prologue: bin workspace too small");
+        GSTEX_REQUIRE(!a->raster_aux || (a->raster_channels >= 1 && a->raster_channels <= 8 &&
+                                         a->raster_aux_bytes >= gstex_raster_aux_bytes(a->capacity, n_tiles,
+                                                                                       a->raster_channels)),
+                      "gstex_train_prologue: raster aux buffer too small or channels out of range");
+    }
     int rc;
     const bool fused = a->n > 0 && a->sh_degree >= 1 && a->sh_degree <= 4 && a->n_rest <= kMaxRest &&
                        a->n_rest >= (a->sh_degree + 1) * (a->sh_degree + 1) - 1 && a->map_cols >= 2;
@@ -130,7 +151,6 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
                       "gstex_train_prologue: null pointer");
         GSTEX_REQUIRE(((reinterpret_cast<uintptr_t>(a->quats) | reinterpret_cast<uintptr_t>(a->quats_n)) & 15) == 0,
                       "gstex_train_prologue: quaternions must be 16-byte aligned");
-        GSTEX_REQUIRE(pre.block > 0 && pre.H > 0 && pre.W > 0, "gstex_train_prologue: invalid camera");
         hipStream_t st = as_stream(stream);
         const int tx = (pre.W + pre.block - 1) / pre.block, ty = (pre.H + pre.block - 1) / pre.block;
         int32_t* sums = static_cast<int32_t*>(a->scan_workspace);
@@ -142,8 +162,15 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
             a->num_tiles_hit, a->rgbs, sums);
         const ScanGuard g{(long long)a->guard.capacity, a->guard.step_flag, a->guard.host_count,
                           a->guard.first ? 1 : 0};
-        train_scan_kernel<<<div_up(a->n, kScanTile), kScanBlock, 0, st>>>(a->n, a->num_tiles_hit, sums, a->offsets,
-                                                                          g);
+        const ZeroSpan zb = bin_count_span(a->bin_workspace, tx * ty, a->capacity);
+        const ZeroSpan za = a->raster_aux ? raster_aux_zero_span(a->raster_aux, a->capacity, tx * ty,
+                                                                 a->raster_channels)
+                                          : ZeroSpan{nullptr, 0};
+        GSTEX_REQUIRE(((reinterpret_cast<uintptr_t>(zb.ptr) | reinterpret_cast<uintptr_t>(za.ptr) | zb.bytes | za.bytes) &
+                       15) == 0, "gstex_train_prologue: workspaces must be 16-byte aligned");
+        train_scan_kernel<<<div_up(a->n, kScanTile), kScanBlock, 0, st>>>(
+            a->n, a->num_tiles_hit, sums, a->offsets, g, static_cast<uint4*>(zb.ptr), (int)(zb.bytes / 16),
+            static_cast<uint4*>(za.ptr), (int)(za.bytes / 16));
         rc = launch_status("gstex_train_prologue");
     } else {  // the per-op entry points (n = 0, or an SH layout the fused kernel does not stage)
         rc = gstex_activate_fwd(a->n, a->means, a->quats, a->log_scales, a->opac_logits, a->mappings, a->map_cols,
@@ -157,11 +184,21 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
         if (rc) return rc;
         rc = gstex_scan_offsets_guarded(a->n, a->num_tiles_hit, a->offsets, a->scan_workspace,
                                         a->scan_workspace_bytes, &a->guard, stream);
+        if (rc == 0 && a->raster_aux) {  // (the caller passes GSTEX_SETTING_AUX_ZEROED to the forward)
+            const int tx = (pre.W + pre.block - 1) / pre.block, ty = (pre.H + pre.block - 1) / pre.block;
+            const ZeroSpan za = raster_aux_zero_span(a->raster_aux, a->capacity, tx * ty, a->raster_channels);
+            if (hipMemsetAsync(za.ptr, 0, za.bytes, as_stream(stream)) != hipSuccess)
+                return launch_status("gstex_train_prologue (aux)");
+        }
     }
     if (rc) return rc;
     rc = gstex_raster_setup(a->n, a->means, a->scales, 1.0f, a->quats_n, a->rgbs, a->opacities, a->centers, a->uv0,
                             a->umap, a->vmap, a->texture_dims, a->num_tiles_hit, &a->cam, a->records, stream);
     if (rc) return rc;
+    if (fused)  // the tile counters were zeroed by train_scan_kernel
+        return bin_sort_capped_prezeroed(a->n, a->capacity, a->centers, a->extents, a->depths, a->offsets, a->cam.H,
+                                         a->cam.W, a->cam.block, a->tile_ranges, a->sorted_ids, a->sorted_slots,
+                                         a->tile_order, a->bin_workspace, a->bin_workspace_bytes, stream);
     return gstex_bin_sort_capped(a->n, a->capacity, a->centers, a->extents, a->depths, a->num_tiles_hit, a->offsets,
                                  a->cam.H, a->cam.W, a->cam.block, a->tile_ranges, a->sorted_ids, a->sorted_slots,
                                  a->tile_order, a->bin_workspace, a->bin_workspace_bytes, stream);

@@ -105,12 +105,14 @@ class _TrainRender(torch.autograd.Function):
             num_tiles_hit=P["num_tiles_hit"], rgbs=P["rgbs"], offsets=P["offsets"], scan_workspace=P["scan_ws"],
             scan_workspace_bytes=sizes["scan_ws"], records=P["records"], tile_ranges=P["tile_ranges"],
             sorted_ids=P["sorted_ids"], sorted_slots=P["sorted_slots"], tile_order=P["tile_order"],
-            bin_workspace=P["bin_ws"], bin_workspace_bytes=sizes["bin_ws"])
+            bin_workspace=P["bin_ws"], bin_workspace_bytes=sizes["bin_ws"],
+            raster_aux=P["aux"] if sizes["aux"] else None, raster_aux_bytes=sizes["aux"], raster_channels=C)
         _lib.call("gstex_train_prologue", ctypes.byref(a), st)
         pcap.commit(slot, cap, tr.step, dev)
         texture = tr.texture_dc
         zn = sink.numel() if zero_sink else 0
-        ops._launch("gstex_raster_fwd_zero", cam, C, int(tr.settings), ptr(tr._bg_zero), P["records"],
+        aux_zeroed = _lib.SETTING_AUX_ZEROED if sizes["aux"] else 0  # (zeroed by the prologue's scan kernel)
+        ops._launch("gstex_raster_fwd_zero", cam, C, int(tr.settings) | aux_zeroed, ptr(tr._bg_zero), P["records"],
                     P["tile_ranges"], P["tile_order"], P["sorted_ids"], ptr(texture), texture.shape[0],
                     SH_C0, 0.5, P["img"], None, None, P["alpha"], P["tex"], None, P["state"], cap,
                     P["aux"] if sizes["aux"] else None, ptr(sink) if zero_sink else None, zn, P["partials"],

@@ -56,6 +56,10 @@ extern "C" {
  * gradients by a splat-parallel kernel (one splat per lane, lane scans for transmittance and colour behind).  Same
  * results within fp32 rounding; an experiment kept off by default.  Ignored in every other case. */
 #define GSTEX_BWD_SPLIT (1 << 29)
+/* gstex_raster_fwd / gstex_raster_fwd_zero only (ABI 17): the aux span the forward accumulates its unit costs, launch
+ * order and unit-order histogram into was zeroed by gstex_train_prologue (args.raster_aux, same n_isect / tiles /
+ * channels) on the same stream, so the forward skips its own fill.  Set it only after such a prologue call. */
+#define GSTEX_SETTING_AUX_ZEROED (1 << 28)
 
 typedef enum {
     GSTEX_OK = 0,
@@ -456,6 +460,11 @@ typedef struct gstex_train_prologue_args {
     int32_t* tile_order;
     void* bin_workspace;
     size_t bin_workspace_bytes;
+    void* raster_aux;        /* nullable: the raster forward's aux buffer (gstex_raster_aux_bytes(capacity, n_tiles,
+                                raster_channels)), whose accumulated span the prologue zeroes -- pass
+                                GSTEX_SETTING_AUX_ZEROED to the forward that follows */
+    size_t raster_aux_bytes;
+    int32_t raster_channels;
 } gstex_train_prologue_args;
 int gstex_train_prologue(const gstex_train_prologue_args* args, void* stream);
 /* Bytes of scan_workspace gstex_train_prologue needs for n splats (>= gstex_scan_workspace_size(n): the fused

@@ -19,7 +19,7 @@ S = [int(r["Start_Timestamp"]) for r in rows]
 E = [int(r["End_Timestamp"]) for r in rows]
 N = [short(r["Kernel_Name"]) for r in rows]
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-act = [i for i, n in enumerate(N) if "activate_fwd" in n]
+act = [i for i, n in enumerate(N) if "activate_fwd" in n or "train_splat" in n]
 steps = list(zip(act[:-1], act[1:]))
 spans = [(S[b] - S[a]) / 1e3 for a, b in steps]
 first = W
