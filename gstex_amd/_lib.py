@@ -26,7 +26,6 @@ SETTING_DIST_REG = 1 << 10
 SETTING_EDIT = 1 << 13
 SETTING_EVAL_NORMAL = 1 << 15
 SETTING_AUX_ZEROED = 1 << 28  # GSTEX_SETTING_AUX_ZEROED: the prologue zeroed the forward's accumulated aux span
-SETTING_ORDER_READY = 1 << 27  # GSTEX_SETTING_ORDER_READY: the backward's unit order came from gstex_raster_unit_order
 
 
 class GstexCamera(ctypes.Structure):
@@ -149,7 +148,6 @@ SIGNATURES = {
          c_int64, _P, _P, c_int64, _P, c_int64, _P],
     ),
     "gstex_raster_aux_bytes": (c_size_t, [c_int64, c_int32, c_int32]),
-    "gstex_raster_unit_order": (c_int32, [c_int64, c_int32, c_int32, _P, _P]),
     "gstex_unit_order": (c_int32, [c_int32, _P, _P, _P, _P]),
     "gstex_unit_order_scratch_words": (c_size_t, []),
     "gstex_raster_bwd": (

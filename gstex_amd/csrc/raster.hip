@@ -2271,8 +2271,7 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
     const bool split = (settings & GSTEX_BWD_SPLIT) != 0;
-    const bool order_ready = (settings & GSTEX_SETTING_ORDER_READY) != 0;
-    settings &= ~(GSTEX_BWD_SPLIT | GSTEX_SETTING_ORDER_READY);
+    settings &= ~GSTEX_BWD_SPLIT;
     int rc = check_settings(settings);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && state && aux, "gstex_raster_bwd: null pointer (tile_ranges, state and the forward's aux)");
@@ -2289,12 +2288,9 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     const AuxPtrs ap = aux_ptrs(aux, al);
     if (n_isect > 0 && row_flags && hipMemsetAsync(row_flags, 0, (size_t)n_isect * 4, st) != hipSuccess)
         return launch_status("gstex_raster_bwd (row_flags)");
-    // costliest units first, from the histogram the forward built (order entries are unit + 1) -- unless the caller
-    // computed the order already (gstex_raster_unit_order, e.g. on a side stream while the loss ran)
-    if (!order_ready) {
-        rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
-        if (rc) return rc;
-    }
+    // costliest units first, from the histogram the forward built (order entries are unit + 1)
+    rc = unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, st);
+    if (rc) return rc;
     // depth / distortion / normal gradients present?  (the distortion one only counts when enabled)
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
 #define GSTEX_BWD(CC, GG)                                                                                      \
@@ -2319,14 +2315,6 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     else GSTEX_BWD(0, true);
 #undef GSTEX_BWD
     return launch_status("gstex_raster_bwd");
-}
-
-extern "C" int gstex_raster_unit_order(int64_t n_isect, int32_t n_tiles, int32_t channels, void* aux, void* stream) {
-    GSTEX_REQUIRE(aux && n_isect >= 0 && n_isect < (int64_t)INT32_MAX && n_tiles > 0 && channels >= 1 && channels <= 8,
-                  "gstex_raster_unit_order: invalid arguments");
-    const AuxLayout al = aux_layout(n_isect, n_tiles, channels);
-    const AuxPtrs ap = aux_ptrs(aux, al);
-    return unit_order_from_hist((int32_t)al.n_units, ap.cost, ap.order, ap.order_ws, as_stream(stream));
 }
 
 extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels) {

@@ -18,7 +18,6 @@ accumulation, not capturing.  Every other case runs the per-op path unchanged.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -28,18 +27,6 @@ from .charts import SH_C0  # SH2RGB(texture_dc) applied by the raster on read (g
 
 _ALIGN = 256
 _LAYOUTS: dict = {}
-# GSTEX_ORDER_AHEAD=1: the backward's unit launch order (gstex_raster_unit_order: two small kernels that depend only on
-# the raster forward) computed on a side stream right after the forward, overlapping the loss kernels, instead of at
-# the start of the raster backward
-ORDER_AHEAD = os.environ.get("GSTEX_ORDER_AHEAD", "0") != "0"
-_SIDE: dict = {}
-
-
-def _side_stream(dev) -> torch.cuda.Stream:
-    s = _SIDE.get(dev)
-    if s is None:
-        s = _SIDE[dev] = torch.cuda.Stream(dev)
-    return s
 
 
 def _layout(n: int, n_rest: int, capacity: int, H: int, W: int, C: int):
@@ -130,16 +117,6 @@ class _TrainRender(torch.autograd.Function):
                     SH_C0, 0.5, P["img"], None, None, P["alpha"], P["tex"], None, P["state"], cap,
                     P["aux"] if sizes["aux"] else None, ptr(sink) if zero_sink else None, zn, P["partials"],
                     PARTIAL_FLOATS * n, st)
-        ctx.order_ready = None
-        if ORDER_AHEAD and sizes["aux"]:
-            side = _side_stream(dev)
-            fwd_done = _lib.OrderEvent()
-            fwd_done.record(stream=st)
-            fwd_done.wait(stream=side.cuda_stream)
-            _lib.call("gstex_raster_unit_order", cap, sizes["n_tiles"], C, P["aux"], side.cuda_stream)
-            ctx.order_ready = _lib.OrderEvent()
-            ctx.order_ready.record(stream=side.cuda_stream)
-            arena.record_stream(side)  # (the caching allocator keeps the arena until the side stream is past it)
         ctx.tr, ctx.arena, ctx.P, ctx.cam_keep = tr, arena, P, (vm, cw)
         ctx.cam, ctx.cap, ctx.sink, ctx.degree, ctx.goff, ctx.gfloats = cam, cap, sink, int(degree), goff, gfloats
         ctx.has_aux = sizes["aux"] > 0
@@ -160,11 +137,7 @@ class _TrainRender(torch.autograd.Function):
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
         v_img, v_alpha, v_tex = c(v_img), c(v_alpha), c(v_tex)
         texture = tr.texture_dc
-        order = 0
-        if ctx.order_ready is not None:  # the unit order computed on the side stream during the loss
-            ctx.order_ready.wait(stream=st)
-            ctx.order_ready, order = None, _lib.SETTING_ORDER_READY
-        ops._launch("gstex_raster_bwd", cam, 3, int(tr.settings) | (_lib.BWD_SPLIT if ops.BWD_SPLIT else 0) | order,
+        ops._launch("gstex_raster_bwd", cam, 3, int(tr.settings) | (_lib.BWD_SPLIT if ops.BWD_SPLIT else 0),
                     ptr(tr._bg_zero), P["records"], P["tile_ranges"], P["sorted_ids"], P["sorted_slots"],
                     ptr(texture), texture.shape[0], SH_C0, 0.5, P["state"], ptr(v_img), None, None,
                     ptr(v_alpha), ptr(v_tex), None, ctx.cap, P["partials"], None, ptr(ctx.sink),

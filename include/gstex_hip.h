@@ -60,10 +60,6 @@ extern "C" {
  * order and unit-order histogram into was zeroed by gstex_train_prologue (args.raster_aux, same n_isect / tiles /
  * channels) on the same stream, so the forward skips its own fill.  Set it only after such a prologue call. */
 #define GSTEX_SETTING_AUX_ZEROED (1 << 28)
-/* gstex_raster_bwd only (ABI 17): the backward's unit launch order was already computed from this aux by
- * gstex_raster_unit_order, ordered before this call (e.g. on a side stream the caller's stream waited for), so the
- * backward skips that step. */
-#define GSTEX_SETTING_ORDER_READY (1 << 27)
 
 typedef enum {
     GSTEX_OK = 0,
@@ -243,10 +239,6 @@ int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, int32_t set
                           float* zero_buf, int64_t zero_floats, float* zero_buf2, int64_t zero_floats2,
                           void* stream);
 size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels);
-/* The backward's unit launch order from a forward's aux (the step gstex_raster_bwd otherwise starts with; ABI 17):
- * depends only on the forward, so it can run on another stream while the loss is computed.  Pass
- * GSTEX_SETTING_ORDER_READY to the backward after ordering its stream behind this call. */
-int gstex_raster_unit_order(int64_t n_isect, int32_t n_tiles, int32_t channels, void* aux, void* stream);
 /* Launch order of n_units backward units: unit_key = cost (bits 0-23, clamped to 1023) | XCD group (bits 24-26).
  * Units of cost 0 get no position; the others are sorted by descending cost within their group and the groups
  * interleaved (k-th unit of group g at position 8 k + g: round-robin dispatch puts it on XCD g), or, when the

@@ -93,33 +93,3 @@ def test_fused_step_trains_like_per_op(monkeypatch):
         scale = max(float(x.abs().max()), 1e-30)
         d = (x - y).abs()
         assert float(d.max()) <= LRS[name] and float(d.mean()) / scale < 1e-6, name
-
-
-def test_order_ahead_matches(monkeypatch):
-    """GSTEX_ORDER_AHEAD: the backward's unit order computed on a side stream during the loss (gstex_raster_unit_order
-    + GSTEX_SETTING_ORDER_READY) gives the same step as the order computed inside the raster backward."""
-    from gstex_amd import fused
-    from gstex_amd.model import GStexTrainer
-
-    dev, sc, views, gts = _setup()
-    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=True)
-    tr.zero_grad()
-    tr.forward_backward(views[0], gts[0])
-    tr.optimizer_step()
-    tr.wait_texture()
-    for k in range(3):
-        res = {}
-        for mode in (True, False):
-            monkeypatch.setattr(fused, "ORDER_AHEAD", mode)
-            tr.zero_grad()
-            out = tr.forward_backward(views[k], gts[k])
-            torch.cuda.synchronize()
-            res[mode] = (out.loss.clone(), out.rgb.clone(),
-                         {name: ps[0].grad.detach().clone() for name, ps in tr.param_groups().items()
-                          if ps[0].grad is not None})
-        (la, ra, ga), (lb, rb, gb) = res[True], res[False]
-        assert torch.equal(ra, rb) and torch.equal(la, lb)
-        for name in ga:
-            a, b = ga[name].double(), gb[name].double()
-            scale = max(float(b.abs().max()), 1e-30)
-            assert float((a - b).abs().max()) / scale < 1e-4, name
