@@ -11,9 +11,10 @@ tests/test_gpu_fused.py compares both paths.  What it removes is host time betwe
 waits through whenever a step starts on an idle device -- the first step after a synchronisation (bench.py's first
 timed step) -- and four launches.
 
-Taken only where it applies (GStexTrainer._fused_ok): one process's own texel-gradient buffer (defer_texture, no
-GradSync route), a sized PairCapacity, SH degree > 0 without fix_init, no geometry outputs, non-deterministic
-accumulation, not capturing.  Every other case runs the per-op path unchanged.
+Taken only where it applies (GStexTrainer._fused_ok): a texel-gradient sink (defer_texture, or GradSync's flat buffer
+at N > 1: its route, tail-collective callback and late texel update are honoured as in the per-op render), a sized
+PairCapacity, SH degree > 0 without fix_init, no geometry outputs, non-deterministic accumulation, not capturing.
+Every other case runs the per-op path unchanged.
 """
 from __future__ import annotations
 
@@ -78,7 +79,8 @@ def _view(arena: torch.Tensor, off: int, shape) -> torch.Tensor:
 
 class _TrainRender(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, tr, view, degree, sink, zero_sink, means, quats, log_scales, opac_logits, features_rest):
+    def forward(ctx, tr, view, degree, sink, zero_sink, on_grad, texture_ready, means, quats, log_scales, opac_logits,
+                features_rest):
         n = means.shape[0]
         n_rest = features_rest.shape[1]
         H, W, C = int(view.H), int(view.W), 3
@@ -109,6 +111,8 @@ class _TrainRender(torch.autograd.Function):
             raster_aux=P["aux"] if sizes["aux"] else None, raster_aux_bytes=sizes["aux"], raster_channels=C)
         _lib.call("gstex_train_prologue", ctypes.byref(a), st)
         pcap.commit(slot, cap, tr.step, dev)
+        if texture_ready is not None:  # the deferred texel update waiting for its collective: the raster forward
+            texture_ready()            # is the first reader of the texels
         texture = tr.texture_dc
         zn = sink.numel() if zero_sink else 0
         aux_zeroed = _lib.SETTING_AUX_ZEROED if sizes["aux"] else 0  # (zeroed by the prologue's scan kernel)
@@ -119,6 +123,7 @@ class _TrainRender(torch.autograd.Function):
                     PARTIAL_FLOATS * n, st)
         ctx.tr, ctx.arena, ctx.P, ctx.cam_keep = tr, arena, P, (vm, cw)
         ctx.cam, ctx.cap, ctx.sink, ctx.degree, ctx.goff, ctx.gfloats = cam, cap, sink, int(degree), goff, gfloats
+        ctx.on_grad = on_grad
         ctx.has_aux = sizes["aux"] > 0
         ctx.save_for_backward(quats, log_scales)
         ctx.set_materialize_grads(False)
@@ -142,6 +147,8 @@ class _TrainRender(torch.autograd.Function):
                     ptr(texture), texture.shape[0], SH_C0, 0.5, P["state"], ptr(v_img), None, None,
                     ptr(v_alpha), ptr(v_tex), None, ctx.cap, P["partials"], None, ptr(ctx.sink),
                     P["aux"] if ctx.has_aux else None, st)
+        if ctx.on_grad is not None:
+            ctx.on_grad()  # the texel gradient is complete in stream order (GradSync starts its tail collective)
         grads = torch.empty((ctx.gfloats,), device=dev, dtype=torch.float32)
         g = {k: grads.data_ptr() + 4 * v for k, v in ctx.goff.items()}
         means = tr.means
@@ -158,7 +165,7 @@ class _TrainRender(torch.autograd.Function):
 
         def gv(name, shape):
             return _view_f(grads, o[name], shape)
-        return (None, None, None, None, None, gv("means", (n, 3)), gv("quats", (n, 4)), gv("log_scales", (n, 3)),
+        return (None, None, None, None, None, None, None, gv("means", (n, 3)), gv("quats", (n, 4)), gv("log_scales", (n, 3)),
                 gv("opac_logits", (n, 1)), gv("features_rest", (n, n_rest, 3)))
 
 
@@ -169,8 +176,9 @@ def _view_f(flat: torch.Tensor, off: int, shape) -> torch.Tensor:
     return flat[off:off + nf].view(shape)
 
 
-def train_render(tr, view, degree: int, sink: torch.Tensor, zero_sink: bool):
+def train_render(tr, view, degree: int, sink: torch.Tensor, zero_sink: bool, on_grad=None, texture_ready=None):
     """-> (img (H,W,3), alpha (H,W), tex (H,W,3)) of GStexTrainer.render's photometric training branch; the texel
-    gradient accumulates into `sink` (zeroed by the raster forward when zero_sink)."""
-    return _TrainRender.apply(tr, view, degree, sink, zero_sink, tr.means, tr.quats, tr.scales, tr.opacities,
-                              tr.features_rest)
+    gradient accumulates into `sink` (zeroed by the raster forward when zero_sink) and on_grad() runs once the raster
+    backward is enqueued; texture_ready() (a deferred texel update) runs right before the raster forward."""
+    return _TrainRender.apply(tr, view, degree, sink, zero_sink, on_grad, texture_ready, tr.means, tr.quats,
+                              tr.scales, tr.opacities, tr.features_rest)

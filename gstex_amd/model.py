@@ -350,17 +350,23 @@ class GStexTrainer:
         """Whether render() takes gstex_amd.fused's path (see its docstring for why each condition is there)."""
         return (self.fused_step and not composite and not (self.geometry_outputs if geometry is None else geometry)
                 and self.fused_activations and self.sh_degree > 0 and not self.fix_init
-                and self.pairs is not None and self.pairs.capacity > 0 and self.texture_grad_route is None
-                and self.texture_grad_sink is not None and self.texture_grad_ready is None
-                and self._pending_tex is None and torch.is_grad_enabled()
-                and not torch.are_deterministic_algorithms_enabled()
+                and self.pairs is not None and self.pairs.capacity > 0 and self.texture_grad_sink is not None
+                and torch.is_grad_enabled() and not torch.are_deterministic_algorithms_enabled()
                 and not torch.cuda.is_current_stream_capturing())
 
     def _render_fused(self, view: View, deg: int):
         from . import fused
 
+        # the texel-gradient target as in the per-op render: GradSync's route (the flat buffer's slice, or its side
+        # buffer once the tail's collective is on the wire) or the trainer's own sink
+        if self.texture_grad_route is not None:
+            sink, zero_sink, on_grad = self.texture_grad_route(self._sink_fresh)
+        else:
+            sink, zero_sink, on_grad = self.texture_grad_sink, self._sink_fresh, self.texture_grad_ready
+        # a deferred texel update that first waits for its collective (GradSync) runs right before the raster forward
+        late = self._run_pending_texture if self._pending_tex is not None and self._pending_collective else None
         self._poll_pairs()
-        img, alpha, tex = fused.train_render(self, view, deg, self.texture_grad_sink, self._sink_fresh)
+        img, alpha, tex = fused.train_render(self, view, deg, sink, zero_sink, on_grad, late)
         self._sink_fresh = False
         z = ops._zero_scalar(self.device)  # not rendered: read-only zeros without gradient, as the per-op path
         H, W = int(view.H), int(view.W)

@@ -93,3 +93,45 @@ def test_fused_step_trains_like_per_op(monkeypatch):
         scale = max(float(x.abs().max()), 1e-30)
         d = (x - y).abs()
         assert float(d.max()) <= LRS[name] and float(d.mean()) / scale < 1e-6, name
+
+
+def test_fused_step_with_gradsync_trains_like_per_op(monkeypatch):
+    """The fused render under gstex_amd.dist.GradSync (world 1, gloo): the flat buffer's texel slice as the sink, the
+    deferred texel update run right before the raster forward once its collective has landed, the head-first exchange
+    -- trains like the per-op render under the same GradSync."""
+    import socket
+
+    import torch.distributed as dist
+
+    from gstex_amd.dist import GradSync
+    from gstex_amd.model import LRS, GStexTrainer
+
+    calls = _count_fused(monkeypatch)
+    dev, sc, views, gts = _setup()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        trs = [GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=f) for f in (False, True)]
+        syncs = [GradSync(tr, 1) for tr in trs]
+        for step in range(5):
+            for tr, sy in zip(trs, syncs):
+                sy.zero()
+                tr.forward_backward(views[step % 3], gts[step % 3])
+                tr.optimizer_step(sync=sy)
+        assert calls[0] == 4
+        a, b = trs
+        for (name, pa), pb in zip(a.param_groups().items(), b.param_groups().values()):
+            x, y = pa[0].detach().double(), pb[0].detach().double()
+            if name == "texture_dc":
+                x, y = a.texels().double(), b.texels().double()
+            scale = max(float(x.abs().max()), 1e-30)
+            d = (x - y).abs()
+            assert float(d.max()) <= LRS[name] and float(d.mean()) / scale < 1e-6, name
+    finally:
+        if own:
+            dist.destroy_process_group()
