@@ -210,10 +210,12 @@ def test_texture_sample_identity_on_same_charts():
     log_scales = torch.log(10 ** (-2.5 + 1.5 * torch.rand((50, 3), generator=torch.Generator().manual_seed(2))))
     dims, _, _ = build_charts(log_scales, 3000)
     T = int((dims[:, 0] * dims[:, 1]).sum())
-    tex = torch.rand(T, 3)
+    tex = torch.rand(T, 3, generator=torch.Generator().manual_seed(3))
     ids, uv = texture_dims_to_query(dims)
     out = O.texture_sample(dims[ids], tex, uv)
-    assert torch.allclose(out, tex, atol=1e-6), "resampling onto identical charts must be the identity"
+    # texel centres come back up to the fp32 rounding of uv * h - 0.5 (|err| <= h * 2^-24 per coordinate, h <= 256
+    # here): a bilinear weight of that size on the neighbour
+    assert torch.allclose(out, tex, atol=2e-5), "resampling onto identical charts must be the identity"
 
 
 def test_sh_low_orders():
