@@ -21,6 +21,7 @@
 #include "gstex_common.h"
 #include "gstex_error.h"
 #include "gstex_internal.h"
+#include "splat_math.h"  // splat_record
 
 using namespace gstex;
 
@@ -153,45 +154,10 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
     if (nth[g] <= 0) return;
-    // the record is evaluated in fp64 and rounded once per value (one thread per splat, ~100 fp64 operations): its
-    // fp32 evaluation was the dominant error of the means / quats gradients (tools/grad_precision.py)
-    const FrameT<double> fr = quat_frame_t<double>(quats + 4 * g);
-    const double su = (double)scales[3 * g] * (double)glob, sv = (double)scales[3 * g + 1] * (double)glob;
-    const d3 mu = d3{(double)means[3 * g], (double)means[3 * g + 1], (double)means[3 * g + 2]};
-    const AnchoredT<double> h = splat_anchored(cam, mu, su, sv, fr);
-    const d3 dir = d3{(double)cam.campos[0] - mu.x, (double)cam.campos[1] - mu.y, (double)cam.campos[2] - mu.z};
-    const double sgn = dot3(fr.tw, dir) < 0.0 ? -1.0 : 1.0;
-    const d3 um = d3{(double)umap[3 * g], (double)umap[3 * g + 1], (double)umap[3 * g + 2]};
-    const d3 vm = d3{(double)vmap[3 * g], (double)vmap[3 * g + 1], (double)vmap[3 * g + 2]};
-    float r[GSTEX_REC_FLOATS];
-    const AffineHomogT<double> ah = affine_homog(h.Tu, h.Tv, h.Tw);
-    r[R_A + 0] = (float)ah.A.x; r[R_A + 1] = (float)ah.A.y; r[R_A + 2] = (float)ah.A.z;
-    r[R_B + 0] = (float)ah.B.x; r[R_B + 1] = (float)ah.B.y; r[R_B + 2] = (float)ah.B.z;
-    r[R_PZ] = (float)ah.Pz;
-    r[R_TW + 0] = (float)h.Tw.x; r[R_TW + 1] = (float)h.Tw.y; r[R_TW + 2] = (float)h.Tw.z;
-    r[R_XY + 0] = centers[2 * g]; r[R_XY + 1] = centers[2 * g + 1];
-    r[R_OPAC] = opacities[g];
-    r[R_RGB + 0] = rgbs[3 * g]; r[R_RGB + 1] = rgbs[3 * g + 1]; r[R_RGB + 2] = rgbs[3 * g + 2];
-    r[R_NRM + 0] = (float)(sgn * fr.tw.x); r[R_NRM + 1] = (float)(sgn * fr.tw.y); r[R_NRM + 2] = (float)(sgn * fr.tw.z);
-    // the texture affine in texel units: the sample point (tu h, tv w) = (tu0 + auu u + auv v) h, ... is read as
-    // fma(u, auu h, fma(v, auv h, tu0 h)) -- two fused multiply-adds per coordinate instead of three operations
-    const double hd = (double)tdims[3 * g], wd = (double)tdims[3 * g + 1];
-    r[R_TU0] = (float)((double)uv0[2 * g] * hd);
-    r[R_AUU] = (float)(su * dot3(fr.tu, um) * hd);
-    r[R_AUV] = (float)(sv * dot3(fr.tv, um) * hd);
-    r[R_TV0] = (float)((double)uv0[2 * g + 1] * wd);
-    r[R_AVU] = (float)(su * dot3(fr.tu, vm) * wd);
-    r[R_AVV] = (float)(sv * dot3(fr.tv, vm) * wd);
-    r[R_H] = __int_as_float(tdims[3 * g]);
-    r[R_W] = __int_as_float(tdims[3 * g + 1]);
-    r[R_OFF] = __int_as_float(tdims[3 * g + 2]);
-    r[R_XA] = (float)h.xa;
-    r[R_YA] = (float)h.ya;
-    r[R_HM1] = (float)(tdims[3 * g] - 1);
-    r[R_WM1] = (float)(tdims[3 * g + 1] - 1);
-    float4* dst = reinterpret_cast<float4*>(rec_out) + (size_t)g * kRecF4;
-#pragma unroll
-    for (int k = 0; k < kRecF4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+    // the record, in fp64 (splat_math.h: the function the training prologue's fused kernel also calls)
+    splat_record(cam, means[3 * g], means[3 * g + 1], means[3 * g + 2], scales[3 * g], scales[3 * g + 1], glob,
+                 quats + 4 * g, rgbs + 3 * g, opacities[g], centers[2 * g], centers[2 * g + 1], uv0 + 2 * g,
+                 umap + 3 * g, vmap + 3 * g, tdims + 3 * g, rec_out + (size_t)g * GSTEX_REC_FLOATS);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -98,6 +98,53 @@ __device__ __forceinline__ Preprocessed preprocess_splat(const Camera& cam, f3 m
     return p;
 }
 
+// ---- the splat's raster record (raster.hip setup_kernel, gstex_raster_setup) ---------------------------------------
+// Evaluated in fp64 and rounded once per value (one thread per splat, ~100 fp64 operations): its fp32 evaluation was
+// the dominant error of the means / quats gradients (tools/grad_precision.py).  Inputs are the splat's
+// fp32 values (the activated scales / quaternion, its colour, opacity, AABB centre, UV frame and texel block dims).
+__device__ __forceinline__ void splat_record(const Camera& cam, float mx, float my, float mz, float s0, float s1,
+                                             float glob, const float* q4, const float* rgb, float opac, float cx,
+                                             float cy, const float* uv0, const float* um3, const float* vm3,
+                                             const int32_t* td, float* __restrict__ rec_out) {
+    const FrameT<double> fr = quat_frame_t<double>(q4);
+    const double su = (double)s0 * (double)glob, sv = (double)s1 * (double)glob;
+    const d3 mu = d3{(double)mx, (double)my, (double)mz};
+    const AnchoredT<double> h = splat_anchored(cam, mu, su, sv, fr);
+    const d3 dir = d3{(double)cam.campos[0] - mu.x, (double)cam.campos[1] - mu.y, (double)cam.campos[2] - mu.z};
+    const double sgn = dot3(fr.tw, dir) < 0.0 ? -1.0 : 1.0;
+    const d3 um = d3{(double)um3[0], (double)um3[1], (double)um3[2]};
+    const d3 vm = d3{(double)vm3[0], (double)vm3[1], (double)vm3[2]};
+    float r[GSTEX_REC_FLOATS];
+    const AffineHomogT<double> ah = affine_homog(h.Tu, h.Tv, h.Tw);
+    r[R_A + 0] = (float)ah.A.x; r[R_A + 1] = (float)ah.A.y; r[R_A + 2] = (float)ah.A.z;
+    r[R_B + 0] = (float)ah.B.x; r[R_B + 1] = (float)ah.B.y; r[R_B + 2] = (float)ah.B.z;
+    r[R_PZ] = (float)ah.Pz;
+    r[R_TW + 0] = (float)h.Tw.x; r[R_TW + 1] = (float)h.Tw.y; r[R_TW + 2] = (float)h.Tw.z;
+    r[R_XY + 0] = cx; r[R_XY + 1] = cy;
+    r[R_OPAC] = opac;
+    r[R_RGB + 0] = rgb[0]; r[R_RGB + 1] = rgb[1]; r[R_RGB + 2] = rgb[2];
+    r[R_NRM + 0] = (float)(sgn * fr.tw.x); r[R_NRM + 1] = (float)(sgn * fr.tw.y); r[R_NRM + 2] = (float)(sgn * fr.tw.z);
+    // the texture affine in texel units: the sample point (tu h, tv w) = (tu0 + auu u + auv v) h, ... is read as
+    // fma(u, auu h, fma(v, auv h, tu0 h)) -- two fused multiply-adds per coordinate instead of three operations
+    const double hd = (double)td[0], wd = (double)td[1];
+    r[R_TU0] = (float)((double)uv0[0] * hd);
+    r[R_AUU] = (float)(su * dot3(fr.tu, um) * hd);
+    r[R_AUV] = (float)(sv * dot3(fr.tv, um) * hd);
+    r[R_TV0] = (float)((double)uv0[1] * wd);
+    r[R_AVU] = (float)(su * dot3(fr.tu, vm) * wd);
+    r[R_AVV] = (float)(sv * dot3(fr.tv, vm) * wd);
+    r[R_H] = __int_as_float(td[0]);
+    r[R_W] = __int_as_float(td[1]);
+    r[R_OFF] = __int_as_float(td[2]);
+    r[R_XA] = (float)h.xa;
+    r[R_YA] = (float)h.ya;
+    r[R_HM1] = (float)(td[0] - 1);
+    r[R_WM1] = (float)(td[1] - 1);
+    float4* dst = reinterpret_cast<float4*>(rec_out);
+#pragma unroll
+    for (int k = 0; k < GSTEX_REC_FLOATS / 4; ++k) dst[k] = make_float4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+}
+
 // ---- SH colour of the gsplat-0.1 lineage, degree <= 4 (see sh_texture.hip) -----------------------------------------
 namespace {
 constexpr float SH_C0 = 0.28209479177387814f;

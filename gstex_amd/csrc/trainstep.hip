@@ -3,16 +3,17 @@
 //
 // Per-op sequence (gstex_amd's per-op path): activate_fwd, preprocess, sh_rest_fwd (one thread per splat each), the
 // guarded offsets scan (three launches: block sums, scan of the sums, final), raster_setup, bin_sort_capped.  Here:
-//   train_splat_kernel  one thread per splat runs activate_splat -> preprocess_splat -> sh_colour (splat_math.h, the
-//                       functions the per-op kernels call, on the same fp32 values: bit-identical outputs) and writes
-//                       every per-op output, plus the tile-count sum of its 128-splat block;
+//   train_splat_kernel  one thread per splat runs activate_splat -> preprocess_splat -> sh_colour -> splat_record
+//                       (splat_math.h, the functions the per-op kernels call, on the same fp32 values: bit-identical
+//                       outputs) and writes every per-op output incl. the raster record, plus the tile-count sum of
+//                       its 128-splat block;
 //   train_scan_kernel   the offsets scan in one launch: each 1024-splat scan tile starts from the sum of the block
 //                       sums before it (8 per tile; at most n / 128 L2-resident words), then scans its tile as
 //                       binning.hip's scan_final_kernel does (same integers, same guard);
 //                       its grid also zeroes the binning's tile counters and the raster forward's accumulated aux span
 //                       (args.raster_aux), so neither needs its fill launch (GSTEX_SETTING_AUX_ZEROED);
-// then gstex_raster_setup and the capped binning.  Six launches fewer and no host time between the launches (the
-// device waits through that whenever a step starts on an idle device, after a synchronisation).
+// then the capped binning.  Seven launches fewer and no host time between the launches (the device waits through that
+// whenever a step starts on an idle device, after a synchronisation).
 #include "gstex_common.h"
 #include "gstex_error.h"
 #include "gstex_internal.h"
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
     float* __restrict__ opacities, float* __restrict__ uv0, float* __restrict__ umap, float* __restrict__ vmap,
     float* __restrict__ viewdirs, float* __restrict__ depths, float* __restrict__ centers,
     float* __restrict__ extents, int32_t* __restrict__ nth, float* __restrict__ rgbs,
-    int32_t* __restrict__ block_sums) {
+    const int32_t* __restrict__ tdims, float* __restrict__ records, int32_t* __restrict__ block_sums) {
     extern __shared__ float s_c[];
     __shared__ int s_wave[kSplatBlock / 64];
     const Camera cam = load_camera(cam_args);
@@ -68,6 +69,13 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
         rgbs[3 * i] = r0;
         rgbs[3 * i + 1] = r1;
         rgbs[3 * i + 2] = r2;
+        if (p.nth > 0) {  // the raster record of a splat that hits a tile (as setup_kernel)
+            const float rgb[3] = {r0, r1, r2};
+            const float uv[2] = {0.5f, 0.5f};
+            const int32_t td[3] = {tdims[3 * i], tdims[3 * i + 1], tdims[3 * i + 2]};
+            splat_record(cam, mx, my, mz, a.s0, a.s1, 1.0f, a.q, rgb, a.opacity, p.cx, p.cy, uv, a.um, a.vm, td,
+                         records + (size_t)i * GSTEX_REC_FLOATS);
+        }
     }
     int total;
     block_excl_scan<kSplatBlock>(count, s_wave, &total);
@@ -147,7 +155,7 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
         GSTEX_REQUIRE(a->means && a->quats && a->log_scales && a->opac_logits && a->mappings && a->campos &&
                           a->features_rest && a->quats_n && a->scales && a->opacities && a->uv0 && a->umap &&
                           a->vmap && a->viewdirs && a->depths && a->centers && a->extents && a->num_tiles_hit &&
-                          a->rgbs && a->offsets,
+                          a->rgbs && a->offsets && a->texture_dims && a->records && a->cam.viewmat,
                       "gstex_train_prologue: null pointer");
         GSTEX_REQUIRE(((reinterpret_cast<uintptr_t>(a->quats) | reinterpret_cast<uintptr_t>(a->quats_n)) & 15) == 0,
                       "gstex_train_prologue: quaternions must be 16-byte aligned");
@@ -157,9 +165,9 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
         train_splat_kernel<<<div_up(a->n, kSplatBlock), kSplatBlock,
                              (size_t)kSplatBlock * a->n_rest * 3 * sizeof(float), st>>>(
             a->n, a->sh_degree, a->n_rest, a->means, a->quats, a->log_scales, a->opac_logits, a->mappings,
-            a->map_cols, a->campos, a->features_rest, to_device_camera(pre), tx, ty, pre.block, a->quats_n,
+            a->map_cols, a->campos, a->features_rest, to_device_camera(a->cam), tx, ty, pre.block, a->quats_n,
             a->scales, a->opacities, a->uv0, a->umap, a->vmap, a->viewdirs, a->depths, a->centers, a->extents,
-            a->num_tiles_hit, a->rgbs, sums);
+            a->num_tiles_hit, a->rgbs, a->texture_dims, a->records, sums);
         const ScanGuard g{(long long)a->guard.capacity, a->guard.step_flag, a->guard.host_count,
                           a->guard.first ? 1 : 0};
         const ZeroSpan zb = bin_count_span(a->bin_workspace, tx * ty, a->capacity);
@@ -192,9 +200,11 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
         }
     }
     if (rc) return rc;
-    rc = gstex_raster_setup(a->n, a->means, a->scales, 1.0f, a->quats_n, a->rgbs, a->opacities, a->centers, a->uv0,
-                            a->umap, a->vmap, a->texture_dims, a->num_tiles_hit, &a->cam, a->records, stream);
-    if (rc) return rc;
+    if (!fused) {  // (the fused kernel wrote the records)
+        rc = gstex_raster_setup(a->n, a->means, a->scales, 1.0f, a->quats_n, a->rgbs, a->opacities, a->centers, a->uv0,
+                                a->umap, a->vmap, a->texture_dims, a->num_tiles_hit, &a->cam, a->records, stream);
+        if (rc) return rc;
+    }
     if (fused)  // the tile counters were zeroed by train_scan_kernel
         return bin_sort_capped_prezeroed(a->n, a->capacity, a->centers, a->extents, a->depths, a->offsets, a->cam.H,
                                          a->cam.W, a->cam.block, a->tile_ranges, a->sorted_ids, a->sorted_slots,
