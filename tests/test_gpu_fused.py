@@ -33,15 +33,17 @@ def _count_fused(monkeypatch):
     return calls
 
 
-@pytest.mark.parametrize("n,texels", [(4000, 80_000), (1500, 30_000), (300, 6_000)])
-def test_fused_render_matches_per_op(monkeypatch, n, texels):
+@pytest.mark.parametrize("n,texels,start", [(4000, 80_000, 3000), (1500, 30_000, 3000), (300, 6_000, 3000),
+                                             (4000, 80_000, 1500), (4000, 80_000, 0)])
+def test_fused_render_matches_per_op(monkeypatch, n, texels, start):
     """n = 4000: several scan tiles with a partial last one; 1500: one full tile and a partial one; 300: a single
-    partial 128-splat block of the fused preprocessing kernel and a single scan tile."""
+    partial block of the fused preprocessing kernel and a single scan tile.  start 1500: SH degree 1 of the ramp;
+    start 0: degree 0, which gstex_train_prologue runs through the per-op entry points."""
     from gstex_amd.model import GStexTrainer
 
     calls = _count_fused(monkeypatch)
     dev, sc, views, gts = _setup(n, texels)
-    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True, fused_step=True)
+    tr = GStexTrainer(sc, dev, start_step=start, defer_texture=True, fused_step=True)
     # the first render sizes the pair capacity (one read-back) through the per-op path
     tr.zero_grad()
     tr.forward_backward(views[0], gts[0])
