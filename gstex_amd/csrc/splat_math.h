@@ -261,7 +261,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
 // Pair-capacity guard (gstex_scan_offsets_guarded, ABI 13), applied by the thread that writes the total out[n]: the
 // step's overflow flag (1.0f when the total exceeds the pair buffers' capacity; the first render of a step writes it,
 // later ones OR into it) and, when given, the total in device-writable host memory (no copy, no synchronisation:
-// the host reads it once the stream has passed this kernel).  Plain vector stores.
+// the host polls the word, which it set to a sentinel before the launch).  Plain vector stores.
 struct ScanGuard {
     long long capacity;
     float* flag;
@@ -273,7 +273,10 @@ __device__ __forceinline__ void apply_guard(const ScanGuard& g, int total) {
         const float over = (long long)total > g.capacity ? 1.0f : 0.0f;
         *g.flag = g.first ? over : fmaxf(*g.flag, over);
     }
-    if (g.host_count) *g.host_count = total;
+    if (g.host_count) {
+        *g.host_count = total;
+        __threadfence_system();  // the host polls this word (ops.PairCapacity): no event marks the scan's end
+    }
 }
 
 }  // namespace gstex

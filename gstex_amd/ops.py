@@ -350,14 +350,18 @@ class PairCapacity:
 
     Every render's scan writes its pair total on the device (gstex_scan_offsets_guarded): into the step's guard flag
     (1.0 when the total exceeds the capacity; the binning then leaves every tile empty and the guarded Adam skips the
-    step's update, gstex_adam_step_guarded) and into one of RING device-writable host words, which the host reads
-    only after the stream has passed that scan (an event query; no copy, no synchronisation).  The capacity starts
-    from one read-back of the first render's total (headroom x total + slack) and grows when a total comes back
-    above grow_at of it, so an overflow needs a jump of more than 1 / grow_at in the total within the few renders the
-    host runs ahead; one that happens anyway skips that step's update (parameters and moments untouched, the step
-    counters still advance, identically on every rank) and is recorded in `overflows`."""
+    step's update, gstex_adam_step_guarded) and into one of RING device-writable host words, followed by a
+    system-scope fence.  The host sets a slot's word to SENTINEL before the render is enqueued and reads the total once
+    the word has changed -- no event in the stream (a recorded event cost ~5 us of device time per render), no copy, no
+    synchronisation.  The capacity starts from one read-back of the first render's total (headroom x total + slack)
+    and grows when a total comes back above grow_at of it, so an overflow needs a jump of more than 1 / grow_at in the
+    total within the few renders the host runs ahead; one that happens anyway skips that step's update (parameters
+    and moments untouched, the step counters still advance, identically on every rank) and is recorded in
+    `overflows`."""
 
     RING = 8
+    SENTINEL = -(1 << 31)  # (a pair total is >= 0)
+    WAIT_S = 10.0  # a slot still unwritten after this long: the stream is synchronised once, then the word must be set
 
     def __init__(self, device, capacity: int = 0, headroom: float = 1.5, slack: int = 1 << 16, grow_at: float = 0.8):
         self.device = torch.device(device)
@@ -367,7 +371,7 @@ class PairCapacity:
         call("gstex_host_words_alloc", self.RING, ctypes.byref(h), ctypes.byref(d))
         self._host_ptr, self._dev_ptr = h.value, d.value
         self._words = (ctypes.c_int32 * self.RING).from_address(self._host_ptr)
-        self._events = [None] * self.RING
+        self._pending = [False] * self.RING
         self._caps = [0] * self.RING
         self._tags = [None] * self.RING
         self._k = 0
@@ -379,9 +383,8 @@ class PairCapacity:
     def __del__(self):
         try:
             if self._host_ptr:
-                for ev in self._events:
-                    if ev is not None:
-                        ev.synchronize()
+                if any(self._pending):  # a scan may still write its word
+                    torch.cuda.synchronize(self.device)
                 _lib.load().gstex_host_words_free(self._host_ptr)
                 self._host_ptr = None
         except Exception:  # noqa: BLE001  (interpreter shutdown)
@@ -389,7 +392,7 @@ class PairCapacity:
 
     def _absorb(self, k):
         total = int(self._words[k])
-        self._events[k] = None
+        self._pending[k] = False
         self.last_total = total
         self.max_total = max(self.max_total, total)
         if total > self._caps[k]:
@@ -397,12 +400,22 @@ class PairCapacity:
         if total > self.grow_at * self.capacity:
             self.capacity = max(self.capacity, int(self.headroom * total) + self.slack)
 
+    def _wait(self, k):
+        """Spin until slot k's scan has written its word (the host is RING renders ahead, or the first render)."""
+        t0 = time.perf_counter()
+        while self._words[k] == self.SENTINEL:
+            if time.perf_counter() - t0 > self.WAIT_S:
+                torch.cuda.synchronize(self.device)
+                if self._words[k] == self.SENTINEL:
+                    raise RuntimeError("PairCapacity: a finished scan did not report its pair total")
+                break
+        self._absorb(k)
+
     def poll(self):
-        """Read the totals of the renders the stream has passed (non-blocking); returns the number of overflows."""
+        """Read the totals of the renders the device has scanned (non-blocking); returns the number of overflows."""
         before = len(self.overflows)
         for k in range(self.RING):
-            ev = self._events[k]
-            if ev is not None and ev.query():
+            if self._pending[k] and self._words[k] != self.SENTINEL:
                 self._absorb(k)
         return len(self.overflows) - before
 
@@ -412,7 +425,7 @@ class PairCapacity:
         if torch.cuda.is_current_stream_capturing():
             # a step being captured into a hipGraph (gstex_amd.graphs.StepGraphs): the current capacity, and the total
             # written into the graph's own host word (graph_word, a device pointer), which the graph's owner reads
-            # between replays -- no ring slot, no event, no wait
+            # between replays -- no ring slot, no wait
             if self.capacity <= 0 or self.graph_word is None:
                 raise RuntimeError("PairCapacity.scan: capturing needs a sized capacity (one eager render first) and a "
                                    "graph_word")
@@ -437,23 +450,19 @@ class PairCapacity:
         if sized and self.capacity <= 0:
             raise RuntimeError("PairCapacity.reserve: no capacity yet (the first render sizes it through scan())")
         k = self._k % self.RING
-        if self._events[k] is not None:  # the host is RING renders ahead: wait for that one (normally long done)
-            self._events[k].synchronize()
-            self._absorb(k)
+        if self._pending[k]:  # the host is RING renders ahead: wait for that one (normally long done)
+            self._wait(k)
         self._k += 1
         cap = (1 << 62) if self.capacity <= 0 else self.capacity
+        self._words[k] = self.SENTINEL  # (stored before the scan is enqueued; the scan overwrites it)
+        self._pending[k], self._caps[k], self._tags[k] = True, cap, tag
         return _lib.GstexPairGuard(cap, ptr(step_flag), self._dev_ptr + 4 * k, 1 if first else 0), k, cap
 
     def commit(self, k: int, cap: int, tag, device) -> int:
-        """Record slot k's event after its scan (on the current stream); the first render reads its total back and
-        sizes the capacity.  -> the capacity."""
-        first_use = self.capacity <= 0
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
-        self._events[k], self._caps[k], self._tags[k] = ev, cap, tag
-        if first_use:  # the one read-back: the first render sizes the capacity
-            ev.synchronize()
-            self._absorb(k)
+        """After slot k's scan has been enqueued: the first render reads its total back and sizes the capacity.
+        -> the capacity."""
+        if self.capacity <= 0:  # the one read-back: the first render sizes the capacity
+            self._wait(k)
             self.capacity = max(self.capacity, int(self.headroom * self.last_total) + self.slack)
         return self.capacity
 
