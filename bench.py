@@ -75,8 +75,6 @@ def parse():
                    help="run the texel Adam update inside optimizer_step instead of deferring it into the next "
                         "step's render (GStexTrainer defer_texture)")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
-    p.add_argument("--kernel-timing-every", type=int, default=4,
-                   help="N = 1: time the raster backward on every k-th timed step (first included) for the roofline")
     p.add_argument("--graph", choices=("first", "all", "none"), default="none",
                    help="N = 1 hipGraph steps (gstex_amd.graphs.StepGraphs): 'first' replays the first timed step, "
                         "the one that starts on an idle device after the pre-region synchronisation, and enqueues the "
@@ -365,11 +363,7 @@ def main():
     # The host-side preparation (event creation: ~K hipEventCreate calls) happens here, while the device still runs
     # the warmup's last steps, not after the synchronisation, where the idle device would drop its clock before the
     # timed region
-    # at N = 1 the dominant kernel is timed on every kernel_timing_every-th step of the timed region (its first
-    # included): the event pair's two markers cost ~9 us of device time per timed launch (A/B, round 5); at N > 1 every
-    # step's forward and backward are timed (the exchange record needs each step's)
-    timing_every = max(1, args.kernel_timing_every) if world == 1 else 1
-    ops.set_kernel_timing(not args.no_kernel_timing, names=timed, every=timing_every)
+    ops.set_kernel_timing(not args.no_kernel_timing, names=timed)
     if sync is not None and not args.no_kernel_timing:
         sync.phase_events = {}  # when the head / tail collectives land, on rank 0's compute stream
     bound = [_lib.TimingEvent() for _ in range(args.steps + 1)]  # fence-free timing events (`value` is the wall clock)
@@ -568,9 +562,6 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "kernel_ms": {k.replace("gstex_", ""): round(v, 4) for k, v in avg.items()},
-        "kernel_timing": {"every": timing_every, "launches": {k.replace("gstex_", ""): len(v) for k, v in kt.items()},
-                          "note": "raster_bwd: HIP events on every `every`-th timed step (first included); "
-                                  "raster_fwd at N = 1: six untimed steps after the timed region"},
         "kernel_ms_median": {k.replace("gstex_", ""): round(v, 4) for k, v in med.items()},
         "counts": {k: int(ab[k]) for k in ("N_v", "I", "T_v", "P")},
         "sub": sub,

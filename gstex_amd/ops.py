@@ -32,19 +32,12 @@ _TIMED_DEFAULT = ("gstex_raster_fwd", "gstex_raster_bwd")  # the roofline kernel
 _TIMED = set(_TIMED_DEFAULT)
 
 
-_TIMING_EVERY = 1
-_TIMING_COUNT: dict = {}
-
-
-def set_kernel_timing(enabled: bool, names=None, every: int = 1) -> None:
+def set_kernel_timing(enabled: bool, names=None) -> None:
     """Record a HIP event pair around the raster forward / backward launches (or the C-ABI entry points in
-    `names`) on the stream they run on (bench.py / profiling only); every > 1: around the first launch of each name
-    and every `every`-th after it (each recorded event is a marker the device stops at, ~4.6 us)."""
-    global _TIMING, _TIMED, _TIMING_EVERY, _TIMING_COUNT
+    `names`) on the stream they run on (bench.py / profiling only)."""
+    global _TIMING, _TIMED
     _TIMING = {} if enabled else None
     _TIMED = set(names) if names is not None else set(_TIMED_DEFAULT)
-    _TIMING_EVERY = max(1, int(every))
-    _TIMING_COUNT = {}
 
 
 def kernel_times() -> dict:
@@ -82,11 +75,6 @@ def _launch(name: str, *args) -> None:
         _CAPTURE_TIMING.append((key, a, b))
         return
     if _TIMING is None or key not in _TIMED or torch.cuda.is_current_stream_capturing():
-        call(name, *args)
-        return
-    c = _TIMING_COUNT.get(key, 0)
-    _TIMING_COUNT[key] = c + 1
-    if c % _TIMING_EVERY:
         call(name, *args)
         return
     # fence-free timing events (_lib.TimingEvent): a default event pair around each launch cost ~10 us of device time
