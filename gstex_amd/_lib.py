@@ -90,6 +90,15 @@ class GstexTrainPrologueArgs(ctypes.Structure):
         ("raster_channels", c_int32)]
 
 
+class GstexTrainEpilogueArgs(ctypes.Structure):
+    """gstex_train_epilogue_args (ABI 17): the training render's backward after the raster backward."""
+    _fields_ = [("n", c_int32), ("sh_degree", c_int32), ("n_rest", c_int32), ("cam", GstexCamera)] + [
+        (name, c_void_p) for name in (
+            "means", "scales", "quats_n", "quats", "log_scales", "opacities", "umap", "vmap", "viewdirs",
+            "num_tiles_hit", "offsets", "partials", "v_means", "v_quats", "v_log_scales", "v_opac_logits",
+            "v_features_rest", "v_scales_act", "v_quats_n", "v_rgbs", "v_opacities_act", "v_centers", "v_uv0")]
+
+
 ADAM_ZERO_GRAD = 1  # GSTEX_ADAM_ZERO_GRAD
 ADAM_GRID_SHIFT = 8  # GSTEX_ADAM_GRID_SHIFT
 _P = c_void_p
@@ -187,6 +196,7 @@ SIGNATURES = {
                                           c_float, _P, _P]),
     "gstex_train_prologue": (c_int32, [POINTER(GstexTrainPrologueArgs), _P]),
     "gstex_train_prologue_scan_bytes": (c_size_t, [c_int32]),
+    "gstex_train_epilogue": (c_int32, [POINTER(GstexTrainEpilogueArgs), _P]),
     "gstex_adam_step_scheduled": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double,
                                             c_int32, c_float, _P, POINTER(GstexAdamSchedule), _P]),
 }

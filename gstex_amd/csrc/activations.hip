@@ -44,27 +44,21 @@ __global__ __launch_bounds__(256) void activate_bwd_kernel(
     float* __restrict__ v_opac_logits) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    if (v_quats) {
-        const float4 q = reinterpret_cast<const float4*>(quats)[i];
-        const float nq = norm4(q.x, q.y, q.z, q.w);
-        const float w = q.x / nq, x = q.y / nq, y = q.z / nq, z = q.w / nq;
-        const float4 g = v_quats_n ? reinterpret_cast<const float4*>(v_quats_n)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float d = ((w * g.x + x * g.y) + y * g.z) + z * g.w;
-        reinterpret_cast<float4*>(v_quats)[i] =
-            make_float4((g.x - w * d) / nq, (g.y - x * d) / nq, (g.z - y * d) / nq, (g.w - z * d) / nq);
-    }
+    const float4 g = v_quats_n ? reinterpret_cast<const float4*>(v_quats_n)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float gs0 = v_scales ? v_scales[3 * i] : 0.f, gs1 = v_scales ? v_scales[3 * i + 1] : 0.f;
+    const float go = v_opacities ? v_opacities[i] : 0.f;
+    float4 vq;
+    float vls0, vls1, vo;
+    // (the function evaluates all three; a null output skips its loads' use only)
+    activate_bwd_splat(reinterpret_cast<const float4*>(quats)[i], log_scales[3 * i], log_scales[3 * i + 1],
+                       opacities[i], g, gs0, gs1, go, vq, vls0, vls1, vo);
+    if (v_quats) reinterpret_cast<float4*>(v_quats)[i] = vq;
     if (v_log_scales) {
-        const float e0 = expf(log_scales[3 * i]), e1 = expf(log_scales[3 * i + 1]);
-        const float g0 = v_scales ? v_scales[3 * i] : 0.f, g1 = v_scales ? v_scales[3 * i + 1] : 0.f;
-        v_log_scales[3 * i] = (e0 >= 1e-9f) ? g0 * e0 : 0.0f;
-        v_log_scales[3 * i + 1] = (e1 >= 1e-9f) ? g1 * e1 : 0.0f;
+        v_log_scales[3 * i] = vls0;
+        v_log_scales[3 * i + 1] = vls1;
         v_log_scales[3 * i + 2] = 0.0f;  // the third axis is 1e-5 * mean(...).detach()
     }
-    if (v_opac_logits) {
-        const float o = opacities[i];
-        const float g = v_opacities ? v_opacities[i] : 0.f;
-        v_opac_logits[i] = g * ((1.0f - o) * o);
-    }
+    if (v_opac_logits) v_opac_logits[i] = vo;
 }
 
 }  // namespace

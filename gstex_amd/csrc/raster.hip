@@ -2116,6 +2116,60 @@ int check_settings(int settings) {
     return GSTEX_OK;
 }
 
+// The training render's backward after the raster backward, one thread per splat (gstex_train_epilogue, ABI 17): the
+// record chain of setup_bwd_chain_kernel<true> (fast mode: the per-splat accumulator rows), then the activations'
+// backward (activate_bwd_splat) and the SH rest coefficients' backward (sh_grad_row, the rows staged in LDS and copied
+// out contiguously) on the chain's outputs -- the functions gstex_raster_setup_bwd_aabb, gstex_activate_bwd and
+// gstex_sh_rest_bwd run, on the same values: bit-identical gradients, two launches fewer.
+constexpr int kEpiBlock = 256;
+__global__ __launch_bounds__(kEpiBlock) void train_epilogue_kernel(
+    int n, int degree, int n_rest, CamArgs cam_args, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ quats_n, const float* __restrict__ quats, const float* __restrict__ log_scales,
+    const float* __restrict__ opacities, const float* __restrict__ umap, const float* __restrict__ vmap,
+    const float* __restrict__ viewdirs, const int32_t* __restrict__ nth, const float* __restrict__ partials,
+    float* __restrict__ v_means, float* __restrict__ v_quats, float* __restrict__ v_log_scales,
+    float* __restrict__ v_opac_logits, float* __restrict__ v_rest, float* __restrict__ v_scales_act,
+    float* __restrict__ v_quats_n, float* __restrict__ v_rgbs, float* __restrict__ v_opac_act,
+    float* __restrict__ v_centers, float* __restrict__ v_uv0) {
+    extern __shared__ float s_row[];
+    const int t = threadIdx.x;
+    const int i0 = blockIdx.x * kEpiBlock;
+    const int cnt_blk = min(kEpiBlock, n - i0);
+    const int kw = n_rest * 3;
+    if (t < cnt_blk) {
+        const int g = i0 + t;
+        const Camera cam = load_camera(cam_args);
+        const int cnt = nth[g];
+        float S[kPartRowGeo];
+        const float4* src = reinterpret_cast<const float4*>(partials + (size_t)g * kPartRow);
+        constexpr int n4 = kPartRow / 4;
+#pragma unroll
+        for (int i = 0; i < kPartRowGeo / 4; ++i) {
+            const float4 v = src[i < n4 ? i : n4 - 1];
+            const bool use = i < n4 && cnt > 0;
+            S[4 * i] = use ? v.x : 0.f; S[4 * i + 1] = use ? v.y : 0.f;
+            S[4 * i + 2] = use ? v.z : 0.f; S[4 * i + 3] = use ? v.w : 0.f;
+        }
+        setup_bwd_chain<true>(g, S, cnt, cam, means, scales, 1.0f, quats_n, umap, vmap, v_means, v_scales_act,
+                              v_quats_n, v_rgbs, v_opac_act, v_centers, v_uv0);
+        // (this thread's own stores, read back)
+        float4 vq;
+        float vls0, vls1, vo;
+        activate_bwd_splat(reinterpret_cast<const float4*>(quats)[g], log_scales[3 * g], log_scales[3 * g + 1],
+                           opacities[g], reinterpret_cast<const float4*>(v_quats_n)[g], v_scales_act[3 * g],
+                           v_scales_act[3 * g + 1], v_opac_act[g], vq, vls0, vls1, vo);
+        reinterpret_cast<float4*>(v_quats)[g] = vq;
+        v_log_scales[3 * g] = vls0;
+        v_log_scales[3 * g + 1] = vls1;
+        v_log_scales[3 * g + 2] = 0.0f;
+        v_opac_logits[g] = vo;
+        sh_grad_row(degree, 1, n_rest, viewdirs[3 * g], viewdirs[3 * g + 1], viewdirs[3 * g + 2], v_rgbs[3 * g],
+                    v_rgbs[3 * g + 1], v_rgbs[3 * g + 2], s_row + t * kw);
+    }
+    __syncthreads();
+    sh_copy_span<kEpiBlock>(v_rest + (size_t)i0 * kw, s_row, cnt_blk * kw);
+}
+
 }  // namespace
 
 namespace gstex {
@@ -2320,6 +2374,41 @@ int setup_bwd_entry(const char* name, int32_t n, const float* means, const float
                                 row_flags, row_floats, n_rows, cam, v_means, v_scales, v_quats, v_rgbs, v_opacities,
                                 v_centers, v_uv0, as_stream(stream));
     return launch_status(name);
+}
+
+extern "C" int gstex_train_epilogue(const gstex_train_epilogue_args* a, void* stream) {
+    GSTEX_REQUIRE(a && a->n >= 0, "gstex_train_epilogue: invalid arguments");
+    if (a->n == 0) return GSTEX_OK;
+    const bool fused = a->sh_degree >= 0 && a->sh_degree <= 4 && a->n_rest >= 0 &&
+                       (size_t)kEpiBlock * a->n_rest * 3 * sizeof(float) <= 65536 &&
+                       a->n_rest >= (a->sh_degree + 1) * (a->sh_degree + 1) - 1;
+    if (!fused) {  // the per-op entry points (an SH layout whose rows do not fit the staging)
+        int rc = gstex_raster_setup_bwd_aabb(a->n, a->means, a->scales, 1.0f, a->quats_n, a->opacities, a->umap,
+                                             a->vmap, a->num_tiles_hit, a->offsets, a->partials, nullptr, kPartRow,
+                                             -1, &a->cam, a->v_means, a->v_scales_act, a->v_quats_n, a->v_rgbs,
+                                             a->v_opacities_act, a->v_centers, a->v_uv0, stream);
+        if (rc) return rc;
+        rc = gstex_sh_rest_bwd(a->n, a->sh_degree, a->n_rest, a->viewdirs, a->v_rgbs, a->v_features_rest, stream);
+        if (rc) return rc;
+        return gstex_activate_bwd(a->n, a->quats, a->log_scales, a->opacities, a->v_quats_n, a->v_scales_act,
+                                  a->v_opacities_act, a->v_quats, a->v_log_scales, a->v_opac_logits, stream);
+    }
+    GSTEX_REQUIRE(a->means && a->scales && a->quats_n && a->quats && a->log_scales && a->opacities && a->umap &&
+                      a->vmap && a->viewdirs && a->num_tiles_hit && a->partials && a->v_means && a->v_quats &&
+                      a->v_log_scales && a->v_opac_logits && (a->v_features_rest || a->n_rest == 0) &&
+                      a->v_scales_act && a->v_quats_n && a->v_rgbs && a->v_opacities_act && a->v_centers && a->v_uv0,
+                  "gstex_train_epilogue: null pointer");
+    GSTEX_REQUIRE(((reinterpret_cast<uintptr_t>(a->quats) | reinterpret_cast<uintptr_t>(a->quats_n) |
+                    reinterpret_cast<uintptr_t>(a->v_quats) | reinterpret_cast<uintptr_t>(a->v_quats_n) |
+                    reinterpret_cast<uintptr_t>(a->partials)) & 15) == 0,
+                  "gstex_train_epilogue: quaternion and partial-row buffers must be 16-byte aligned");
+    train_epilogue_kernel<<<div_up(a->n, kEpiBlock), kEpiBlock, (size_t)kEpiBlock * a->n_rest * 3 * sizeof(float),
+                            as_stream(stream)>>>(
+        a->n, a->sh_degree, a->n_rest, to_device_camera(a->cam), a->means, a->scales, a->quats_n, a->quats,
+        a->log_scales, a->opacities, a->umap, a->vmap, a->viewdirs, a->num_tiles_hit, a->partials, a->v_means,
+        a->v_quats, a->v_log_scales, a->v_opac_logits, a->v_features_rest, a->v_scales_act, a->v_quats_n, a->v_rgbs,
+        a->v_opacities_act, a->v_centers, a->v_uv0);
+    return launch_status("gstex_train_epilogue");
 }
 
 extern "C" int gstex_raster_setup_bwd(int32_t n, const float* means, const float* scales, float glob_scale,

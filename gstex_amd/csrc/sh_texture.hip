@@ -42,17 +42,8 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degree, int k0, 
                                                      const float* __restrict__ v_out, float* __restrict__ v_coeffs) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    float b[25];
-    sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
-    const int nb = (degree + 1) * (degree + 1);
-    const float g0 = v_out[3 * i], g1 = v_out[3 * i + 1], g2 = v_out[3 * i + 2];
-    float* vc = v_coeffs + (size_t)i * K * 3;
-    for (int k = 0; k < K; ++k) {
-        const float bk = (k + k0 < nb) ? b[k + k0] : 0.0f;
-        vc[3 * k] = bk * g0;
-        vc[3 * k + 1] = bk * g1;
-        vc[3 * k + 2] = bk * g2;
-    }
+    sh_grad_row(degree, k0, K, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], v_out[3 * i], v_out[3 * i + 1],
+                v_out[3 * i + 2], v_coeffs + (size_t)i * K * 3);
 }
 
 // The same two kernels with the coefficient rows staged through LDS: a workgroup's 128 splats own one
@@ -95,17 +86,8 @@ __global__ __launch_bounds__(kShBlock) void sh_bwd_staged_kernel(int n, int degr
     const int kw = K * 3;
     if (t < cnt) {
         const int i = i0 + t;
-        float b[25];
-        sh_basis(degree, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], b);
-        const int nb = (degree + 1) * (degree + 1);
-        const float g0 = v_out[3 * i], g1 = v_out[3 * i + 1], g2 = v_out[3 * i + 2];
-        float* vc = s_c + t * kw;
-        for (int k = 0; k < K; ++k) {
-            const float bk = (k + k0 < nb) ? b[k + k0] : 0.0f;
-            vc[3 * k] = bk * g0;
-            vc[3 * k + 1] = bk * g1;
-            vc[3 * k + 2] = bk * g2;
-        }
+        sh_grad_row(degree, k0, K, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], v_out[3 * i], v_out[3 * i + 1],
+                    v_out[3 * i + 2], s_c + t * kw);
     }
     __syncthreads();
     sh_copy_span<kShBlock>(v_coeffs + (size_t)i0 * kw, s_c, cnt * kw);

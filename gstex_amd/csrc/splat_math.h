@@ -70,6 +70,21 @@ __device__ __forceinline__ void store_activated(int i, const Activated& a, float
     viewdirs[3 * i + 2] = a.vd[2];
 }
 
+// the activations' backward (activations.hip): the quaternion normalisation, exp with the clamp mask for the first two
+// scale axes (the third is detached) and the sigmoid
+__device__ __forceinline__ void activate_bwd_splat(float4 q, float ls0, float ls1, float o, float4 g, float gs0,
+                                                   float gs1, float go, float4& vq, float& vls0, float& vls1,
+                                                   float& vo) {
+    const float nq = act_norm4(q.x, q.y, q.z, q.w);
+    const float w = q.x / nq, x = q.y / nq, y = q.z / nq, z = q.w / nq;
+    const float d = ((w * g.x + x * g.y) + y * g.z) + z * g.w;
+    vq = make_float4((g.x - w * d) / nq, (g.y - x * d) / nq, (g.z - y * d) / nq, (g.w - z * d) / nq);
+    const float e0 = expf(ls0), e1 = expf(ls1);
+    vls0 = (e0 >= 1e-9f) ? gs0 * e0 : 0.0f;
+    vls1 = (e1 >= 1e-9f) ? gs1 * e1 : 0.0f;
+    vo = go * ((1.0f - o) * o);
+}
+
 // ---- preprocessing: project_points' depth, get_aabb_2d, get_num_tiles_hit_2d (gstex.py:1077-1080) ---------------
 struct Preprocessed {
     float depth, cx, cy, ex, ey;
@@ -207,6 +222,20 @@ __device__ __forceinline__ void sh_colour(int degree, int k0, float dx, float dy
         r0 = r0 + b[k] * c[3 * k];
         r1 = r1 + b[k] * c[3 * k + 1];
         r2 = r2 + b[k] * c[3 * k + 2];
+    }
+}
+
+// the coefficient gradient row of one splat: row[3 k + c] = basis[k + k0] * g_c for k < K (0 past the degree)
+__device__ __forceinline__ void sh_grad_row(int degree, int k0, int K, float dx, float dy, float dz, float g0,
+                                            float g1, float g2, float* row) {
+    float b[25];
+    sh_basis(degree, dx, dy, dz, b);
+    const int nb = (degree + 1) * (degree + 1);
+    for (int k = 0; k < K; ++k) {
+        const float bk = (k + k0 < nb) ? b[k + k0] : 0.0f;
+        row[3 * k] = bk * g0;
+        row[3 * k + 1] = bk * g1;
+        row[3 * k + 2] = bk * g2;
     }
 }
 

@@ -6,7 +6,8 @@ guarded scan (three kernels), the splat records, the capped binning -- each behi
 call, autograd node and a dozen tensor allocations.  Here they are one C call (gstex_train_prologue, ABI 17) into one
 arena allocation: activate + preprocess + sh_rest as one per-splat kernel and the scan as one launch (the same device
 functions on the same values, gstex_amd/csrc/splat_math.h: bit-identical outputs), then the records and the binning
-as before; the backward chains raster_bwd -> setup_bwd_aabb -> sh_rest_bwd -> activate_bwd in one node.
+as before; the backward is the raster backward and one epilogue call (gstex_train_epilogue: setup bwd, SH rest bwd
+and activation bwd as one per-splat kernel, again on shared device functions).
 tests/test_gpu_fused.py compares both paths.  What it removes is host time between the launches, which the device
 waits through whenever a step starts on an idle device -- the first step after a synchronisation (bench.py's first
 timed step) -- and four launches.
@@ -23,7 +24,7 @@ import ctypes
 import torch
 
 from . import _lib, ops
-from ._lib import PARTIAL_FLOATS, PARTIAL_FLOATS_PHOTO, REC_FLOATS, ptr
+from ._lib import PARTIAL_FLOATS, REC_FLOATS, ptr
 from .charts import SH_C0  # SH2RGB(texture_dc) applied by the raster on read (gstex.py:1119), as GStexTrainer.render
 
 _ALIGN = 256
@@ -152,14 +153,17 @@ class _TrainRender(torch.autograd.Function):
         grads = torch.empty((ctx.gfloats,), device=dev, dtype=torch.float32)
         g = {k: grads.data_ptr() + 4 * v for k, v in ctx.goff.items()}
         means = tr.means
-        ops._launch("gstex_raster_setup_bwd_aabb", n, ptr(means), P["scales"], 1.0, P["quats_n"], P["opacities"],
-                    P["umap"], P["vmap"], P["num_tiles_hit"], P["offsets"], P["partials"], None, PARTIAL_FLOATS_PHOTO,
-                    -1, cam, g["means"], P["v_scales"], P["v_quats_n"], P["v_rgbs"], P["v_opacities"],
-                    P["v_centers"], P["v_uv0"], st)
         n_rest = tr.features_rest.shape[1]
-        _lib.call("gstex_sh_rest_bwd", n, ctx.degree, n_rest, P["viewdirs"], P["v_rgbs"], g["features_rest"], st)
-        _lib.call("gstex_activate_bwd", n, ptr(quats), ptr(log_scales), P["opacities"], P["v_quats_n"],
-                  P["v_scales"], P["v_opacities"], g["quats"], g["log_scales"], g["opac_logits"], st)
+        # setup bwd -> activations bwd + SH rest bwd in one launch (gstex_train_epilogue)
+        e = _lib.GstexTrainEpilogueArgs(
+            n=n, sh_degree=ctx.degree, n_rest=n_rest, cam=cam, means=ptr(means), scales=P["scales"],
+            quats_n=P["quats_n"], quats=ptr(quats), log_scales=ptr(log_scales), opacities=P["opacities"],
+            umap=P["umap"], vmap=P["vmap"], viewdirs=P["viewdirs"], num_tiles_hit=P["num_tiles_hit"],
+            offsets=P["offsets"], partials=P["partials"], v_means=g["means"], v_quats=g["quats"],
+            v_log_scales=g["log_scales"], v_opac_logits=g["opac_logits"], v_features_rest=g["features_rest"],
+            v_scales_act=P["v_scales"], v_quats_n=P["v_quats_n"], v_rgbs=P["v_rgbs"], v_opacities_act=P["v_opacities"],
+            v_centers=P["v_centers"], v_uv0=P["v_uv0"])
+        _lib.call("gstex_train_epilogue", ctypes.byref(e), st)
         ctx.arena = None
         o = ctx.goff
 

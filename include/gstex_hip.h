@@ -471,6 +471,43 @@ int gstex_train_prologue(const gstex_train_prologue_args* args, void* stream);
  * preprocessing kernel leaves one tile-count sum per 128 splats there for the one-launch offsets scan). */
 size_t gstex_train_prologue_scan_bytes(int32_t n);
 
+/* The photometric training render's backward after gstex_raster_bwd (fast mode: partials = the zeroed (n, 24)
+ * per-splat accumulator rows it added into), in one call (ABI 17; gstex_amd.fused): gstex_raster_setup_bwd_aabb
+ * (glob_scale 1, the camera with c2w), then gstex_activate_bwd and gstex_sh_rest_bwd on its outputs -- one kernel, the
+ * same device functions on the same values (bit-identical), when the SH rows fit its LDS staging.  v_* are the
+ * parameter gradients (written, not accumulated); v_*_act and v_centers / v_uv0 are scratch of n rows each (the
+ * activated parameters' gradients, as the per-op calls write them). */
+typedef struct gstex_train_epilogue_args {
+    int32_t n;
+    int32_t sh_degree;
+    int32_t n_rest;
+    gstex_camera cam;
+    const float* means;
+    const float* scales;     /* activated (gstex_activate_fwd) */
+    const float* quats_n;    /* normalised */
+    const float* quats;      /* raw parameter */
+    const float* log_scales;
+    const float* opacities;  /* activated */
+    const float* umap;
+    const float* vmap;
+    const float* viewdirs;
+    const int32_t* num_tiles_hit;
+    const int32_t* offsets;
+    float* partials;
+    float* v_means;
+    float* v_quats;
+    float* v_log_scales;
+    float* v_opac_logits;
+    float* v_features_rest;
+    float* v_scales_act;
+    float* v_quats_n;
+    float* v_rgbs;
+    float* v_opacities_act;
+    float* v_centers;
+    float* v_uv0;
+} gstex_train_epilogue_args;
+int gstex_train_epilogue(const gstex_train_epilogue_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -170,7 +170,8 @@ def test_struct_layouts_match_header(tmp_path):
 
     structs = {"gstex_camera": _lib.GstexCamera, "gstex_pair_guard": _lib.GstexPairGuard,
                "gstex_adam_tensor": _lib.GstexAdamTensor, "gstex_adam_schedule": _lib.GstexAdamSchedule,
-               "gstex_train_prologue_args": _lib.GstexTrainPrologueArgs}
+               "gstex_train_prologue_args": _lib.GstexTrainPrologueArgs,
+               "gstex_train_epilogue_args": _lib.GstexTrainEpilogueArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gstex_hip.h"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -198,3 +199,5 @@ def test_train_prologue_scan_bytes(lib):
 def test_train_prologue_rejects_null_args(lib):
     rc, msg = _status(lib, "gstex_train_prologue", None, None)
     assert rc != 0 and "null" in msg
+    rc, msg = _status(lib, "gstex_train_epilogue", None, None)
+    assert rc != 0 and "invalid" in msg

@@ -137,3 +137,58 @@ def test_fused_step_with_gradsync_trains_like_per_op(monkeypatch):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+def test_epilogue_matches_per_op_entry_points():
+    """gstex_train_epilogue (setup bwd + activation bwd + SH rest bwd in one kernel) writes bit-identical gradients to
+    gstex_raster_setup_bwd_aabb -> gstex_activate_bwd / gstex_sh_rest_bwd on the same accumulator rows."""
+    import ctypes
+
+    from gstex_amd import _lib, ops
+    from gstex_amd.activations import activate
+    from gstex_amd.model import GStexTrainer
+
+    dev, sc, views, _ = _setup(1500, 30_000)
+    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+    view = views[1]
+    with torch.no_grad():
+        qn, scl, op, uv0, umap, vmap, vd = activate(tr.means, tr.quats, tr.scales, tr.opacities, tr.mappings,
+                                                    view.campos)
+        _, _, _, nth = ops.preprocess(tr.means, scl, 1, qn, view.viewmat, (view.fx, view.fy, view.cx, view.cy),
+                                      view.H, view.W)
+    n, n_rest = tr.means.shape[0], tr.features_rest.shape[1]
+    g = torch.Generator().manual_seed(7)
+    partials = (torch.randn((n, 24), generator=g) * 1e-3).to(dev)
+    vm, cw = ops._viewmat(view.viewmat), ops._c2w(view.c2w)
+    cam = _lib.make_camera(vm, cw, view.fx, view.fy, view.cx, view.cy, view.H, view.W, ops.BLOCK_WIDTH)
+    offsets = torch.zeros((n + 1,), device=dev, dtype=torch.int32)
+    f = dict(device=dev, dtype=torch.float32)
+
+    def bufs():
+        return dict(v_means=torch.empty((n, 3), **f), v_quats=torch.empty((n, 4), **f),
+                    v_log_scales=torch.empty((n, 3), **f), v_opac_logits=torch.empty((n, 1), **f),
+                    v_rest=torch.empty((n, n_rest, 3), **f), v_sc=torch.empty((n, 3), **f),
+                    v_qn=torch.empty((n, 4), **f), v_rgbs=torch.empty((n, 3), **f), v_op=torch.empty((n, 1), **f),
+                    v_c=torch.empty((n, 2), **f), v_uv=torch.empty((n, 2), **f))
+    P = _lib.ptr
+    st = _lib.stream_of(dev)
+    a = bufs()
+    _lib.call("gstex_raster_setup_bwd_aabb", n, P(tr.means), P(scl), 1.0, P(qn), P(op), P(umap), P(vmap), P(nth),
+              P(offsets), P(partials), None, 24, -1, cam, P(a["v_means"]), P(a["v_sc"]), P(a["v_qn"]),
+              P(a["v_rgbs"]), P(a["v_op"]), P(a["v_c"]), P(a["v_uv"]), st)
+    _lib.call("gstex_sh_rest_bwd", n, 3, n_rest, P(vd), P(a["v_rgbs"]), P(a["v_rest"]), st)
+    _lib.call("gstex_activate_bwd", n, P(tr.quats), P(tr.scales), P(op), P(a["v_qn"]), P(a["v_sc"]), P(a["v_op"]),
+              P(a["v_quats"]), P(a["v_log_scales"]), P(a["v_opac_logits"]), st)
+    b = bufs()
+    e = _lib.GstexTrainEpilogueArgs(
+        n=n, sh_degree=3, n_rest=n_rest, cam=cam, means=P(tr.means), scales=P(scl), quats_n=P(qn), quats=P(tr.quats),
+        log_scales=P(tr.scales), opacities=P(op), umap=P(umap), vmap=P(vmap), viewdirs=P(vd), num_tiles_hit=P(nth),
+        offsets=P(offsets), partials=P(partials), v_means=P(b["v_means"]), v_quats=P(b["v_quats"]),
+        v_log_scales=P(b["v_log_scales"]), v_opac_logits=P(b["v_opac_logits"]), v_features_rest=P(b["v_rest"]),
+        v_scales_act=P(b["v_sc"]), v_quats_n=P(b["v_qn"]), v_rgbs=P(b["v_rgbs"]), v_opacities_act=P(b["v_op"]),
+        v_centers=P(b["v_c"]), v_uv0=P(b["v_uv"]))
+    _lib.call("gstex_train_epilogue", ctypes.byref(e), st)
+    torch.cuda.synchronize()
+    assert int((nth > 0).sum()) > n // 2
+    for k in ("v_means", "v_quats", "v_log_scales", "v_opac_logits", "v_rest", "v_rgbs"):
+        assert torch.equal(a[k], b[k]), k
