@@ -23,20 +23,16 @@ using namespace gstex;
 
 namespace {
 
-#ifndef GSTEX_PROLOGUE_BLOCK
-#define GSTEX_PROLOGUE_BLOCK 256  // splats per workgroup of train_splat_kernel (64: 33.9 us, 128: 34.9, 256: 30.8 at cfg3)
-#endif
-#ifndef GSTEX_PROLOGUE_STAGE
-#define GSTEX_PROLOGUE_STAGE 1    // (experiment knob: 0 = each thread reads its SH row from global memory)
-#endif
-constexpr int kSplatBlock = GSTEX_PROLOGUE_BLOCK;  // the coefficient rows of a workgroup's splats staged in LDS
+// splats per workgroup of train_splat_kernel, whose SH coefficient rows are staged in LDS (cfg3: 30.8 us at 256, 33.9
+// at 64, 34.9 at 128; unstaged rows 38.8-40.8 -- EXPERIMENTS.md)
+constexpr int kSplatBlock = 256;
 constexpr int kScanBlock = 256;
 constexpr int kScanItems = 4;
 constexpr int kScanTile = kScanBlock * kScanItems;  // = binning.hip's scan tile
 constexpr int kBlocksPerTile = kScanTile / kSplatBlock;
 // SH rows staged per workgroup within 64 KiB of LDS (256 splats: up to 21 rest coefficients, degree 3's 15; degree 4
 // takes the per-op path)
-constexpr int kMaxRest = GSTEX_PROLOGUE_STAGE ? 65536 / (kSplatBlock * 3 * 4) : 24;
+constexpr int kMaxRest = 65536 / (kSplatBlock * 3 * 4);
 
 __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
     int n, int degree, int n_rest, const float* __restrict__ means, const float* __restrict__ quats,
@@ -54,10 +50,8 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
     const int i0 = blockIdx.x * kSplatBlock;
     const int cnt = min(kSplatBlock, n - i0);
     const int kw = n_rest * 3;
-    if (GSTEX_PROLOGUE_STAGE) {
-        sh_copy_span<kSplatBlock>(s_c, coeffs_rest + (size_t)i0 * kw, cnt * kw);
-        __syncthreads();
-    }
+    sh_copy_span<kSplatBlock>(s_c, coeffs_rest + (size_t)i0 * kw, cnt * kw);
+    __syncthreads();
     int count = 0;
     if (t < cnt) {
         const int i = i0 + t;
@@ -75,8 +69,7 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
         nth[i] = p.nth;
         count = p.nth;
         float r0, r1, r2;
-        sh_colour(degree, 1, a.vd[0], a.vd[1], a.vd[2],
-                  (GSTEX_PROLOGUE_STAGE ? s_c + t * kw : coeffs_rest + (size_t)i * kw) - 3, r0, r1, r2);
+        sh_colour(degree, 1, a.vd[0], a.vd[1], a.vd[2], s_c + t * kw - 3, r0, r1, r2);
         rgbs[3 * i] = r0;
         rgbs[3 * i + 1] = r1;
         rgbs[3 * i + 2] = r2;
@@ -174,7 +167,7 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
         const int tx = (pre.W + pre.block - 1) / pre.block, ty = (pre.H + pre.block - 1) / pre.block;
         int32_t* sums = static_cast<int32_t*>(a->scan_workspace);
         train_splat_kernel<<<div_up(a->n, kSplatBlock), kSplatBlock,
-                             GSTEX_PROLOGUE_STAGE ? (size_t)kSplatBlock * a->n_rest * 3 * sizeof(float) : 0, st>>>(
+                             (size_t)kSplatBlock * a->n_rest * 3 * sizeof(float), st>>>(
             a->n, a->sh_degree, a->n_rest, a->means, a->quats, a->log_scales, a->opac_logits, a->mappings,
             a->map_cols, a->campos, a->features_rest, to_device_camera(a->cam), tx, ty, pre.block, a->quats_n,
             a->scales, a->opacities, a->uv0, a->umap, a->vmap, a->viewdirs, a->depths, a->centers, a->extents,
