@@ -71,26 +71,9 @@ extern "C" int gstex_debug_wg(unsigned long long* out) {
 #define GSTEX_STAT(i, v) do { } while (0)
 #define GSTEX_STATW(i, v) do { } while (0)
 #endif
-#ifndef GSTEX_FWD_PREFETCH
-#define GSTEX_FWD_PREFETCH 0  // forward: next visit's record planes 0-3 read from LDS one visit ahead
-#endif
-#ifndef GSTEX_FWD_ORDER
-#define GSTEX_FWD_ORDER 0  // forward tile launch order (experiment): 0 the binning's largest-first order, 1 row-major,
-                           // 2 XCD macro-blocks (GSTEX_FWD_MB^2 tiles dealt to one XCD back to back, row-major),
-                           // 3 largest-first within XCD groups of MB x MB macro-blocks
-#endif
-#ifndef GSTEX_FWD_MB
-#define GSTEX_FWD_MB 4
-#endif
-#ifndef GSTEX_FWD_DEFER2
-#define GSTEX_FWD_DEFER2 0  // forward: texel gathers folded two visits later (two pending sets; experiment, C = 3 only)
-#endif
-#ifndef GSTEX_FWD_HOIST
-#define GSTEX_FWD_HOIST 0  // forward: the contributing branch's record planes read with the evaluation's (experiment)
-#endif
 #ifndef GSTEX_FWD_OCC
-#define GSTEX_FWD_OCC ((GSTEX_FWD_PREFETCH || GSTEX_FWD_DEFER2) ? 5 : 6)  // forward waves per SIMD the register allocation targets (measured:
-                                                   // 8 at 64 VGPRs is slower)
+#define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower; 5 with
+                         // a record prefetch or a second pending texel set, both measured slower in round 5)
 #endif
 #ifndef GSTEX_XCD_MB
 #define GSTEX_XCD_MB 2  // backward units of one 2x2-tile macro-block dispatched to one XCD (unit_order groups)
@@ -126,8 +109,7 @@ constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in
 #define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
                         // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
                         // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
-                        // 256 = no partial-row / flag stores, 512 = forward without the gradient-buffer zeroing,
-                        // 1024 = forward texel gathers replaced by register values (addresses and arithmetic kept)
+                        // 256 = no partial-row / flag stores, 512 = forward without the gradient-buffer zeroing
                         // (backward ablations skip work: timing experiments only)
 #endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
@@ -209,58 +191,7 @@ __device__ __forceinline__ WaveBlock wave_block(int tx, int ty, int tid) {
     return b;
 }
 
-// Experimental forward launch orders (GSTEX_FWD_ORDER 1, 2).  Mode 2: workgroups b and b + 8 share an XCD (blocks are
-// dealt round-robin over the 8 XCDs); position p = 8 r + g runs the r-th tile of XCD group g, whose tiles are the
-// MB x MB macro-blocks m = 8 k + g (row-major), each walked tile by tile -- a macro-block's tiles share splats and run
-// back to back on one XCD's L2.  Holes (-1): positions past the last macro-block or outside the tile grid.
-__host__ __device__ __forceinline__ int fwd_grid(int tiles_x, int tiles_y) {
-#if GSTEX_FWD_ORDER == 2
-    const int mbx = (tiles_x + GSTEX_FWD_MB - 1) / GSTEX_FWD_MB, mby = (tiles_y + GSTEX_FWD_MB - 1) / GSTEX_FWD_MB;
-    return 8 * GSTEX_FWD_MB * GSTEX_FWD_MB * ((mbx * mby + 7) / 8);
-#else
-    return tiles_x * tiles_y;
-#endif
-}
-__device__ __forceinline__ int fwd_xcd_tile(int p, int tiles_x, int tiles_y) {
-#if GSTEX_FWD_ORDER == 2
-    constexpr int MB = GSTEX_FWD_MB;
-    const int g = p & 7, r = p >> 3;
-    const int m = 8 * (r / (MB * MB)) + g, q = r % (MB * MB);
-    const int mbx = (tiles_x + MB - 1) / MB, mby = (tiles_y + MB - 1) / MB;
-    if (m >= mbx * mby) return -1;
-    const int tx = (m % mbx) * MB + q % MB, ty = (m / mbx) * MB + q / MB;
-    return (tx < tiles_x && ty < tiles_y) ? ty * tiles_x + tx : -1;
-#else
-    return p;
-#endif
-}
-
-// GSTEX_FWD_ORDER 3 (experiment): largest-first inside XCD groups -- tile t belongs to group g(t) of its MB x MB
-// macro-block and runs at position 8 * (its rank by pair count within the group) + g(t); holes stay -1.
-__host__ __device__ __forceinline__ int fwd_group_of(int t, int tiles_x) {
-    const int mbw = (tiles_x + GSTEX_FWD_MB - 1) / GSTEX_FWD_MB;
-    return ((t % tiles_x) / GSTEX_FWD_MB + ((t / tiles_x) / GSTEX_FWD_MB) * mbw) & 7;
-}
-__global__ __launch_bounds__(256) void fwd_group_order_kernel(int n_tiles, int tiles_x,
-                                                              const int2* __restrict__ tile_ranges,
-                                                              int32_t* __restrict__ order) {
-    // (experiment only: every tile's count and group staged in LDS, n_tiles <= 4096)
-    __shared__ int s_cnt[4096];
-    for (int u = threadIdx.x; u < n_tiles && u < 4096; u += 256) {
-        const int2 ru = tile_ranges[u];
-        s_cnt[u] = ((ru.y - ru.x) << 3) | fwd_group_of(u, tiles_x);
-    }
-    __syncthreads();
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= n_tiles || n_tiles > 4096) return;
-    const int g = s_cnt[t] & 7, c = s_cnt[t] >> 3;
-    int r = 0;
-    for (int u = 0; u < n_tiles; ++u) {
-        const int k = s_cnt[u];
-        r += ((k & 7) == g && ((k >> 3) > c || ((k >> 3) == c && u < t))) ? 1 : 0;
-    }
-    order[8 * r + g] = t;
-}
+__host__ __device__ __forceinline__ int fwd_grid(int tiles_x, int tiles_y) { return tiles_x * tiles_y; }
 
 // Record j of a batch staged in LDS as [plane][splat] float4
 template <int NB>
@@ -664,13 +595,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
     const int ti = (int)blockIdx.x;
-#if GSTEX_FWD_ORDER == 0 || GSTEX_FWD_ORDER == 3
     const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
-    if (GSTEX_FWD_ORDER == 3 && tile < 0) return;
-#else
-    const int tile = fwd_xcd_tile(ti, tiles_x, n_tiles / tiles_x);
-    if (tile < 0) return;  // a hole of the macro-block layout (whole workgroup, before any barrier)
-#endif
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int tid = (int)threadIdx.x;
     const WaveBlock wb = wave_block(tx, ty, tid);
@@ -721,25 +646,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             apend = 0.0f;
         }
     };
-#if GSTEX_FWD_DEFER2
-    // two pending sets (experiment): the gathers of wave visit v land in set v & 1 and are folded at visit v + 2 (every
-    // lane holding one, contributing or not), i.e. still in visit order; `par` = the parity of the next visit, whose set
-    // holds the older pending gathers
-    float qpend = 0.0f;
-    float q00[CM], q01[CM], q10[CM], q11[CM], qax = 0.f, qay = 0.f, qw = 0.f;
-    int par = 0;
-    auto fold_pending = [&]() {  // both sets, older first
-        if (par) {
-            fold_set(q00, q01, q10, q11, qax, qay, qw, qpend);
-            fold_set(p00, p01, p10, p11, pax, pay, pw, pend);
-        } else {
-            fold_set(p00, p01, p10, p11, pax, pay, pw, pend);
-            fold_set(q00, q01, q10, q11, qax, qay, qw, qpend);
-        }
-    };
-#else
     auto fold_pending = [&]() { fold_set(p00, p01, p10, p11, pax, pay, pw, pend); };
-#endif
     auto tex_value = [&](int c) {  // the texture output of channel c so far
         return kDefer ? __builtin_fmaf(tex[c], tex_scale, tex_bias * texw) : tex[c];
     };
@@ -813,28 +720,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         bool all_done = __all(GSTEX_FWD_DONE);
         for (int hb = 0; hb < kWords && !all_done; ++hb) {
           unsigned long long m = todo[hb];
-#if GSTEX_FWD_PREFETCH
-          // the cull / evaluation planes (0-3) of the next visited record are read from LDS one visit ahead, so their
-          // latency overlaps the current visit instead of opening it
-          int jc = hb * 64 + (m ? __builtin_ctzll(m) : 0);
-          float4 q0 = s_rec[0 * kFwdBatch + jc], q1 = s_rec[1 * kFwdBatch + jc];
-          float4 q2 = s_rec[2 * kFwdBatch + jc], q3 = s_rec[3 * kFwdBatch + jc];
-#endif
           while (m) {
-#if GSTEX_FWD_PREFETCH
-            const int j = jc;
-            m &= m - 1;
-            jc = m ? hb * 64 + __builtin_ctzll(m) : jc;
-            const float4 n0 = s_rec[0 * kFwdBatch + jc], n1 = s_rec[1 * kFwdBatch + jc];
-            const float4 n2 = s_rec[2 * kFwdBatch + jc], n3 = s_rec[3 * kFwdBatch + jc];
-            const Rec r = rec_from_planes(q0, q1, q2, q3, s_rec[4 * kFwdBatch + j], s_rec[5 * kFwdBatch + j],
-                                          s_rec[6 * kFwdBatch + j], s_rec[7 * kFwdBatch + j]);
-            q0 = n0; q1 = n1; q2 = n2; q3 = n3;
-#else
             const int j = hb * 64 + __builtin_ctzll(m);
             m &= m - 1;
             const Rec r = read_rec<kFwdBatch>(s_rec, j);
-#endif
             ++seg_visits;
             Hit h;
             const bool ok = eval_hit(r, px, py, aa, h) && alive != 0.0f;
@@ -844,65 +733,26 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             GSTEX_STAT(11, __ballot(ok) ? 1 : 0);                 // ... with a contributing lane
             GSTEX_STAT(12, __popcll(__ballot(ok && !stop)));      // contributing lanes
             alive = stop ? 0.0f : alive;
-#if GSTEX_FWD_DEFER2
-            // this visit's set: its gathers of two visits ago are folded first (all lanes holding one)
-            if (par) fold_set(q00, q01, q10, q11, qax, qay, qw, qpend);
-            else fold_set(p00, p01, p10, p11, pax, pay, pw, pend);
-#endif
-#if GSTEX_FWD_HOIST
-            // the contributing branch's record fields (planes 3-7) consumed here, ahead of the branch, so their LDS
-            // reads issue with the evaluation's and their latency hides behind it instead of opening the branch
-            const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
-            const int boff = __builtin_amdgcn_readfirstlane(r.off);
-            asm volatile("" ::"v"(r.rgb[0]), "v"(r.rgb[1]), "v"(r.rgb[2]), "v"(r.tu0), "v"(r.auu), "v"(r.auv),
-                         "v"(r.tv0), "v"(r.avu), "v"(r.avv), "v"(r.hm1), "v"(r.wm1));
-#endif
             if (ok && !stop) {
                 const float w = h.alpha * T;
-#if !GSTEX_FWD_HOIST
                 const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
                 const int boff = __builtin_amdgcn_readfirstlane(r.off);
-#endif
                 const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels && !(GSTEX_ABLATE & 4);
                 if (kDefer) {
                     // (computed whether or not the splat has texels: used only when it has)
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
                     const Bilerp b = bilerp_xy(tu, tv, bh, bw, r.hm1, r.wm1);
-#if GSTEX_FWD_DEFER2
-                    if constexpr (CM != 3) {
-                        fold_pending();  // (two sets only for C = 3; kDefer is false otherwise)
-                    } else if (has_tex) {
-                        const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
-                        if (par) {
-                            load_texel_quad_unclamped(rs, b, bw, q00, q01, q10, q11);
-                            qax = b.ax; qay = b.ay; qw = w; qpend = 1.0f;
-                        } else {
-                            load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
-                            pax = b.ax; pay = b.ay; pw = w; pend = 1.0f;
-                        }
-                    }
-#else
                     fold_pending();
                     if (has_tex) {
                         const __amdgpu_buffer_rsrc_t rs = texel_rsrc(texture, boff, bh * bw, Cn);
-                        if constexpr (CM == 3) {
-                            if (GSTEX_ABLATE & 1024) {  // diagnostic: the gathers' values from the registers instead
-#pragma unroll
-                                for (int c = 0; c < 3; ++c) {
-                                    p00[c] = b.ax + c; p01[c] = b.ay + c; p10[c] = b.ax * c; p11[c] = b.ay * c;
-                                }
-                            } else {
-                                load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
-                            }
-                        }
+                        if constexpr (CM == 3) load_texel_quad_unclamped(rs, b, bw, p00, p01, p10, p11);
                         else load_texel_quad<CM>(rs, b, bw, Cn, p00, p01, p10, p11);
                         pax = b.ax;
                         pay = b.ay;
                         pw = w;
                         pend = 1.0f;
                     }
-#endif
                 } else if (has_tex) {
                     float tu, tv;
                     tex_coords(r, h.u, h.v, tu, tv);
@@ -933,9 +783,6 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                 T = test_T;
                 last = b0 - rng.x + j;
             }
-#if GSTEX_FWD_DEFER2
-            par ^= 1;
-#endif
             if (__builtin_amdgcn_ballot_w64(alive != 0.0f) == 0) {
                 all_done = true;
                 break;
@@ -2245,25 +2092,6 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     zbuf.p[1] = zero_floats2 > 0 && !(GSTEX_ABLATE & 512) ? zero_buf2 : nullptr;
     zbuf.n[1] = zero_floats2;
     int fgrid = fwd_grid(tiles_x, tiles_y);
-#if GSTEX_FWD_ORDER == 3
-    {
-        static int32_t* s_order = nullptr;
-        static int s_cap = 0;
-        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int t = 0; t < nblk; ++t) ++cnt[fwd_group_of(t, tiles_x)];
-        int mx = 0;
-        for (int g = 0; g < 8; ++g) mx = cnt[g] > mx ? cnt[g] : mx;
-        fgrid = 8 * mx;
-        if (fgrid > s_cap) {
-            if (s_order) (void)hipFree(s_order);
-            if (hipMalloc(&s_order, (size_t)fgrid * 4) != hipSuccess) return launch_status("gstex_raster_fwd (order)");
-            s_cap = fgrid;
-        }
-        if (hipMemsetAsync(s_order, 0xFF, (size_t)fgrid * 4, st) != hipSuccess) return launch_status("gstex_raster_fwd");
-        fwd_group_order_kernel<<<(nblk + 255) / 256, 256, 0, st>>>(nblk, tiles_x, (const int2*)tile_ranges, s_order);
-        tile_order = s_order;
-    }
-#endif
 #define GSTEX_FWD(CC, GG)                                                                                      \
     raster_fwd_kernel<CC, GG><<<fgrid, kThreads, 0, st>>>(                                                    \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
