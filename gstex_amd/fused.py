@@ -66,6 +66,8 @@ def _layout(n: int, n_rest: int, capacity: int, H: int, W: int, C: int):
         goff[name] = gpos
         gpos += (nf + 63) // 64 * 64  # floats (256-byte aligned)
     hit = (off, pos, dict(aux=aux, scan_ws=scan_ws, bin_ws=bin_ws, n_tiles=n_tiles), goff, gpos)
+    if len(_LAYOUTS) >= 64:  # (the capacity grows and recharts change n: keep the cache bounded)
+        _LAYOUTS.clear()
     _LAYOUTS[key] = hit
     return hit
 
