@@ -589,10 +589,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             }
         }
     };
-#ifndef GSTEX_ZERO_LATE
-#define GSTEX_ZERO_LATE 0
-#endif
-    if (!GSTEX_ZERO_LATE) zero_grad_buf();
+    zero_grad_buf();
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
@@ -805,7 +802,6 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         const int wl = wave_max_i(last);
         if (wl >= kSegLen) write_ck(sbase + wl / kSegLen);
     }
-    if (GSTEX_ZERO_LATE) zero_grad_buf();
     if (!inside) return;
     const size_t pix = (size_t)pyi * cam.W + pxi;
     out_img[3 * pix + 0] = img[0] + T * bg0;
