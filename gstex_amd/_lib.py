@@ -164,6 +164,11 @@ SIGNATURES = {
         [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, _P, _P, _P],
     ),
+    "gstex_raster_bwd_zero": (
+        c_int32,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+         c_int64, _P, _P, _P, _P, _P, c_int64, _P],
+    ),
     "gstex_raster_setup_bwd": (
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int32, c_int64, _CAM, _P, _P, _P, _P, _P, _P, _P,

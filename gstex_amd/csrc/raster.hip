@@ -235,6 +235,27 @@ struct AuxPtrs {
 };
 struct AuxLayout { size_t masks, cost, order, order_ws, slot_tile, ckpt, bytes; int64_t n_slots, n_units; int F; };
 struct ZeroBufs { float* p[2]; int64_t n[2]; };  // buffers the forward's grid zeroes (gstex_raster_fwd_zero)
+// The accumulation buffers a raster kernel's whole grid zeroes as a side job (gstex_raster_fwd_zero: the texel gradient
+// and the splat-gradient sums of the backward that follows; gstex_raster_bwd_zero: the next step's texel gradient):
+// plain streaming stores the VALU-bound raster kernels hide, instead of fill passes (or an Adam update's zero stores)
+__device__ __forceinline__ void zero_bufs(const ZeroBufs& zb) {
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        float* zp = zb.p[b];
+        const int64_t zn = zb.n[b];
+        if (!zp) continue;
+        if ((reinterpret_cast<uintptr_t>(zp) & 15) == 0) {
+            typedef float z4v __attribute__((ext_vector_type(4)));
+            z4v* z4 = reinterpret_cast<z4v*>(zp);
+            const z4v zero = {0.f, 0.f, 0.f, 0.f};
+            for (int64_t i = t0; i < zn / 4; i += nthr) __builtin_nontemporal_store(zero, z4 + i);
+            if (t0 < zn % 4) zp[zn / 4 * 4 + t0] = 0.0f;
+        } else {
+            for (int64_t i = t0; i < zn; i += nthr) zp[i] = 0.0f;
+        }
+    }
+}
 __host__ inline AuxLayout aux_layout(int64_t n_isect, int n_tiles, int C) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     AuxLayout a;
@@ -568,28 +589,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     int n_tiles, const ZeroBufs zb) {
     const Camera cam = load_camera(cam_args);
     unsigned long long* __restrict__ visit_masks = aux.masks;
-    auto zero_grad_buf = [&]() {
-        // the backward's accumulation buffers (texel gradient, splat-gradient sums) zeroed by the whole grid
-        // (gstex_raster_fwd_zero): plain streaming stores the VALU-bound forward hides, instead of fill passes (or an
-        // Adam update's zero stores) elsewhere
-        const int64_t nthr = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            float* zp = zb.p[b];
-            const int64_t zn = zb.n[b];
-            if (!zp) continue;
-            if ((reinterpret_cast<uintptr_t>(zp) & 15) == 0) {
-                typedef float z4v __attribute__((ext_vector_type(4)));
-                z4v* z4 = reinterpret_cast<z4v*>(zp);
-                const z4v zero = {0.f, 0.f, 0.f, 0.f};
-                for (int64_t i = t0; i < zn / 4; i += nthr) __builtin_nontemporal_store(zero, z4 + i);
-                if (t0 < zn % 4) zp[zn / 4 * 4 + t0] = 0.0f;
-            } else {
-                for (int64_t i = t0; i < zn; i += nthr) zp[i] = 0.0f;
-            }
-        }
-    };
-    zero_grad_buf();
+    zero_bufs(zb);
     constexpr int CM = (C > 0) ? C : 8;  // register capacity for the runtime-C path
     const int Cn = (C > 0) ? C : Cdyn;
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
@@ -1025,7 +1025,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
     const float* __restrict__ v_tex, const float* __restrict__ v_normal, float* __restrict__ partials,
-    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux) {
+    unsigned char* __restrict__ row_flags, float* __restrict__ v_texture, const AuxPtrs aux, const ZeroBufs zb) {
+    zero_bufs(zb);
     const Camera cam = load_camera(cam_args);
     constexpr int CM = (C > 0) ? C : 8;
     const int Cn = (C > 0) ? C : Cdyn;
@@ -2107,14 +2108,13 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     return launch_status("gstex_raster_fwd");
 }
 
-extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
-                                const float* background, const float* records, const int32_t* tile_ranges,
-                                const int32_t* sorted_ids, const int32_t* sorted_slots,
-                                const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
-                                const float* state, const float* v_img,
-                                const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
-                                const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
-                                float* v_texture, void* aux, void* stream) {
+namespace {
+int raster_bwd_impl(const gstex_camera* cam, int32_t channels, int32_t settings, const float* background,
+                    const float* records, const int32_t* tile_ranges, const int32_t* sorted_ids,
+                    const int32_t* sorted_slots, const float* texture, int64_t n_texels, float tex_scale,
+                    float tex_bias, const float* state, const float* v_img, const float* v_depth, const float* v_reg,
+                    const float* v_alpha, const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
+                    uint32_t* row_flags, float* v_texture, void* aux, ZeroBufs zbuf, void* stream) {
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
@@ -2145,13 +2145,14 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     raster_bwd_kernel<CC, GG><<<(unsigned)al.n_units, 64, 0, st>>>(                                            \
         dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
         sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
-        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap)
+        v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap,   \
+        zbuf)
     if (split && channels == 3 && !geo && !row_flags) {
         // the split backward: texel gradients pixel-major, splat gradients splat-parallel
         raster_bwd_kernel<3, false, true><<<(unsigned)al.n_units, 64, 0, st>>>(
             dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, sorted_ids,
             sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state, v_img, v_depth, v_reg,
-            v_alpha, v_tex, v_normal, partials, nullptr, v_texture, ap);
+            v_alpha, v_tex, v_normal, partials, nullptr, v_texture, ap, zbuf);
         raster_bwd_splat_kernel<<<(unsigned)al.n_units, 64, 0, st>>>(
             dc, tiles_x, settings, background, (const float4*)records, (const int2*)tile_ranges, sorted_ids, texture,
             (int)n_texels, tex_scale, tex_bias, (const float4*)state, v_img, v_alpha, v_tex, partials, ap);
@@ -2163,6 +2164,38 @@ extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32
     else GSTEX_BWD(0, true);
 #undef GSTEX_BWD
     return launch_status("gstex_raster_bwd");
+}
+}  // namespace
+
+extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
+                                const float* background, const float* records, const int32_t* tile_ranges,
+                                const int32_t* sorted_ids, const int32_t* sorted_slots,
+                                const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
+                                const float* state, const float* v_img,
+                                const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
+                                const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
+                                float* v_texture, void* aux, void* stream) {
+    return raster_bwd_impl(cam, channels, settings, background, records, tile_ranges, sorted_ids, sorted_slots,
+                           texture, n_texels, tex_scale, tex_bias, state, v_img, v_depth, v_reg, v_alpha, v_tex,
+                           v_normal, n_isect, partials, row_flags, v_texture, aux, ZeroBufs{{nullptr, nullptr}, {0, 0}},
+                           stream);
+}
+
+extern "C" int gstex_raster_bwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
+                                     const float* background, const float* records, const int32_t* tile_ranges,
+                                     const int32_t* sorted_ids, const int32_t* sorted_slots,
+                                     const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
+                                     const float* state, const float* v_img,
+                                     const float* v_depth, const float* v_reg, const float* v_alpha,
+                                     const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
+                                     uint32_t* row_flags, float* v_texture, void* aux, float* zero_buf,
+                                     int64_t zero_floats, void* stream) {
+    GSTEX_REQUIRE(zero_floats >= 0 && (zero_floats == 0 || zero_buf) && zero_buf != v_texture,
+                  "gstex_raster_bwd_zero: invalid zero_buf / zero_floats (it must not be the gradient accumulated)");
+    return raster_bwd_impl(cam, channels, settings, background, records, tile_ranges, sorted_ids, sorted_slots,
+                           texture, n_texels, tex_scale, tex_bias, state, v_img, v_depth, v_reg, v_alpha, v_tex,
+                           v_normal, n_isect, partials, row_flags, v_texture, aux,
+                           ZeroBufs{{zero_floats > 0 ? zero_buf : nullptr, nullptr}, {zero_floats, 0}}, stream);
 }
 
 extern "C" size_t gstex_raster_aux_bytes(int64_t n_isect, int32_t n_tiles, int32_t channels) {

@@ -82,8 +82,8 @@ def _view(arena: torch.Tensor, off: int, shape) -> torch.Tensor:
 
 class _TrainRender(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, tr, view, degree, sink, zero_sink, on_grad, texture_ready, means, quats, log_scales, opac_logits,
-                features_rest):
+    def forward(ctx, tr, view, degree, sink, zero_sink, on_grad, texture_ready, zero_next, means, quats, log_scales,
+                opac_logits, features_rest):
         n = means.shape[0]
         n_rest = features_rest.shape[1]
         H, W, C = int(view.H), int(view.W), 3
@@ -127,6 +127,7 @@ class _TrainRender(torch.autograd.Function):
         ctx.tr, ctx.arena, ctx.P, ctx.cam_keep = tr, arena, P, (vm, cw)
         ctx.cam, ctx.cap, ctx.sink, ctx.degree, ctx.goff, ctx.gfloats = cam, cap, sink, int(degree), goff, gfloats
         ctx.on_grad = on_grad
+        ctx.zero_next = zero_next
         ctx.has_aux = sizes["aux"] > 0
         ctx.save_for_backward(quats, log_scales)
         ctx.set_materialize_grads(False)
@@ -145,11 +146,18 @@ class _TrainRender(torch.autograd.Function):
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
         v_img, v_alpha, v_tex = c(v_img), c(v_alpha), c(v_tex)
         texture = tr.texture_dc
-        ops._launch("gstex_raster_bwd", cam, 3, int(tr.settings) | (_lib.BWD_SPLIT if ops.BWD_SPLIT else 0),
-                    ptr(tr._bg_zero), P["records"], P["tile_ranges"], P["sorted_ids"], P["sorted_slots"],
-                    ptr(texture), texture.shape[0], SH_C0, 0.5, P["state"], ptr(v_img), None, None,
-                    ptr(v_alpha), ptr(v_tex), None, ctx.cap, P["partials"], None, ptr(ctx.sink),
-                    P["aux"] if ctx.has_aux else None, st)
+        bwd_args = (cam, 3, int(tr.settings) | (_lib.BWD_SPLIT if ops.BWD_SPLIT else 0), ptr(tr._bg_zero),
+                    P["records"], P["tile_ranges"], P["sorted_ids"], P["sorted_slots"], ptr(texture),
+                    texture.shape[0], SH_C0, 0.5, P["state"], ptr(v_img), None, None, ptr(v_alpha), ptr(v_tex), None,
+                    ctx.cap, P["partials"], None, ptr(ctx.sink), P["aux"] if ctx.has_aux else None)
+        zn = ctx.zero_next
+        if zn is not None and zn is tr._tex_grad_next and zn.data_ptr() != ctx.sink.data_ptr():
+            # the trainer's other texel-gradient buffer, zeroed by this backward's grid for the next step
+            ops._launch("gstex_raster_bwd_zero", *bwd_args, ptr(zn), zn.numel(), st)
+            tr._next_zeroed = True
+        else:
+            ops._launch("gstex_raster_bwd", *bwd_args, st)
+        ctx.zero_next = None
         if ctx.on_grad is not None:
             ctx.on_grad()  # the texel gradient is complete in stream order (GradSync starts its tail collective)
         grads = torch.empty((ctx.gfloats,), device=dev, dtype=torch.float32)
@@ -171,7 +179,7 @@ class _TrainRender(torch.autograd.Function):
 
         def gv(name, shape):
             return _view_f(grads, o[name], shape)
-        return (None, None, None, None, None, None, None, gv("means", (n, 3)), gv("quats", (n, 4)), gv("log_scales", (n, 3)),
+        return (None, None, None, None, None, None, None, None, gv("means", (n, 3)), gv("quats", (n, 4)), gv("log_scales", (n, 3)),
                 gv("opac_logits", (n, 1)), gv("features_rest", (n, n_rest, 3)))
 
 
@@ -182,9 +190,11 @@ def _view_f(flat: torch.Tensor, off: int, shape) -> torch.Tensor:
     return flat[off:off + nf].view(shape)
 
 
-def train_render(tr, view, degree: int, sink: torch.Tensor, zero_sink: bool, on_grad=None, texture_ready=None):
+def train_render(tr, view, degree: int, sink: torch.Tensor, zero_sink: bool, on_grad=None, texture_ready=None,
+                 zero_next=None):
     """-> (img (H,W,3), alpha (H,W), tex (H,W,3)) of GStexTrainer.render's photometric training branch; the texel
     gradient accumulates into `sink` (zeroed by the raster forward when zero_sink) and on_grad() runs once the raster
-    backward is enqueued; texture_ready() (a deferred texel update) runs right before the raster forward."""
-    return _TrainRender.apply(tr, view, degree, sink, zero_sink, on_grad, texture_ready, tr.means, tr.quats,
-                              tr.scales, tr.opacities, tr.features_rest)
+    backward is enqueued; texture_ready() (a deferred texel update) runs right before the raster forward; zero_next
+    (the trainer's other texel-gradient buffer) is zeroed by the raster backward's grid."""
+    return _TrainRender.apply(tr, view, degree, sink, zero_sink, on_grad, texture_ready, zero_next, tr.means,
+                              tr.quats, tr.scales, tr.opacities, tr.features_rest)

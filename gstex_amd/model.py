@@ -194,15 +194,35 @@ class GStexTrainer:
             fused_step = os.environ.get("GSTEX_FUSED_STEP", "1") != "0"
         self.fused_step = bool(fused_step)
         self._tex_grad = None
+        self._tex_grad_next = None
+        self._cur_zeroed = self._next_zeroed = False
         if self.defer_texture:
             self._own_texture_grad()
         self._build_optimizer()
 
     def _own_texture_grad(self):
-        # the persistent texel-gradient buffer (replaced by a flat-buffer slice when GradSync takes over)
+        # the persistent texel-gradient buffer (replaced by a flat-buffer slice when GradSync takes over).  With the
+        # fused render a second one: step k's raster backward accumulates into one and zeroes the other
+        # (gstex_raster_bwd_zero), which step k + 1 accumulates into, so no forward spends its grid zeroing 120 MB
         self._tex_grad = torch.zeros_like(self.texture_dc)
+        self._tex_grad_next = torch.zeros_like(self.texture_dc) if self.fused_step else None
+        self._cur_zeroed = True  # the current buffer holds no gradient
+        self._next_zeroed = self._tex_grad_next is not None
         self.texture_dc.grad = self._tex_grad
         self.texture_grad_sink = self._tex_grad
+
+    def _double_buffered(self) -> bool:
+        return (self._tex_grad_next is not None and self.texture_grad_route is None
+                and self.texture_grad_sink is self._tex_grad)
+
+    def _step_texels(self, buf, only, skip_flag):
+        """The deferred texel update reading `buf` (the gradient buffer of the step it belongs to)."""
+        keep = self.texture_dc.grad
+        self.texture_dc.grad = buf
+        try:
+            self._step(only=only, skip_flag=skip_flag)
+        finally:
+            self.texture_dc.grad = keep
 
     @property
     def texture_grad_zeroed_by_update(self) -> bool:
@@ -340,6 +360,7 @@ class GStexTrainer:
             pair_guard=guard)
         if torch.is_grad_enabled():
             self._sink_fresh = False  # zeroed by this forward: further renders before the step accumulate on top
+            self._cur_zeroed = False
         out = dict(img=img, tex=tex, depth=depth, reg=reg, alpha=alpha, normal=normal)
         if composite:
             out["rgb"] = torch.clamp(img + tex[:, :, 0:3] + (1 - alpha[:, :, None]) * self.background[None, None, :],
@@ -365,9 +386,14 @@ class GStexTrainer:
             sink, zero_sink, on_grad = self.texture_grad_sink, self._sink_fresh, self.texture_grad_ready
         # a deferred texel update that first waits for its collective (GradSync) runs right before the raster forward
         late = self._run_pending_texture if self._pending_tex is not None and self._pending_collective else None
+        zero_next = None
+        if self._double_buffered():
+            zero_sink = zero_sink and not self._cur_zeroed  # (zeroed by the previous step's raster backward)
+            zero_next = None if self._next_zeroed else self._tex_grad_next  # this backward zeroes the other buffer
         self._poll_pairs()
-        img, alpha, tex = fused.train_render(self, view, deg, sink, zero_sink, on_grad, late)
+        img, alpha, tex = fused.train_render(self, view, deg, sink, zero_sink, on_grad, late, zero_next)
         self._sink_fresh = False
+        self._cur_zeroed = False
         z = ops._zero_scalar(self.device)  # not rendered: read-only zeros without gradient, as the per-op path
         H, W = int(view.H), int(view.W)
         return dict(img=img, tex=tex, depth=z.expand(H, W), reg=z.expand(H, W), alpha=alpha,
@@ -484,8 +510,16 @@ class GStexTrainer:
                 self._pending_collective = True
             else:
                 self._step(skip=tex, skip_flag=sf)
-                self._pending_tex = lambda: self._step(only=tex, skip_flag=sf)
+                buf = self.texture_dc.grad
+                self._pending_tex = lambda: self._step_texels(buf, tex, sf)
                 self._pending_collective = False
+                if self._double_buffered():
+                    # the next step accumulates into the other buffer (zeroed by this step's raster backward, or
+                    # else by the next forward); the pending update reads this one
+                    self._tex_grad, self._tex_grad_next = self._tex_grad_next, self._tex_grad
+                    self._cur_zeroed, self._next_zeroed = self._next_zeroed, False
+                    self.texture_dc.grad = self._tex_grad
+                    self.texture_grad_sink = self._tex_grad
             self.step += 1
             return
         if sync is not None and self.fused_adam:

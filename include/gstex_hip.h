@@ -268,6 +268,17 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
                      const float* v_img, const float* v_depth, const float* v_reg, const float* v_alpha,
                      const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
                      uint32_t* row_flags, float* v_texture, void* aux, void* stream);
+/* gstex_raster_bwd that also zeroes zero_buf[0, zero_floats) with its grid (ABI 17): a persistent gradient buffer of
+ * the NEXT step (gstex_amd.fused double-buffers the texel gradient: this backward accumulates into v_texture and zeroes
+ * the other buffer, which the next step's backward accumulates into) -- instead of the forward's zeroing
+ * (gstex_raster_fwd_zero).  zero_buf must not be v_texture. */
+int gstex_raster_bwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings, const float* background,
+                          const float* records, const int32_t* tile_ranges, const int32_t* sorted_ids,
+                          const int32_t* sorted_slots, const float* texture, int64_t n_texels, float tex_scale,
+                          float tex_bias, const float* state, const float* v_img, const float* v_depth,
+                          const float* v_reg, const float* v_alpha, const float* v_tex, const float* v_normal,
+                          int64_t n_isect, float* partials, uint32_t* row_flags, float* v_texture, void* aux,
+                          float* zero_buf, int64_t zero_floats, void* stream);
 /* Sums each splat's flagged partial rows (slot-major, quadrant-minor order: bitwise reproducible) and chains
  * them to the splat parameters. Outputs are overwritten.  partials is consumed: each splat's sums are written
  * over its first row (the rows are backward scratch, not read again).  row_flags == NULL: partials is the

@@ -178,8 +178,10 @@ def test_deferred_texture_update_matches_plain_step():
             tr.wait_texture()
         torch.cuda.synchronize()
         # the persistent texel-gradient buffers hold the last gradient until the next differentiable raster forward
-        # zeroes them (gstex_raster_fwd_zero)
-        assert float(alone.texture_dc.grad.abs().max()) > 0.0
+        # zeroes them (gstex_raster_fwd_zero); a fused-render trainer keeps it in the second buffer of its pair (the
+        # current one was zeroed by the last raster backward, gstex_raster_bwd_zero)
+        last = alone._tex_grad_next if alone._tex_grad_next is not None else alone.texture_dc.grad
+        assert float(last.abs().max()) > 0.0
         for tr in (alone, synced):
             tr.render(views[0])
         torch.cuda.synchronize()
