@@ -123,8 +123,10 @@ def test_deferred_texture_update_across_rechart_and_eval():
             tr.wait_texture()
         torch.cuda.synchronize()
         # the persistent texel-gradient buffers hold the last gradient until the next differentiable raster forward
-        # zeroes them (gstex_raster_fwd_zero), before its backward accumulates into them
-        assert float(alone.texture_dc.grad.abs().max()) > 0.0
+        # zeroes them (gstex_raster_fwd_zero), before its backward accumulates into them; a fused-render trainer keeps
+        # it in the second buffer of its pair (the current one was zeroed by the last raster backward)
+        last = alone._tex_grad_next if alone._tex_grad_next is not None else alone.texture_dc.grad
+        assert float(last.abs().max()) > 0.0
         for tr in (alone, synced):
             tr.render(views[0])
         torch.cuda.synchronize()
