@@ -333,8 +333,7 @@ def main():
             # twice the first step's transient memory reserved in the caching allocator's pool (allocated and freed at
             # once; the block stays cached): with --warmup < N_POSES a pose with more pairs than any warmup pose is
             # first rendered inside the timed region, where growing the pool (hipMalloc) added 1.2-1.5 ms to that step
-            if os.environ.get("GSTEX_BENCH_WARM_SYNC", "1") != "0":
-                torch.cuda.synchronize()
+            torch.cuda.synchronize()
             transient = torch.cuda.max_memory_allocated(dev) - torch.cuda.memory_allocated(dev)
             torch.empty(2 * transient, dtype=torch.uint8, device=dev)
         # the first step is eager (it sizes the pair capacity); --graph all: every pose's step captured right after
