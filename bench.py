@@ -265,6 +265,8 @@ def main():
     t_scene = time.perf_counter()
     scene = make_scene(args.n_splats, args.n_texels, seed=args.seed)
     views = [sphere_view(i, H, W, n_views=N_POSES).to(dev) for i in range(N_POSES)]
+    for v in views:  # each view's camera centre, cached with the view (View.campos), made with the views
+        v.campos
     # start_step = 3 x sh_degree_interval: SH at its full degree 3 (the regime of 12k of the 15k iterations)
     trainer = GStexTrainer(scene, dev, start_step=3000, defer_texture=not args.no_defer_texture)
     sync = GradSync(trainer, world) if world > 1 else None
