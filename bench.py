@@ -75,11 +75,6 @@ def parse():
                    help="run the texel Adam update inside optimizer_step instead of deferring it into the next "
                         "step's render (GStexTrainer defer_texture)")
     p.add_argument("--cpu-crop", type=int, default=96, help="side of the crop the CPU oracle renders")
-    p.add_argument("--graph", choices=("first", "all", "none"), default="none",
-                   help="N = 1 hipGraph steps (gstex_amd.graphs.StepGraphs): 'first' replays the first timed step, "
-                        "the one that starts on an idle device after the pre-region synchronisation, and enqueues the "
-                        "rest eagerly while the host runs ahead; 'all' replays every step; 'none' is all eager")
-    p.add_argument("--no-graph", dest="graph", action="store_const", const="none", help="= --graph none")
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="diagnostics only: no HIP events around the raster launches (no roofline figures)")
     return p.parse_args()
@@ -287,33 +282,11 @@ def main():
         # N > 1: the collectives inside the step (texel group updated while the head's collective runs)
         trainer.optimizer_step(sync=sync)
 
-    # N = 1: steps captured as hipGraphs (gstex_amd.graphs.StepGraphs; one launch per step instead of ~40 launches
-    # and ~1 ms of Python): the same kernels, the same Adam scalars per step.  A replay spares the device the host's
-    # ~0.5 ms to reach the raster forward after a synchronisation (the first timed step); once the host runs ahead a
-    # replay costs ~10 us more than the eager step (graph-to-graph launch gap, the row-counter kernel), so by default
-    # only the first timed step is a replay
     timed = {"gstex_raster_bwd"} if world == 1 else {"gstex_raster_fwd", "gstex_raster_bwd"}
-    graphs = None
-    if (world == 1 and args.graph != "none" and args.warmup >= 1 and trainer.pairs is not None
-            and trainer.defer_texture):
-        from gstex_amd.graphs import StepGraphs
 
-        graphs = StepGraphs(trainer, body, N_POSES, timed=() if args.no_kernel_timing else timed)
-
-    graph_error = [None]
-
-    def step(eager=False):
-        nonlocal graphs
+    def step():
         pose = (rank + step_no[0] * world) % N_POSES
         step_no[0] += 1
-        if graphs is not None and not eager:
-            try:
-                graphs.replay(pose)  # (a pose's graph is captured at its first replay, while the device runs)
-                return
-            except Exception as ex:  # noqa: BLE001  (a failed capture leaves the host state as it was: eager instead)
-                graph_error[0] = repr(ex)[:300]
-                graphs = None
-                torch.cuda.synchronize()
         body(pose)
 
     # counted quantities for the roofline (every pose of this rank's cycle; the geometry is stationary), before the
@@ -338,22 +311,7 @@ def main():
             torch.cuda.synchronize()
             transient = torch.cuda.max_memory_allocated(dev) - torch.cuda.memory_allocated(dev)
             torch.empty(2 * transient, dtype=torch.uint8, device=dev)
-        # the first step is eager (it sizes the pair capacity); --graph all: every pose's step captured right after
-        # it, early in the warmup (a capture idles the device for a moment and the clock takes several steps to ramp
-        # back up), the rest of the warmup replays them
-        step(eager=w < 1 or args.graph == "first")
-        if w == 0 and graphs is not None and args.graph == "all":
-            try:
-                graphs.capture()
-            except Exception as ex:  # noqa: BLE001
-                graph_error[0] = repr(ex)[:300]
-                graphs = None
-    if graphs is not None and args.graph == "first":
-        try:  # the first timed step's pose, captured after the warmup's eager steps
-            graphs.capture([(rank + args.warmup * world) % N_POSES])
-        except Exception as ex:  # noqa: BLE001
-            graph_error[0] = repr(ex)[:300]
-            graphs = None
+        step()
     # the last warmup step's deferred texel update stays pending: it is the first kernel of the first timed step (as
     # every step starts with the previous step's texel update), and the last timed step's update runs after the timed
     # region -- K steps, K texel updates, and the first timed step starts with ~90 us of device work queued instead of
@@ -379,7 +337,7 @@ def main():
     bound[0].record()
     for k in range(args.steps):
         h0 = time.perf_counter()
-        step(eager=args.graph == "first" and k > 0)
+        step()
         bound[k + 1].record()
         host_s.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
@@ -396,7 +354,7 @@ def main():
         # the raster forward's launch time from a few untimed steps right after the timed region (same workload)
         ops.set_kernel_timing(True, names={"gstex_raster_fwd"})
         for _ in range(6):
-            step(eager=True)  # (the graphs time only the backward)
+            step()
         trainer.wait_texture()
         kt.update(ops.kernel_times())
         ops.set_kernel_timing(False)
@@ -545,16 +503,9 @@ def main():
             "pair_buffers": ("capacity-sized, pair total kept on the device: no host read-back or synchronisation in "
                              "the step (ops.PairCapacity, capacity %d)" % trainer.pairs.capacity
                              if trainer.pairs is not None else "sized by a host read-back of the pair total"),
-            "step_launch": (("first timed step replayed from a hipGraph captured in the warmup (the whole step: "
-                             "geometry restore, render, loss, backward, Adam with per-step bias corrections from device "
-                             "tables; gstex_amd.graphs.StepGraphs), the others enqueued eagerly while the host runs "
-                             "ahead" if args.graph == "first" else
-                             "every step a hipGraph replay of its pose's captured step (gstex_amd.graphs.StepGraphs)")
-                            if graphs is not None
-                            else "eager: every launch enqueued by the host each step" +
+            "step_launch": ("eager: every launch enqueued by the host each step" +
                             ("; the render's launches before the raster forward as one C call and the render as one "
-                             "autograd node (gstex_amd.fused)" if trainer.fused_step else "") +
-                            (f" (graph capture failed: {graph_error[0]})" if graph_error[0] else "")),
+                             "autograd node (gstex_amd.fused)" if trainer.fused_step else "")),
             "texture_update": ("deferred: step k's texel Adam update is the first kernel of step k+1 (same stream, "
                                     "before the raster forward); the timed region holds exactly K texel updates "
                                     "(the last warmup step's and those of timed steps 1..K-1)"

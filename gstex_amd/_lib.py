@@ -16,9 +16,8 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgstex_hip.so")
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 REC_FLOATS = 32
-BWD_SPLIT = 1 << 29  # GSTEX_BWD_SPLIT: gstex_raster_bwd's split (texel-only pixel-major + splat-parallel) backward
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
 SETTING_AA_BLUR = 1 << 9
@@ -64,16 +63,6 @@ class GstexPairGuard(ctypes.Structure):
 
 
 ADAM_MAX_TENSORS = 16
-
-
-class GstexAdamSchedule(ctypes.Structure):
-    """gstex_adam_schedule (ABI 16): per-tensor (step_size, bc2_sqrt) tables read at row base + *counter."""
-    _fields_ = [
-        ("counter", c_void_p),
-        ("table", c_void_p * 16),
-        ("base", c_int32 * 16),
-        ("rows", c_int32 * 16),
-    ]
 
 
 class GstexTrainPrologueArgs(ctypes.Structure):
@@ -138,10 +127,6 @@ SIGNATURES = {
     "gstex_event_elapsed": (c_int32, [c_void_p, c_void_p, POINTER(ctypes.c_float)]),
     "gstex_stream_wait_event": (c_int32, [c_void_p, c_void_p]),
     "gstex_event_destroy": (c_int32, [c_void_p]),
-    "gstex_event_record_external": (c_int32, [c_void_p, c_void_p]),
-    "gstex_graph_event_nodes": (c_int32, [c_void_p, POINTER(c_void_p), c_int32, POINTER(c_void_p)]),
-    "gstex_graph_exec_set_event": (c_int32, [c_void_p, c_void_p, c_void_p]),
-    "gstex_graph_upload": (c_int32, [c_void_p, c_void_p]),
     "gstex_raster_setup": (
         c_int32,
         [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
@@ -202,8 +187,6 @@ SIGNATURES = {
     "gstex_train_prologue": (c_int32, [POINTER(GstexTrainPrologueArgs), _P]),
     "gstex_train_prologue_scan_bytes": (c_size_t, [c_int32]),
     "gstex_train_epilogue": (c_int32, [POINTER(GstexTrainEpilogueArgs), _P]),
-    "gstex_adam_step_scheduled": (c_int32, [c_int32, POINTER(GstexAdamTensor), c_double, c_double, c_double,
-                                            c_int32, c_float, _P, POINTER(GstexAdamSchedule), _P]),
 }
 
 _lib = None
@@ -270,11 +253,9 @@ class _Event:
         call("gstex_event_create", self.KIND, ctypes.byref(h))
         self._h = h.value
 
-    def record(self, device=None, stream: int | None = None, external: bool = False) -> None:
-        """Record on `stream` (a HIP stream handle), default the current stream of `device`.  external: as an
-        event-record node of the graph being captured on that stream (gstex_event_record_external)."""
-        call("gstex_event_record_external" if external else "gstex_event_record", self._h,
-             stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
+    def record(self, device=None, stream: int | None = None) -> None:
+        """Record on `stream` (a HIP stream handle), default the current stream of `device`."""
+        call("gstex_event_record", self._h, stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
 
     @property
     def handle(self) -> int:

@@ -49,7 +49,6 @@ struct AdamArgs {
     float beta1, beta2, eps, one_m_beta1, one_m_beta2;
     float gscale;  // gradient scale applied on read (gstex_adam_step_scaled: a data-parallel 1 / world), 1 = none
     const float* skip;  // gstex_adam_step_guarded: nothing is updated when *skip != 0 (nullable)
-    gstex_adam_schedule sched;  // gstex_adam_step_scheduled (sched.counter non-null): per-tensor scalars from tables
 };
 
 template <bool SCALE>
@@ -70,13 +69,7 @@ __device__ __forceinline__ void adam_chunk(const AdamArgs& a, const int64_t b) {
     while (k + 1 < a.n && a.block_start[k + 1] <= b) ++k;
     const gstex_adam_tensor& t = a.t[k];
     const int64_t base = (b - a.block_start[k]) * kAdamPerBlock;
-    float neg_step = -t.step_size, bc2s = t.bias_correction2_sqrt;
-    if (a.sched.counter) {  // a graph replay's step: row base + *counter of the tensor's (step_size, bc2_sqrt) table
-        const int row = min(max(a.sched.base[k] + *a.sched.counter, 0), a.sched.rows[k] - 1);
-        const float2 sc = reinterpret_cast<const float2*>(a.sched.table[k])[row];
-        neg_step = -sc.x;
-        bc2s = sc.y;
-    }
+    const float neg_step = -t.step_size, bc2s = t.bias_correction2_sqrt;
     const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
                        reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
     if (vec) {
@@ -138,8 +131,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_kernel(const AdamArgs a) {
 
 namespace {
 int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2, double eps,
-                int32_t flags, float grad_scale, void* stream, const float* skip = nullptr,
-                const gstex_adam_schedule* sched = nullptr) {
+                int32_t flags, float grad_scale, void* stream, const float* skip = nullptr) {
     GSTEX_REQUIRE(n_tensors >= 0 && n_tensors <= kAdamMaxTensors,
                   "gstex_adam_step: n_tensors must be in [0, %d] (got %d)", kAdamMaxTensors, n_tensors);
     GSTEX_REQUIRE(n_tensors == 0 || tensors, "gstex_adam_step: null tensor table");
@@ -152,12 +144,6 @@ int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta
         if (t.numel == 0) continue;
         GSTEX_REQUIRE(t.param && t.grad && t.exp_avg && t.exp_avg_sq, "gstex_adam_step: tensor %d: null pointer", i);
         a.t[k] = t;
-        if (sched) {
-            GSTEX_REQUIRE(sched->table[i] && sched->rows[i] > 0, "gstex_adam_step_scheduled: tensor %d has no table", i);
-            a.sched.table[k] = sched->table[i];
-            a.sched.base[k] = sched->base[i];
-            a.sched.rows[k] = sched->rows[i];
-        }
         a.block_start[k] = blocks;
         blocks += (t.numel + kAdamPerBlock - 1) / kAdamPerBlock;
         ++k;
@@ -173,7 +159,6 @@ int adam_launch(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta
     a.one_m_beta2 = (float)(1.0 - beta2);
     a.gscale = grad_scale;
     a.skip = skip;
-    a.sched.counter = sched ? sched->counter : nullptr;
     const int64_t cap = (flags >> GSTEX_ADAM_GRID_SHIFT) & 0xFFFF;
     const unsigned grid = (unsigned)(cap > 0 && cap < blocks ? cap : blocks);
     const hipStream_t st = gstex::as_stream(stream);
@@ -214,15 +199,4 @@ extern "C" int gstex_adam_step_guarded(int32_t n_tensors, const gstex_adam_tenso
     GSTEX_REQUIRE(grad_scale == grad_scale && grad_scale > 0.0f && grad_scale <= 1.0f,
                   "gstex_adam_step_guarded: grad_scale must be in (0, 1] (got %g)", (double)grad_scale);
     return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, grad_scale, stream, skip);
-}
-
-extern "C" int gstex_adam_step_scheduled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1,
-                                         double beta2, double eps, int32_t flags, float grad_scale, const float* skip,
-                                         const gstex_adam_schedule* schedule, void* stream) {
-    GSTEX_REQUIRE((flags & ~(GSTEX_ADAM_ZERO_GRAD | (0xFFFF << GSTEX_ADAM_GRID_SHIFT))) == 0,
-                  "gstex_adam_step_scheduled: unknown flags 0x%x", flags);
-    GSTEX_REQUIRE(grad_scale == grad_scale && grad_scale > 0.0f && grad_scale <= 1.0f,
-                  "gstex_adam_step_scheduled: grad_scale must be in (0, 1] (got %g)", (double)grad_scale);
-    GSTEX_REQUIRE(schedule && schedule->counter, "gstex_adam_step_scheduled: null schedule / counter");
-    return adam_launch(n_tensors, tensors, beta1, beta2, eps, flags, grad_scale, stream, skip, schedule);
 }

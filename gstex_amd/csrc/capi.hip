@@ -2,7 +2,6 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
-#include <vector>
 
 #include "gstex_error.h"
 
@@ -110,89 +109,6 @@ extern "C" int gstex_stream_wait_event(void* stream, void* event) {
 extern "C" int gstex_event_destroy(void* event) {
     if (event && hipEventDestroy((hipEvent_t)event) != hipSuccess) {
         gstex::set_error("gstex_event_destroy: hipEventDestroy failed");
-        return GSTEX_ERR_LAUNCH;
-    }
-    return GSTEX_OK;
-}
-
-// HIP-graph support (ABI 16, see gstex_hip.h)
-// On a capturing stream: an event-record node appended after the capture's current dependencies, which then become
-// that node (what hipEventRecordWithFlags(hipEventRecordExternal) is specified to do; that call fails on this runtime
-// during capture); otherwise a plain record.
-extern "C" int gstex_event_record_external(void* event, void* stream) {
-    if (!event) {
-        gstex::set_error("gstex_event_record_external: null event");
-        return GSTEX_ERR_INVALID_ARG;
-    }
-    const hipStream_t st = gstex::as_stream(stream);
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    hipGraph_t graph = nullptr;
-    const hipGraphNode_t* deps = nullptr;
-    size_t n_deps = 0;
-    hipError_t e = hipStreamGetCaptureInfo_v2(st, &cs, nullptr, &graph, &deps, &n_deps);
-    if (e != hipSuccess) {
-        gstex::set_error("gstex_event_record_external: hipStreamGetCaptureInfo_v2: %s", hipGetErrorString(e));
-        return GSTEX_ERR_LAUNCH;
-    }
-    if (cs != hipStreamCaptureStatusActive) return gstex_event_record(event, stream);
-    hipGraphNode_t node = nullptr;
-    e = hipGraphAddEventRecordNode(&node, graph, deps, n_deps, (hipEvent_t)event);
-    if (e == hipSuccess) e = hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
-    if (e != hipSuccess) {
-        gstex::set_error("gstex_event_record_external: event-record node: %s", hipGetErrorString(e));
-        return GSTEX_ERR_LAUNCH;
-    }
-    return GSTEX_OK;
-}
-
-extern "C" int gstex_graph_event_nodes(void* graph, void* const* events, int32_t n, void** nodes) {
-    if (!graph || n < 0 || (n > 0 && (!events || !nodes))) {
-        gstex::set_error("gstex_graph_event_nodes: invalid arguments");
-        return GSTEX_ERR_INVALID_ARG;
-    }
-    size_t count = 0;
-    if (hipGraphGetNodes((hipGraph_t)graph, nullptr, &count) != hipSuccess) {
-        gstex::set_error("gstex_graph_event_nodes: hipGraphGetNodes failed");
-        return GSTEX_ERR_LAUNCH;
-    }
-    std::vector<hipGraphNode_t> all(count);
-    if (count && hipGraphGetNodes((hipGraph_t)graph, all.data(), &count) != hipSuccess) {
-        gstex::set_error("gstex_graph_event_nodes: hipGraphGetNodes failed");
-        return GSTEX_ERR_LAUNCH;
-    }
-    for (int32_t i = 0; i < n; ++i) nodes[i] = nullptr;
-    for (hipGraphNode_t node : all) {
-        hipGraphNodeType type;
-        if (hipGraphNodeGetType(node, &type) != hipSuccess || type != hipGraphNodeTypeEventRecord) continue;
-        hipEvent_t ev = nullptr;
-        if (hipGraphEventRecordNodeGetEvent(node, &ev) != hipSuccess) continue;
-        for (int32_t i = 0; i < n; ++i)
-            if ((void*)ev == events[i]) nodes[i] = (void*)node;
-    }
-    for (int32_t i = 0; i < n; ++i)
-        if (!nodes[i]) {
-            gstex::set_error("gstex_graph_event_nodes: event %d is recorded by no node of the graph", i);
-            return GSTEX_ERR_INVALID_ARG;
-        }
-    return GSTEX_OK;
-}
-
-extern "C" int gstex_graph_exec_set_event(void* exec, void* node, void* event) {
-    if (!exec || !node || !event) {
-        gstex::set_error("gstex_graph_exec_set_event: null argument");
-        return GSTEX_ERR_INVALID_ARG;
-    }
-    const hipError_t e = hipGraphExecEventRecordNodeSetEvent((hipGraphExec_t)exec, (hipGraphNode_t)node, (hipEvent_t)event);
-    if (e != hipSuccess) {
-        gstex::set_error("gstex_graph_exec_set_event: hipGraphExecEventRecordNodeSetEvent: %s", hipGetErrorString(e));
-        return GSTEX_ERR_LAUNCH;
-    }
-    return GSTEX_OK;
-}
-
-extern "C" int gstex_graph_upload(void* exec, void* stream) {
-    if (!exec || hipGraphUpload((hipGraphExec_t)exec, gstex::as_stream(stream)) != hipSuccess) {
-        gstex::set_error("gstex_graph_upload: hipGraphUpload failed");
         return GSTEX_ERR_LAUNCH;
     }
     return GSTEX_OK;

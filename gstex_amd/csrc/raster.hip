@@ -22,6 +22,7 @@
 #include "gstex_error.h"
 #include "gstex_internal.h"
 #include "splat_math.h"  // splat_record
+#include "raster_diag.h"  // diagnostic builds only (GSTEX_STATS counters); empty by default
 
 using namespace gstex;
 
@@ -45,31 +46,6 @@ constexpr int kThreads = kTilePixels;  // 256
 #ifndef GSTEX_UNIT_COARSE
 #define GSTEX_UNIT_COARSE 3  // backward unit-order cost buckets of 2^k visits (inside a bucket: about slot order,
                              // better L2 reuse of texel blocks). Measured: 3 same time, bwd fetch -18 %; 5, 6 slower
-#endif
-#ifndef GSTEX_STATS
-#define GSTEX_STATS 0  // diagnostic builds: count backward work (iterations, culled, active lanes)
-#endif
-#if GSTEX_STATS
-__device__ unsigned long long g_stats[24];  // [0, 8) backward, [8, 13) forward counters, [13, 20) backward
-extern "C" int gstex_debug_stats(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(g_stats)) == hipSuccess ? 0 : 2;
-}
-__device__ unsigned long long g_wg[65536 * 4];
-extern "C" int gstex_debug_wg(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg), sizeof(g_wg)) == hipSuccess ? 0 : 2;
-}
-#if GSTEX_STATS == 1
-#define GSTEX_STAT(i, v) do { const unsigned long long v_ = (v); if ((threadIdx.x & 63) == 0) atomicAdd(&g_stats[i], v_); } while (0)
-// the same from the first active lane (divergent code)
-#define GSTEX_STATW(i, v) do { const unsigned long long v_ = (v); \
-    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_stats[i], v_); } while (0)
-#else
-#define GSTEX_STAT(i, v) do { } while (0)
-#define GSTEX_STATW(i, v) do { } while (0)
-#endif
-#else
-#define GSTEX_STAT(i, v) do { } while (0)
-#define GSTEX_STATW(i, v) do { } while (0)
 #endif
 #ifndef GSTEX_FWD_OCC
 #define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower; 5 with
@@ -105,13 +81,6 @@ constexpr int kFwdBatch = GSTEX_FWD_BATCH;
 #define GSTEX_FWD_DEFER 1
 #endif
 constexpr bool kFwdDefer = GSTEX_FWD_DEFER;  // forward: texel gathers folded in one visit later (C = 3)
-#ifndef GSTEX_ABLATE
-#define GSTEX_ABLATE 0  // diagnostic builds only: 1 = no texel-gradient atomics, 2 = no wave reduction,
-                        // 4 = fwd without texel fetch, 8 = bwd without texel-value fetch, 16 = no texel-gradient
-                        // atomics (segmented scan kept), 32 = no flush atomics, 64 = no fixed-point conversion,
-                        // 256 = no partial-row / flag stores, 512 = forward without the gradient-buffer zeroing
-                        // (backward ablations skip work: timing experiments only)
-#endif
 constexpr int kRecF4 = GSTEX_REC_FLOATS / 4;  // 8 float4 per record
 #ifndef GSTEX_WORD_WAIT
 #define GSTEX_WORD_WAIT 1  // backward: the visit loop's id wait hoisted to the word start (see raster_bwd_kernel)
@@ -373,45 +342,6 @@ __device__ __forceinline__ int wave_max_i(int v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return __builtin_amdgcn_readfirstlane(v);
 }
-// inclusive prefix product / sum over the 64 lanes (lane 0 first): in-row Hillis-Steele steps (row_shr 1, 2, 4, 8; a
-// lane whose source lies before its row start is not written, i.e. multiplied by 1 / added 0), then rows 1, 3 take
-// lane 15 of the row before and rows 2, 3 lane 31 (row_bcast).  s_nop 1 covers each VALU-write -> DPP-read hazard.
-__device__ __forceinline__ float lane_scan_mul(float v) {
-    asm volatile("s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
-                 "v_mul_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n s_nop 1"
-                 : "+v"(v));
-    return v;
-}
-__device__ __forceinline__ float lane_scan_add(float v) {
-    asm volatile("s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
-                 "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n s_nop 1"
-                 : "+v"(v));
-    return v;
-}
-// lane l - 1's value (0 in lane 0): the exclusive scan from the inclusive one
-__device__ __forceinline__ float lane_shift_up(float v) {
-    float r;
-    asm volatile("s_nop 1\n v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 1"
-                 : "=v"(r) : "v"(v));
-    return r;
-}
-
-// sum over the wave, wave-uniform result (a bound, not a parity value: any summation order): the DPP lane scan's
-// last lane, no LDS round trips (ds_bpermute shuffles would put six serial LDS latencies on the visit's chain)
-__device__ __forceinline__ float wave_sum_f(float v) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lane_scan_add(v)), 63));
-}
-
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
 __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool aa, Hit& h) {
     // branch-free: a skipped pair's values are computed anyway (possibly inf/NaN) and never used, so
@@ -737,7 +667,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                 const float w = h.alpha * T;
                 const int bh = __builtin_amdgcn_readfirstlane(r.h), bw = __builtin_amdgcn_readfirstlane(r.w);
                 const int boff = __builtin_amdgcn_readfirstlane(r.off);
-                const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels && !(GSTEX_ABLATE & 4);
+                const bool has_tex = bh * bw > 0 && boff + bh * bw <= n_texels;
                 if (kDefer) {
                     // (computed whether or not the splat has texels: used only when it has)
                     float tu, tv;
@@ -1014,10 +944,7 @@ constexpr int kFlushU = GSTEX_FLUSH_U;  // staging entries per lane per flush pa
 static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging area");
 
 
-// TEXONLY (the split backward's texel half, GSTEX_BWD_SPLIT): the same walk, T recurrence and texel-gradient scan /
-// staging / flush, without the texel gathers, the splat-gradient arithmetic and its reduce; the splat gradients then
-// come from raster_bwd_splat_kernel.
-template <int C, bool GEO, bool TEXONLY = false>
+template <int C, bool GEO>
 __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
     const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
@@ -1073,19 +1000,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     // the wave's last contributor: pairs behind it receive no gradient from this quadrant (no row, no flag); this
     // unit walks tile-list positions [lo, hi] of its segment
     const int wave_last = wave_max_i(last);
-#if GSTEX_STATS == 3  // per-wave timeline (diagnostic builds): start, end (s_memrealtime), tile depth, wave_last
-    struct WgStamp {
-        unsigned long long t0; int depth, wl;
-        __device__ ~WgStamp() {
-            if (threadIdx.x == 0 && blockIdx.x < 65536) {
-                g_wg[4 * blockIdx.x] = t0;
-                g_wg[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-                g_wg[4 * blockIdx.x + 2] = (unsigned long long)depth;
-                g_wg[4 * blockIdx.x + 3] = (unsigned long long)(long long)wl;
-            }
-        }
-    } stamp_{__builtin_amdgcn_s_memrealtime(), rng.y - rng.x, wave_last};
-#endif
+    GSTEX_WG_STAMP(rng.y - rng.x, wave_last);
     const int sbase = seg_base(rng.x, tile);
     const int seg = slot - sbase, lo = seg * kSegLen;
     if (wave_last < lo) return;
@@ -1125,11 +1040,6 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
     for (int c = 0; c < CM; ++c) gabs = fmaxf(gabs, fabsf(Gtex[c]));
     for (int i = lane; i < kTexStage; i += 64) s_texq[i] = 0;
     const size_t vm_base = visit_mask_base(rng.x, tile);
-#if GSTEX_STATS == 1  // packing counters: runs of consecutive visits whose contributing lane sets are disjoint
-    unsigned long long st_acc = 0, st_acc2 = 0, st_acc4 = 0;
-    int st_n2 = 0, st_n4 = 0;
-    long long st_lanes = 0;
-#endif
 
     for (int wd = hi >> 6; wd >= (lo >> 6); --wd) {
         const int pos0 = wd << 6;
@@ -1166,35 +1076,17 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
             GSTEX_STAT(14, __popcll(__ballot(contrib)) <= 16 ? 1 : 0);  // sparse visits
             GSTEX_STAT(15, __popcll(__ballot(contrib)) >= 48 ? 1 : 0);  // dense visits
-#if GSTEX_STATS == 1
-            {
-                const unsigned long long m = __ballot(contrib);
-                if (m) {
-                    if (st_acc == 0 || (m & st_acc)) { GSTEX_STAT(16, 1); st_acc = m; } else { st_acc |= m; }
-                    if (st_n2 == 0 || st_n2 == 2 || (m & st_acc2)) { GSTEX_STAT(17, 1); st_acc2 = m; st_n2 = 1; }
-                    else { st_acc2 |= m; st_n2 = 2; }
-                    if (st_n4 == 0 || st_n4 == 4 || (m & st_acc4)) { GSTEX_STAT(18, 1); st_acc4 = m; st_n4 = 1; }
-                    else { st_acc4 |= m; ++st_n4; }
-                    st_lanes += __popcll(m);
-                    // 8x4 half-blocks (lanes 0-31 = rows 0-3, 32-63 = rows 4-7) with a contributing pixel
-                    GSTEX_STAT(20, (unsigned long long)(((unsigned)m != 0u) + ((unsigned)(m >> 32) != 0u)));
-                }
-            }
-#endif
             constexpr int NP = GEO ? kPartRowGeo : kPartRow;
             // a spare slot of the row (zero when stored): the texel fixed-point bound
             constexpr int kMBound = GEO ? 27 : P_NRM;
             float P[NP];
-            float mb = 0.0f;  // TEXONLY: this pixel's share of the visit's texel fixed-point bound
-            if constexpr (!TEXONLY) {
 #pragma unroll
-                for (int i = 0; i < NP; i += 2) {
-                    // zero rows in 64-bit moves (one v_mov_b64 per register pair)
-                    unsigned long long zz;
-                    asm volatile("v_mov_b64 %0, 0" : "=v"(zz));
-                    P[i] = __uint_as_float((unsigned)zz);
-                    P[i + 1] = __uint_as_float((unsigned)(zz >> 32));
-                }
+            for (int i = 0; i < NP; i += 2) {
+                // zero rows in 64-bit moves (one v_mov_b64 per register pair)
+                unsigned long long zz;
+                asm volatile("v_mov_b64 %0, 0" : "=v"(zz));
+                P[i] = __uint_as_float((unsigned)zz);
+                P[i + 1] = __uint_as_float((unsigned)(zz >> 32));
             }
             // texel-gradient inputs, expanded into the 4*C bilinear contributions after P is reduced:
             // tkey = top-left texel of the block | (i1 - i0) << 29 | (j1 - j0) << 30, -1 if none
@@ -1207,18 +1099,6 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 const float one_m = 1.0f - h.alpha;
                 T = T * grad_rcp(one_m);
                 const float w = h.alpha * T;
-                if constexpr (TEXONLY) {
-                    if (r.h * r.w > 0 && blk_ok && !(GSTEX_ABLATE & 1)) {
-                        float xr, yr;
-                        tex_coords(r, h.u, h.v, xr, yr);
-                        const Bilerp b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
-                        tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
-                        tw = w * tex_scale;
-                        mb = fabsf(tw) * gabs;
-                        tax = b.ax;
-                        tay = b.ay;
-                    }
-                } else {
                 // issue the texel gathers first, then everything that does not need them
                 const bool has_tex = r.h * r.w > 0 && blk_ok;
                 Bilerp b;
@@ -1233,8 +1113,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
                     // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
-                    if (GSTEX_ABLATE & 8) {
-                    } else if constexpr (CM == 3) {
+                    if constexpr (CM == 3) {
                         load_texel_quad_unclamped(rs, b, r.w, t00, t01, t10, t11);
                     } else {
                         load_texel_quad<CM>(rs, b, r.w, Cn, t00, t01, t10, t11);
@@ -1256,7 +1135,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     dz = w * Gd;
                     if (dreg) dz += Greg * (2.0f * w * (m * Af - M1f)) * ((kFarRatio * kNear) * (iz * iz));
                 }
-                if (has_tex && !(GSTEX_ABLATE & 1)) {
+                if (has_tex) {
                     tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
                     tw = w * tex_scale;  // d value / d stored texel
                     P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
@@ -1331,19 +1210,11 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     P[P_TW + 1] = h.use3 ? dz * h.v : 0.f;
                     P[P_TW + 2] = dz;
                 }
-                }  // !TEXONLY
             }
             float vis_M = 0.f;  // sum over the wave's pixels of |w tex_scale| max_c |dL/dtex[c]| for this splat
-            if constexpr (TEXONLY) {
-                if (__any(tkey >= 0)) vis_M = wave_sum_f(mb);
-            } else if (__any(contrib)) {
+            if (__any(contrib)) {
                 GSTEX_STAT(2, 1);
-                if (GSTEX_ABLATE & 2) {
-#pragma unroll
-                    for (int i = 3; i < NP; ++i) asm volatile("" ::"v"(P[i]));
-                } else {
-                    wave_reduce<NP>(P);
-                }
+                wave_reduce<NP>(P);
                 // take the bound out of the spare slot (kMBound) before the row is stored
                 constexpr int kML = GEO ? 48 : 56, kMI = GEO ? 3 : 0;  // its lane and index after the reduce-scatter
                 vis_M = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(P[kMI]), kML));
@@ -1356,7 +1227,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 const int base = (NP / 2) * ((lane >> 5) & 1) + (NP / 4) * ((lane >> 4) & 1) + E * ((lane >> 3) & 1);
                 if (row_flags) {
                     const int slot = __builtin_amdgcn_readlane(my_slot, j);
-                    if ((lane & 7) == 0 && !(GSTEX_ABLATE & 256)) {
+                    if ((lane & 7) == 0) {
                         float* dst = partials + ((size_t)slot * 4 + quad) * NP + base;  // rows NP floats apart
                         if constexpr (E == 4) {
                             *reinterpret_cast<float4*>(dst) = make_float4(P[0], P[1], P[2], P[3]);
@@ -1366,8 +1237,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                             dst[2] = P[2];
                         }
                     }
-                    if (lane == 0 && !(GSTEX_ABLATE & 256)) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
-                } else if (!(GSTEX_ABLATE & 256)) {
+                    if (lane == 0) row_flags[(size_t)slot * 4 + quad] = GEO ? 2 : 1;
+                } else {
                     float* dst = partials + (size_t)gid * NP + base;
                     // lane 8k + e takes value e of lane 8k (DPP row shifts): one atomic instruction covers the NP
                     // contiguous floats (2 cache-line requests; E atomics from each lane 8k measured +0.2 ms)
@@ -1412,15 +1283,12 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                         tg[3 * CM + c] = gt * w11;
                     }
                 }
-                const bool tail = (GSTEX_ABLATE & 128) ? tkey >= 0 : seg_reduce_rows<4 * CM>(tkey, tg);
+                const bool tail = seg_reduce_rows<4 * CM>(tkey, tg);
                 const int bsize = r.h * r.w * Cn;  // wave-uniform
                 const bool staged = bsize <= kTexStage;
                 GSTEX_STAT(5, __popcll(__ballot(tail)));
                 GSTEX_STAT(7, 1);
-                if (GSTEX_ABLATE & 16) {
-#pragma unroll
-                    for (int i = 0; i < 4 * CM; ++i) asm volatile("" ::"v"(tg[i]));
-                } else if (tail) {
+                if (tail) {
                     const int t0 = tkey & ((1 << 29) - 1), tdi = (tkey >> 29) & 1, tdj = (tkey >> 30) & 1;
                     const int c00 = t0 * Cn, c01 = (t0 + tdj) * Cn;
                     const int c10 = (t0 + tdi * r.w) * Cn, c11 = (t0 + tdi * r.w + tdj) * Cn;
@@ -1449,7 +1317,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                         }
                     }
                 }
-                if (staged && !(GSTEX_ABLATE & 64)) {
+                if (staged) {
                     // flush the block (non-zero entries only) and leave the staging area zeroed; the wave's LDS
                     // operations complete in order, so these reads see every tail added above
                     float* dst = v_texture + (size_t)r.off * Cn;
@@ -1465,214 +1333,11 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                             GSTEX_STAT(6, __popcll(__ballot(v[k] != 0)));
                             if (v[k] == 0) continue;
                             s_texq[e0 + 64 * k] = 0;
-                            if (!(GSTEX_ABLATE & 32)) atomicAdd(dst + e0 + 64 * k, (float)v[k] * pow_mS);
+                            atomicAdd(dst + e0 + 64 * k, (float)v[k] * pow_mS);
                         }
                     }
                 }
             }
-        }
-    }
-#if GSTEX_STATS == 1
-    GSTEX_STAT(19, (st_lanes + 63) / 64);  // passes if this unit's contributing pairs were packed densely
-#endif
-}
-
-// ------------------------------------------------------------------------------------------
-// split backward, splat half (GSTEX_BWD_SPLIT; photometric C = 3, float-atomic splat sums): splat-parallel
-// ------------------------------------------------------------------------------------------
-// The same units as raster_bwd_kernel (tile, 8x8 quadrant, 256-position segment; same launch order, checkpoints and
-// cull bits), transposed: the unit's visits (the forward's cull bits up to the wave's last contributor) are listed back
-// to front and taken 64 at a time, ONE SPLAT PER LANE (lane 0 the backmost), and the wave walks the quadrant's 64
-// pixels.  At a pixel every lane evaluates its own pair; the transmittance in front of lane l is T_end / prod_{l' <= l}
-// (1 - alpha_l') (an inclusive product scan over the lanes, DPP row shifts + row broadcasts) and the colour behind it
-// S_end + sum_{l' < l} w_l' g_l' (an exclusive sum scan), where T_end / S_end are the pixel's transmittance and colour
-// behind the chunk (the forward's final state or checkpoint, then carried from chunk to chunk in LDS).  Each lane keeps
-// its splat's 21 gradient sums in registers over the 64 pixels -- no per-visit wave reduction -- and adds them to the
-// splat's accumulator row once per chunk.  Texel gradients are not computed here (raster_bwd_kernel TEXONLY).
-#ifndef GSTEX_SPLAT_WAVES
-#define GSTEX_SPLAT_WAVES 4
-#endif
-constexpr int kPxF = 12;  // per-pixel LDS record: T_end, S_end, last (bits), Ga, Gimg[3], Gtex[3], tex_bias term, pad
-
-__global__ __launch_bounds__(64) void lane_scan_probe_kernel(const float* in, float* out) {
-    const float v = in[threadIdx.x];
-    out[threadIdx.x] = lane_scan_mul(v);
-    out[64 + threadIdx.x] = lane_scan_add(v);
-    out[128 + threadIdx.x] = lane_shift_up(v);
-}
-
-__global__ __launch_bounds__(64, GSTEX_SPLAT_WAVES) void raster_bwd_splat_kernel(
-    CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, const float4* __restrict__ records,
-    const int2* __restrict__ tile_ranges, const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture,
-    int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
-    const float* __restrict__ v_alpha, const float* __restrict__ v_tex, float* __restrict__ partials,
-    const AuxPtrs aux) {
-    const Camera cam = load_camera(cam_args);
-    __shared__ __attribute__((aligned(16))) float s_px[64 * kPxF];
-    __shared__ int s_list[kSegLen];
-    const int unit = aux.order[blockIdx.x] - 1;
-    if (unit < 0) return;
-    const int quad = unit & 3, slot = unit >> 2;
-    const int tile = aux.slot_tile[slot];
-    const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int lane = threadIdx.x;
-    const WaveBlock wb = wave_block(tx, ty, quad * 64 + lane);
-    const bool inside = wb.px < cam.W && wb.py < cam.H;
-    const bool aa = (settings & GSTEX_SETTING_AA_BLUR) != 0;
-    const int2 rng = tile_ranges[tile];
-    const float bg0 = bg ? bg[0] : 0.f, bg1 = bg ? bg[1] : 0.f, bg2 = bg ? bg[2] : 0.f;
-    // lane = pixel: the pixel's state behind the unit's segment, as raster_bwd_kernel's prologue
-    float T = 1.0f, Gimg[3] = {0.f, 0.f, 0.f}, Gtex[3] = {0.f, 0.f, 0.f}, Ga = 0.f;
-    int last = -1;
-    if (inside) {
-        const size_t pix = (size_t)wb.py * cam.W + wb.px;
-        const float4 st = state[pix];
-        T = st.x;
-        last = __float_as_int(st.w);
-        if (v_img) { Gimg[0] = v_img[3 * pix]; Gimg[1] = v_img[3 * pix + 1]; Gimg[2] = v_img[3 * pix + 2]; }
-        if (v_tex) { Gtex[0] = v_tex[3 * pix]; Gtex[1] = v_tex[3 * pix + 1]; Gtex[2] = v_tex[3 * pix + 2]; }
-        Ga = v_alpha ? v_alpha[pix] : 0.f;
-    }
-    const int wave_last = wave_max_i(last);
-    const int sbase = seg_base(rng.x, tile);
-    const int seg = slot - sbase, lo = seg * kSegLen;
-    if (wave_last < lo) return;
-    const int hi = min(lo + kSegLen - 1, wave_last), kf = wave_last / kSegLen;
-    // S = the colour behind, unnormalised: T_final (bg term) + sum over the splats behind the segment of w_j g_j
-    float S = T * ((Gimg[0] * bg0 + Gimg[1] * bg1) + Gimg[2] * bg2);
-    if (seg < kf) {
-        const float* ck = aux.ckpt + ((size_t)slot * 4 + quad) * aux.F * 64 + lane;
-        const float* fin = aux.ckpt + ((size_t)(sbase + kf) * 4 + quad) * aux.F * 64 + lane;
-        const float Tk = ck[0];
-        float back = (Gimg[0] * (fin[64] - ck[64]) + Gimg[1] * (fin[128] - ck[128])) + Gimg[2] * (fin[192] - ck[192]);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) back += Gtex[c] * (fin[(4 + c) * 64] - ck[(4 + c) * 64]);
-        back += Ga * (Tk - T);
-        if (inside) {
-            S = back + S;
-            T = Tk;
-        }
-    }
-    {
-        float* q = s_px + lane * kPxF;
-        q[0] = T;
-        q[1] = S;
-        q[2] = __int_as_float(inside ? last : -1);
-        q[3] = Ga;
-        q[4] = Gimg[0]; q[5] = Gimg[1]; q[6] = Gimg[2];
-        q[7] = Gtex[0]; q[8] = Gtex[1]; q[9] = Gtex[2];
-        q[10] = tex_bias * ((Gtex[0] + Gtex[1]) + Gtex[2]);
-        q[11] = 0.f;
-    }
-    // the segment's visits, back to front
-    const size_t vm_base = visit_mask_base(rng.x, tile);
-    int n_vis = 0;
-    for (int wd = hi >> 6; wd >= (lo >> 6); --wd) {
-        const int pos0 = wd << 6;
-        unsigned long long todo = aux.masks[(vm_base + wd) * 4 + quad];
-        const int lim = hi - pos0 + 1;
-        if (lim < 64) todo &= (1ull << lim) - 1ull;
-        if (!todo) continue;
-        if ((todo >> lane) & 1ull) {
-            const int above = lane == 63 ? 0 : __popcll(todo >> (lane + 1));
-            s_list[n_vis + above] = pos0 + lane;
-        }
-        n_vis += __popcll(todo);
-    }
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(texture), 0,
-                                                                          n_texels * 12, 0x00020000);
-    const float ox = (float)(tx * kTile + (quad & 1) * 8) + 0.5f, oy = (float)(ty * kTile + (quad >> 1) * 8) + 0.5f;
-    for (int c0 = 0; c0 < n_vis; c0 += 64) {
-        const bool has = c0 + lane < n_vis;
-        const int rel = has ? s_list[c0 + lane] : 0x7fffffff;
-        const int relmin = s_list[min(n_vis, c0 + 64) - 1];  // the chunk's frontmost position
-        const int gid = has ? sorted_ids[rng.x + rel] : sorted_ids[rng.x + relmin];
-        const Rec r = read_rec_global(records + (size_t)gid * kRecF4);
-        const bool tex_ok = has && r.h * r.w > 0 && r.off + r.h * r.w <= n_texels;
-        const int rowb = r.w * 12;
-        const int boff = r.off * 12;
-        float acc[21];
-#pragma unroll
-        for (int k = 0; k < 21; ++k) acc[k] = 0.f;
-        for (int p = 0; p < 64; ++p) {
-#pragma clang fp contract(fast)
-            const float4 s0 = *reinterpret_cast<const float4*>(s_px + p * kPxF);
-            const int lastp = __float_as_int(s0.z);
-            if (lastp < relmin) continue;  // no pair of this chunk reaches the pixel (or it lies outside the image)
-            const float4 s1 = *reinterpret_cast<const float4*>(s_px + p * kPxF + 4);
-            const float4 s2 = *reinterpret_cast<const float4*>(s_px + p * kPxF + 8);
-            const float pxp = ox + (float)(p & 7), pyp = oy + (float)(p >> 3);
-            Hit h;
-            const bool contrib = has && eval_hit(r, pxp, pyp, aa, h) && rel <= lastp;
-            const float om = contrib ? 1.0f - h.alpha : 1.0f;
-            const float Q = lane_scan_mul(om);
-            const float Tb = s0.x * grad_rcp(Q);  // transmittance in front of this lane's splat
-            const float w = contrib ? h.alpha * Tb : 0.0f;
-            // texel value and its sample-point gradient (all channels folded with the pixel's dL/dtex)
-            // s0 = (T_end, S_end, last, Ga), s1 = (Gimg[0..2], Gtex[0]), s2 = (Gtex[1..2], tex_bias term, -)
-            float g = ((s1.x * r.rgb[0] + s1.y * r.rgb[1]) + s1.z * r.rgb[2]) + s0.w;
-            float dxr = 0.f, dyr = 0.f, su = 0.f, sv = 0.f;
-            Bilerp b;
-            if (contrib && tex_ok) {
-                float xr, yr;
-                tex_coords(r, h.u, h.v, xr, yr);
-                b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
-                const int o00 = boff + (int)(__umul24(b.i0, (unsigned)rowb) + __umul24(b.j0, 12u));
-                const int o10 = o00 + rowb;
-                const auto a0 = __builtin_amdgcn_raw_buffer_load_b96(trs, o00, 0, 0);
-                const auto a1 = __builtin_amdgcn_raw_buffer_load_b96(trs, o00 + 12, 0, 0);
-                const auto a2 = __builtin_amdgcn_raw_buffer_load_b96(trs, o10, 0, 0);
-                const auto a3 = __builtin_amdgcn_raw_buffer_load_b96(trs, o10 + 12, 0, 0);
-                const float D00 = (s1.w * __int_as_float(a0[0]) + s2.x * __int_as_float(a0[1])) + s2.y * __int_as_float(a0[2]);
-                const float D01 = (s1.w * __int_as_float(a1[0]) + s2.x * __int_as_float(a1[1])) + s2.y * __int_as_float(a1[2]);
-                const float D10 = (s1.w * __int_as_float(a2[0]) + s2.x * __int_as_float(a2[1])) + s2.y * __int_as_float(a2[2]);
-                const float D11 = (s1.w * __int_as_float(a3[0]) + s2.x * __int_as_float(a3[1])) + s2.y * __int_as_float(a3[2]);
-                g += bilerp_mix(D00, D01, D10, D11, b.ax, b.ay) * tex_scale + s2.z;
-                su = (1.0f - b.ay) * (D10 - D00) + b.ay * (D11 - D01);
-                sv = (1.0f - b.ax) * (D01 - D00) + b.ax * (D11 - D10);
-                dxr = b.in_u ? w * su : 0.0f;
-                dyr = b.in_v ? w * sv : 0.0f;
-            }
-            const float wg = w * g;
-            const float Sin = lane_scan_add(wg);
-            const float Sb = s0.y + lane_shift_up(Sin);  // the colour behind this lane's splat
-            const float Q63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Q), 63));
-            const float S63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sin), 63));
-            if (lane == 0) {
-                s_px[p * kPxF] = s0.x * grad_rcp(Q63);
-                s_px[p * kPxF + 1] = s0.y + S63;
-            }
-            if (contrib) {
-                const float dL_dalpha = Tb * g - Sb * grad_rcp(om);
-                float drho = 0.f;
-                if (h.a_raw < kAlphaMax) {
-                    acc[P_OPAC] += dL_dalpha * h.G;
-                    drho = dL_dalpha * h.a_raw * -0.5f;
-                }
-                acc[P_RGB + 0] += w * s1.x;
-                acc[P_RGB + 1] += w * s1.y;
-                acc[P_RGB + 2] += w * s1.z;
-                const float dxs = dxr * tex_scale, dys = dyr * tex_scale;
-                const float dtu = dxs * (float)r.h, dtv = dys * (float)r.w;
-                acc[P_TU0] += dtu; acc[P_AUU] += dtu * h.u; acc[P_AUV] += dtu * h.v;
-                acc[P_TV0] += dtv; acc[P_AVU] += dtv * h.u; acc[P_AVV] += dtv * h.v;
-                float du = dxs * r.auu + dys * r.avu;
-                float dv = dxs * r.auv + dys * r.avv;
-                du = h.use3 ? du + drho * 2.0f * h.u : du;
-                dv = h.use3 ? dv + drho * 2.0f * h.v : dv;
-                acc[P_XY + 0] += h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.x - pxp);
-                acc[P_XY + 1] += h.use3 ? 0.f : drho * (2.0f * kFilterInvSq) * (r.y - pyp);
-                const f3 dp = f3{du * h.ipz, dv * h.ipz, -(du * h.u + dv * h.v) * h.ipz};
-                acc[P_A + 0] += dp.x * h.dx; acc[P_A + 1] += dp.y * h.dx; acc[P_A + 2] += dp.z * h.dx;
-                acc[P_B + 0] += dp.x * h.dy; acc[P_B + 1] += dp.y * h.dy; acc[P_B + 2] += dp.z * h.dy;
-                acc[P_P0 + 0] += dp.x; acc[P_P0 + 1] += dp.y; acc[P_P0 + 2] += dp.z;
-            }
-        }
-        if (has) {
-            float* dst = partials + (size_t)gid * kPartRow;
-#pragma unroll
-            for (int k = 0; k < 21; ++k) atomicAdd(dst + k, acc[k]);
         }
     }
 }
@@ -2088,9 +1753,9 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
         return launch_status("gstex_raster_fwd (aux)");
     settings &= ~GSTEX_SETTING_AUX_ZEROED;
     ZeroBufs zbuf;
-    zbuf.p[0] = zero_floats > 0 && !(GSTEX_ABLATE & 512) ? zero_buf : nullptr;
+    zbuf.p[0] = zero_floats > 0 ? zero_buf : nullptr;
     zbuf.n[0] = zero_floats;
-    zbuf.p[1] = zero_floats2 > 0 && !(GSTEX_ABLATE & 512) ? zero_buf2 : nullptr;
+    zbuf.p[1] = zero_floats2 > 0 ? zero_buf2 : nullptr;
     zbuf.n[1] = zero_floats2;
     int fgrid = fwd_grid(tiles_x, tiles_y);
 #define GSTEX_FWD(CC, GG)                                                                                      \
@@ -2118,8 +1783,6 @@ int raster_bwd_impl(const gstex_camera* cam, int32_t channels, int32_t settings,
     GSTEX_REQUIRE(cam && cam->H > 0 && cam->W > 0, "gstex_raster_bwd: invalid camera");
     GSTEX_REQUIRE(cam->block == kTile, "gstex_raster_bwd: block_width must be %d", kTile);
     GSTEX_REQUIRE(channels >= 1 && channels <= 8, "gstex_raster_bwd: channels must be in [1, 8]");
-    const bool split = (settings & GSTEX_BWD_SPLIT) != 0;
-    settings &= ~GSTEX_BWD_SPLIT;
     int rc = check_settings(settings);
     if (rc) return rc;
     GSTEX_REQUIRE(tile_ranges && state && aux, "gstex_raster_bwd: null pointer (tile_ranges, state and the forward's aux)");
@@ -2147,16 +1810,7 @@ int raster_bwd_impl(const gstex_camera* cam, int32_t channels, int32_t settings,
         sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
         v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap,   \
         zbuf)
-    if (split && channels == 3 && !geo && !row_flags) {
-        // the split backward: texel gradients pixel-major, splat gradients splat-parallel
-        raster_bwd_kernel<3, false, true><<<(unsigned)al.n_units, 64, 0, st>>>(
-            dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges, sorted_ids,
-            sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state, v_img, v_depth, v_reg,
-            v_alpha, v_tex, v_normal, partials, nullptr, v_texture, ap, zbuf);
-        raster_bwd_splat_kernel<<<(unsigned)al.n_units, 64, 0, st>>>(
-            dc, tiles_x, settings, background, (const float4*)records, (const int2*)tile_ranges, sorted_ids, texture,
-            (int)n_texels, tex_scale, tex_bias, (const float4*)state, v_img, v_alpha, v_tex, partials, ap);
-    } else if (channels == 3 && !geo) GSTEX_BWD(3, false);
+    if (channels == 3 && !geo) GSTEX_BWD(3, false);
     else if (channels == 3) GSTEX_BWD(3, true);
     else if (channels == 6 && !geo) GSTEX_BWD(6, false);
     else if (channels == 6) GSTEX_BWD(6, true);
@@ -2317,11 +1971,4 @@ extern "C" int gstex_texture_edit(const gstex_camera* cam, int32_t settings, con
         dc, tiles_x, settings, (const float4*)records, (const int2*)tile_ranges, tile_order, sorted_ids, edit_rgb,
         edit_alpha, depth_lo, depth_hi, (int)n_texels, out);
     return launch_status("gstex_texture_edit");
-}
-
-// Test hook (not part of include/gstex_hip.h): the splat-parallel backward's lane scans on in[64] -> out[192] =
-// inclusive product, inclusive sum, shift by one lane (tests/test_gpu_split.py).
-extern "C" int gstex_debug_lane_scans(const float* in, float* out, void* stream) {
-    lane_scan_probe_kernel<<<1, 64, 0, as_stream(stream)>>>(in, out);
-    return launch_status("gstex_debug_lane_scans");
 }

@@ -6,9 +6,9 @@
 //   train_splat_kernel  one thread per splat runs activate_splat -> preprocess_splat -> sh_colour -> splat_record
 //                       (splat_math.h, the functions the per-op kernels call, on the same fp32 values: bit-identical
 //                       outputs) and writes every per-op output incl. the raster record, plus the tile-count sum of
-//                       its 128-splat block;
+//                       its kSplatBlock (256)-splat block;
 //   train_scan_kernel   the offsets scan in one launch: each 1024-splat scan tile starts from the sum of the block
-//                       sums before it (8 per tile; at most n / 128 L2-resident words), then scans its tile as
+//                       sums before it (kBlocksPerTile = 4 per tile; at most n / 256 L2-resident words), then scans its tile as
 //                       binning.hip's scan_final_kernel does (same integers, same guard);
 //                       its grid also zeroes the binning's tile counters and the raster forward's accumulated aux span
 //                       (args.raster_aux), so neither needs its fill launch (GSTEX_SETTING_AUX_ZEROED);

@@ -115,6 +115,11 @@ class GradSync:
             self.trainer.texture_grad_ready = (self._tail_ready_sink if self.overlap_tail and not self.head_first
                                                else None)
             self.trainer.texture_grad_route = self._route
+            # the trainer's second (double-buffered) texel-gradient buffer is never used once the flat buffer's slice
+            # is the sink (GStexTrainer._double_buffered() is False): free it
+            if getattr(self.trainer, "_tex_grad_next", None) is not None:
+                self.trainer._tex_grad_next = None
+                self.trainer._next_zeroed = False
         else:
             self._install_hook(params[-1])
         return True

@@ -82,8 +82,8 @@ def _view(arena: torch.Tensor, off: int, shape) -> torch.Tensor:
 
 class _TrainRender(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, tr, view, degree, sink, zero_sink, on_grad, texture_ready, zero_next, means, quats, log_scales,
-                opac_logits, features_rest):
+    def forward(ctx, tr, view, degree, sink, zero_sink, first, on_grad, texture_ready, zero_next, means, quats,
+                log_scales, opac_logits, features_rest):
         n = means.shape[0]
         n_rest = features_rest.shape[1]
         H, W, C = int(view.H), int(view.W), 3
@@ -91,7 +91,9 @@ class _TrainRender(torch.autograd.Function):
         st = _lib.stream_of(dev)
         pcap = tr.pairs
         step_flag = tr._skip_flag()
-        guard, slot, cap = pcap.reserve(step_flag, bool(zero_sink), tr.step)
+        # `first`: the step's first render, which resets the step's guard flag (not whether the sink is zeroed here:
+        # with the double-buffered texel gradient the previous backward zeroed it)
+        guard, slot, cap = pcap.reserve(step_flag, bool(first), tr.step)
         off, nbytes, sizes, goff, gfloats = _layout(n, n_rest, cap, H, W, C)
         arena = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
         base = arena.data_ptr()
@@ -146,7 +148,7 @@ class _TrainRender(torch.autograd.Function):
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
         v_img, v_alpha, v_tex = c(v_img), c(v_alpha), c(v_tex)
         texture = tr.texture_dc
-        bwd_args = (cam, 3, int(tr.settings) | (_lib.BWD_SPLIT if ops.BWD_SPLIT else 0), ptr(tr._bg_zero),
+        bwd_args = (cam, 3, int(tr.settings), ptr(tr._bg_zero),
                     P["records"], P["tile_ranges"], P["sorted_ids"], P["sorted_slots"], ptr(texture),
                     texture.shape[0], SH_C0, 0.5, P["state"], ptr(v_img), None, None, ptr(v_alpha), ptr(v_tex), None,
                     ctx.cap, P["partials"], None, ptr(ctx.sink), P["aux"] if ctx.has_aux else None)
@@ -179,7 +181,7 @@ class _TrainRender(torch.autograd.Function):
 
         def gv(name, shape):
             return _view_f(grads, o[name], shape)
-        return (None, None, None, None, None, None, None, None, gv("means", (n, 3)), gv("quats", (n, 4)), gv("log_scales", (n, 3)),
+        return (None, None, None, None, None, None, None, None, None, gv("means", (n, 3)), gv("quats", (n, 4)), gv("log_scales", (n, 3)),
                 gv("opac_logits", (n, 1)), gv("features_rest", (n, n_rest, 3)))
 
 
@@ -190,11 +192,12 @@ def _view_f(flat: torch.Tensor, off: int, shape) -> torch.Tensor:
     return flat[off:off + nf].view(shape)
 
 
-def train_render(tr, view, degree: int, sink: torch.Tensor, zero_sink: bool, on_grad=None, texture_ready=None,
-                 zero_next=None):
+def train_render(tr, view, degree: int, sink: torch.Tensor, zero_sink: bool, first: bool, on_grad=None,
+                 texture_ready=None, zero_next=None):
     """-> (img (H,W,3), alpha (H,W), tex (H,W,3)) of GStexTrainer.render's photometric training branch; the texel
-    gradient accumulates into `sink` (zeroed by the raster forward when zero_sink) and on_grad() runs once the raster
+    gradient accumulates into `sink` (zeroed by the raster forward when zero_sink), `first` marks the step's first
+    render (it resets the step's pair-capacity guard flag), and on_grad() runs once the raster
     backward is enqueued; texture_ready() (a deferred texel update) runs right before the raster forward; zero_next
     (the trainer's other texel-gradient buffer) is zeroed by the raster backward's grid."""
-    return _TrainRender.apply(tr, view, degree, sink, zero_sink, on_grad, texture_ready, zero_next, tr.means,
+    return _TrainRender.apply(tr, view, degree, sink, zero_sink, first, on_grad, texture_ready, zero_next, tr.means,
                               tr.quats, tr.scales, tr.opacities, tr.features_rest)

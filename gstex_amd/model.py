@@ -185,7 +185,6 @@ class GStexTrainer:
             pair_capacity = os.environ.get("GSTEX_SYNC_PAIRS", "0") == "0"
         self.pairs = ops.PairCapacity(d) if (pair_capacity and fused_adam and self.device.type == "cuda") else None
         self.step_control = torch.zeros(8, device=d, dtype=torch.float32)
-        self.single_flag = False  # gstex_amd.graphs.StepGraphs: every step uses step_control[0]
         self.skipped_steps = []  # steps whose update the pair-capacity guard skipped (found by _poll_pairs)
         # fused_step (not in the reference): the photometric training render as one C prologue call and one autograd
         # node (gstex_amd.fused) -- the same launches with ~0.23 ms less host time before the raster forward (the
@@ -205,7 +204,9 @@ class GStexTrainer:
         # fused render a second one: step k's raster backward accumulates into one and zeroes the other
         # (gstex_raster_bwd_zero), which step k + 1 accumulates into, so no forward spends its grid zeroing 120 MB
         self._tex_grad = torch.zeros_like(self.texture_dc)
-        self._tex_grad_next = torch.zeros_like(self.texture_dc) if self.fused_step else None
+        # (not under GradSync, whose flat-buffer slice is the sink: the second buffer would never be used)
+        self._tex_grad_next = (torch.zeros_like(self.texture_dc)
+                               if self.fused_step and self.texture_grad_route is None else None)
         self._cur_zeroed = True  # the current buffer holds no gradient
         self._next_zeroed = self._tex_grad_next is not None
         self.texture_dc.grad = self._tex_grad
@@ -242,7 +243,7 @@ class GStexTrainer:
         """The current step's guard flag (1-element view of step_control) for its Adam launches, or None."""
         if self.pairs is None:
             return None
-        k = 0 if self.single_flag else self.step % 8
+        k = self.step % 8
         return self.step_control[k:k + 1]
 
     def _poll_pairs(self):
@@ -345,8 +346,7 @@ class GStexTrainer:
             sink, zero_sink, on_grad = self.texture_grad_sink, self._sink_fresh, self.texture_grad_ready
         guard = None
         if self.pairs is not None and torch.is_grad_enabled():
-            if not torch.cuda.is_current_stream_capturing():  # (a captured step's owner polls between replays)
-                self._poll_pairs()
+            self._poll_pairs()
             guard = (self.pairs, self._skip_flag(), self._sink_fresh, self.step)
         img, depth, reg, alpha, tex, normal = ops.texture_gaussians(
             (n, 1, 3), self.texture_dims, centers, extents, depths, nth, rgbs, opacities, means, scales, 1, quats,
@@ -391,7 +391,8 @@ class GStexTrainer:
             zero_sink = zero_sink and not self._cur_zeroed  # (zeroed by the previous step's raster backward)
             zero_next = None if self._next_zeroed else self._tex_grad_next  # this backward zeroes the other buffer
         self._poll_pairs()
-        img, alpha, tex = fused.train_render(self, view, deg, sink, zero_sink, on_grad, late, zero_next)
+        img, alpha, tex = fused.train_render(self, view, deg, sink, zero_sink, self._sink_fresh, on_grad, late,
+                                             zero_next)
         self._sink_fresh = False
         self._cur_zeroed = False
         z = ops._zero_scalar(self.device)  # not rendered: read-only zeros without gradient, as the per-op path

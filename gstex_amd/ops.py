@@ -8,7 +8,6 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 from __future__ import annotations
 
 import ctypes
-import os
 import time
 from typing import NamedTuple, Tuple
 
@@ -18,9 +17,6 @@ from . import _lib
 from ._lib import PARTIAL_FLOATS, PARTIAL_FLOATS_PHOTO, REC_FLOATS, call, ptr
 
 BLOCK_WIDTH = 16
-# GSTEX_BWD_SPLIT=1: the photometric backward as the split pair (gstex_raster_bwd with GSTEX_BWD_SPLIT, ABI 15) -- an
-# experiment, off by default (measured slower than the single pixel-major kernel)
-BWD_SPLIT = os.environ.get("GSTEX_BWD_SPLIT", "0") != "0"
 
 # ----------------------------------------------------------------------------------------
 # optional per-kernel timing: HIP events recorded on the stream each kernel is launched on
@@ -53,27 +49,9 @@ def _TIMING_EVENTS(name: str) -> list:
     return list((_TIMING or {}).get(name, []))
 
 
-# Inside a hipGraph capture (gstex_amd.graphs.StepGraphs) the launches named in _CAPTURE_TIMED get their event pair
-# as event-record nodes of the graph (gstex_event_record_external), logged as (name, start, end) in _CAPTURE_TIMING;
-# the graph's owner points those nodes at a fresh pair before every replay.  A plain record there would only order
-# the capture, so no other launch is timed while capturing.
-_CAPTURE_TIMED: set | None = None
-_CAPTURE_TIMING: list | None = None
-
-
 def _launch(name: str, *args) -> None:
     # gstex_raster_fwd_zero times as the forward
     key = name[:-len("_zero")] if name.endswith("_zero") else name
-    if _CAPTURE_TIMED is not None and torch.cuda.is_current_stream_capturing():
-        if key not in _CAPTURE_TIMED:
-            call(name, *args)
-            return
-        a, b = _lib.TimingEvent(), _lib.TimingEvent()
-        a.record(external=True)
-        call(name, *args)
-        b.record(external=True)
-        _CAPTURE_TIMING.append((key, a, b))
-        return
     if _TIMING is None or key not in _TIMED or torch.cuda.is_current_stream_capturing():
         call(name, *args)
         return
@@ -378,7 +356,6 @@ class PairCapacity:
         self.max_total = 0
         self.last_total = None
         self.overflows = []  # tags (trainer steps) of renders whose total exceeded the capacity
-        self.graph_word = None  # device pointer of the host word a render being captured reports into (StepGraphs)
 
     def __del__(self):
         try:
@@ -422,20 +399,6 @@ class PairCapacity:
     def scan(self, nth: torch.Tensor, step_flag: torch.Tensor, first: bool, tag=None):
         """The offsets scan of one render with the guard: -> (offsets (n+1,), capacity for this render)."""
         n = nth.shape[0]
-        if torch.cuda.is_current_stream_capturing():
-            # a step being captured into a hipGraph (gstex_amd.graphs.StepGraphs): the current capacity, and the total
-            # written into the graph's own host word (graph_word, a device pointer), which the graph's owner reads
-            # between replays -- no ring slot, no wait
-            if self.capacity <= 0 or self.graph_word is None:
-                raise RuntimeError("PairCapacity.scan: capturing needs a sized capacity (one eager render first) and a "
-                                   "graph_word")
-            offsets = torch.empty((n + 1,), device=nth.device, dtype=torch.int32)
-            ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=nth.device,
-                             dtype=torch.uint8)
-            guard = _lib.GstexPairGuard(self.capacity, ptr(step_flag), self.graph_word, 1 if first else 0)
-            call("gstex_scan_offsets_guarded", n, ptr(nth), ptr(offsets), ptr(ws), ws.numel(), ctypes.byref(guard),
-                 _stream(nth))
-            return offsets, self.capacity
         guard, k, cap = self.reserve(step_flag, first, tag, sized=False)
         offsets = torch.empty((n + 1,), device=nth.device, dtype=torch.int32)
         ws = torch.empty((max(int(_lib.load().gstex_scan_workspace_size(n)), 1),), device=nth.device, dtype=torch.uint8)
@@ -687,7 +650,7 @@ class _TextureGaussians(torch.autograd.Function):
             row_flags = None
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
-        _launch("gstex_raster_bwd", cam, C, int(settings) | (_lib.BWD_SPLIT if BWD_SPLIT else 0), ptr(bg), ptr(records),
+        _launch("gstex_raster_bwd", cam, C, int(settings), ptr(bg), ptr(records),
                 ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),

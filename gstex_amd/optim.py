@@ -8,65 +8,9 @@ updated by one HIP launch (16 tensors per launch) instead of torch's ~7 foreach 
 """
 from __future__ import annotations
 
-import ctypes
-
-import numpy as np
 import torch
 
 from . import _lib
-
-
-class AdamSchedule:
-    """Per-step Adam bias corrections on the device, for training steps captured into hipGraphs
-    (gstex_adam_step_scheduled, gstex_amd.graphs.StepGraphs).
-
-    A captured launch cannot take a new step_size / bias_correction2_sqrt each replay, so for every parameter this keeps
-    a device table of those two fp32 scalars for steps t0, t0 + 1, ... -- the same python-double expressions
-    FusedAdam.step evaluates per call, rounded to fp32 the same way -- and the captured update reads row
-    (t_capture - t0) + counter, where `counter` (a device int32) is advanced by one at the end of every replayed step.
-    Replay r therefore applies the corrections of step t_capture + r, exactly what the eager step r would.  shift(n)
-    slides every table n steps forward and takes n off the counter (stream-ordered) before the rows run out."""
-
-    def __init__(self, optimizer, device, rows: int = 8192):
-        self.rows = int(rows)
-        self.device = torch.device(device)
-        self.counter = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self._t0, self._tables, self._groups = {}, {}, {}
-        self.updates = {}  # id(param) -> updates registered since reset_updates() (one per parameter per step)
-        for group in optimizer.param_groups:
-            for p in group["params"]:
-                t0 = int(optimizer.state[p].get("step", 0)) + 1 if p in optimizer.state else 1
-                self._t0[id(p)] = t0
-                self._groups[id(p)] = group
-                self._tables[id(p)] = torch.from_numpy(self._host_table(group, t0)).to(self.device)
-
-    def _host_table(self, group, t0: int) -> np.ndarray:
-        b1, b2 = group["betas"]
-        lr = group["lr"]
-        out = np.empty((self.rows, 2), dtype=np.float32)
-        for r in range(self.rows):
-            t = t0 + r
-            out[r, 0] = lr / (1.0 - b1 ** t)  # FusedAdam.step's step_size and bc2_sqrt, fp32-rounded like c_float
-            out[r, 1] = (1.0 - b2 ** t) ** 0.5
-        return out
-
-    def entry(self, p, t: int):
-        """(table pointer, row of counter = 0) for parameter p's update at step t."""
-        key = id(p)
-        if key not in self._tables:
-            raise RuntimeError("AdamSchedule: a parameter added after the schedule was built (re-capture the step)")
-        self.updates[key] = self.updates.get(key, 0) + 1
-        return self._tables[key].data_ptr(), t - self._t0[key]
-
-    def reset_updates(self):
-        self.updates = {}
-
-    def shift(self, n: int):
-        """Slide every table n steps forward and take n off the device counter (stream-ordered, between replays)."""
-        for key, tab in self._tables.items():
-            self._t0[key] += n
-            tab.copy_(torch.from_numpy(self._host_table(self._groups[key], self._t0[key])))
-        self.counter.sub_(n)
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -74,9 +18,6 @@ class FusedAdam(torch.optim.Optimizer):
         if lr < 0 or eps < 0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps))
-        # an AdamSchedule while a training step is being captured into a hipGraph (gstex_amd.graphs): the launches then
-        # read their bias corrections from its device tables (gstex_adam_step_scheduled)
-        self.schedule = None
 
     @torch.no_grad()
     def step(self, closure=None, only=None, skip=None, zero_grad=False, grid=0, grad_scale=1.0, skip_flag=None):
@@ -125,8 +66,7 @@ class FusedAdam(torch.optim.Optimizer):
                 desc = _lib.GstexAdamTensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
                                             st["exp_avg_sq"].data_ptr(), p.numel(), step_size, bc2_sqrt)
                 key = (b1, b2, group["eps"], p.device)
-                sched = self.schedule.entry(p, t) if self.schedule is not None else None
-                batches.setdefault(key, []).append((desc, sched))
+                batches.setdefault(key, []).append(desc)
         self._launch(batches, zero_grad, grid, grad_scale, skip_flag)
         return loss
 
@@ -160,25 +100,16 @@ class FusedAdam(torch.optim.Optimizer):
         o = 4 * lo
         desc = _lib.GstexAdamTensor(p.data_ptr() + o, g.data_ptr() + o, st["exp_avg"].data_ptr() + o,
                                     st["exp_avg_sq"].data_ptr() + o, hi - lo, step_size, bc2_sqrt)
-        if self.schedule is not None:
-            raise RuntimeError("FusedAdam.step_range: not supported inside a captured step (StepGraphs is single-GPU)")
-        self._launch({(b1, b2, group["eps"], p.device): [(desc, None)]}, zero_grad, 0, grad_scale, skip_flag)
+        self._launch({(b1, b2, group["eps"], p.device): [desc]}, zero_grad, 0, grad_scale, skip_flag)
 
     def _launch(self, batches, zero_grad, grid, grad_scale, skip_flag=None):
         for (b1, b2, eps, dev), items in batches.items():
             st = _lib.stream_of(dev)
             for i in range(0, len(items), _lib.ADAM_MAX_TENSORS):
                 chunk = items[i:i + _lib.ADAM_MAX_TENSORS]
-                arr = (_lib.GstexAdamTensor * len(chunk))(*[d for d, _ in chunk])
+                arr = (_lib.GstexAdamTensor * len(chunk))(*chunk)
                 flags = (_lib.ADAM_ZERO_GRAD if zero_grad else 0) | ((int(grid) & 0xFFFF) << _lib.ADAM_GRID_SHIFT)
-                if chunk[0][1] is not None:  # captured step: bias corrections from the AdamSchedule's tables
-                    sch = _lib.GstexAdamSchedule()
-                    sch.counter = self.schedule.counter.data_ptr()
-                    for j, (_, (tab, base)) in enumerate(chunk):
-                        sch.table[j], sch.base[j], sch.rows[j] = tab, base, self.schedule.rows
-                    _lib.call("gstex_adam_step_scheduled", len(chunk), arr, float(b1), float(b2), float(eps), flags,
-                              float(grad_scale), _lib.ptr(skip_flag), ctypes.byref(sch), st)
-                elif skip_flag is not None:
+                if skip_flag is not None:
                     _lib.call("gstex_adam_step_guarded", len(chunk), arr, float(b1), float(b2), float(eps), flags,
                               float(grad_scale), _lib.ptr(skip_flag), st)
                 elif grad_scale != 1.0:

@@ -22,7 +22,7 @@
  *   - Every pointer is a DEVICE pointer to contiguous row-major fp32 / int32 memory, except
  *     `const gstex_camera*` which is a HOST struct (read at call time) of device pointers.
  *   - `stream` is a hipStream_t (NULL = default stream). Calls only enqueue work: no allocation,
- *     no host synchronisation, so they are safe to capture in a hipGraph.
+ *     no host synchronisation.
  *   - Scratch memory is caller-owned: query the size with the *_workspace_size function, allocate
  *     it (e.g. with the torch caching allocator) and pass it in.
  *   - Return value: 0 (GSTEX_OK) or a gstex_status; the message of the last failure on the calling
@@ -38,7 +38,9 @@
 extern "C" {
 #endif
 
-#define GSTEX_ABI_VERSION 17
+/* ABI 18 (round 6): the hipGraph step support of ABI 16 (event-record nodes, gstex_adam_step_scheduled) and the
+ * split-backward settings bit of ABI 15 are removed (measured slower). */
+#define GSTEX_ABI_VERSION 18
 
 /* Per-record layout of the splat table written by gstex_raster_setup (floats). */
 #define GSTEX_REC_FLOATS 32
@@ -51,11 +53,6 @@ extern "C" {
 #define GSTEX_SETTING_DIST_REG (1 << 10) /* 2DGS NDC depth-distortion output */
 #define GSTEX_SETTING_EDIT (1 << 13)     /* texture_edit request (gstex.py:599) */
 #define GSTEX_SETTING_EVAL_NORMAL (1 << 15) /* eval normal/edit render (gstex.py:1198): normal output unit-length, forward only */
-/* gstex_raster_bwd only (ABI 15): the split backward for the photometric C = 3 case with float-atomic splat sums
- * (row_flags NULL, no depth / normal / distortion gradient) -- texel gradients by the pixel-major kernel alone, splat
- * gradients by a splat-parallel kernel (one splat per lane, lane scans for transmittance and colour behind).  Same
- * results within fp32 rounding; an experiment kept off by default.  Ignored in every other case. */
-#define GSTEX_BWD_SPLIT (1 << 29)
 /* gstex_raster_fwd / gstex_raster_fwd_zero only (ABI 17): the aux span the forward accumulates its unit costs, launch
  * order and unit-order histogram into was zeroed by gstex_train_prologue (args.raster_aux, same n_isect / tiles /
  * channels) on the same stream, so the forward skips its own fill.  Set it only after such a prologue call. */
@@ -171,20 +168,6 @@ int gstex_event_record(void* event, void* stream);
 int gstex_event_elapsed(void* start, void* end, float* ms);
 int gstex_stream_wait_event(void* stream, void* event);
 int gstex_event_destroy(void* event);
-/* HIP-graph support (ABI 16; not in the reference, which has no graph capture).  A training step captured into a
- * hipGraph (gstex_amd.graphs.StepGraphs) times its raster kernels with event-record nodes:
- *   gstex_event_record_external: on a capturing stream, an event-record node appended to the graph after the
- *     capture's current dependencies (what hipEventRecordExternal specifies; a plain record there only orders the
- *     capture); on any other stream a plain record;
- *   gstex_graph_event_nodes: nodes[i] = the event-record node of `graph` (a hipGraph_t) recording events[i]; an event no
- *     node records is an error;
- *   gstex_graph_exec_set_event: point that node of the instantiated graph `exec` (a hipGraphExec_t) at another event
- *     (a fresh timing pair per replay). */
-int gstex_event_record_external(void* event, void* stream);
-int gstex_graph_event_nodes(void* graph, void* const* events, int32_t n, void** nodes);
-int gstex_graph_exec_set_event(void* exec, void* node, void* event);
-/* hipGraphUpload of an instantiated graph on `stream` (its first launch then pays no upload). */
-int gstex_graph_upload(void* exec, void* stream);
 int gstex_scan_offsets_guarded(int32_t n, const int32_t* num_tiles_hit, int32_t* offsets, void* workspace,
                                size_t workspace_bytes, const gstex_pair_guard* guard, void* stream);
 int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* centers, const float* extents,
@@ -409,21 +392,6 @@ int gstex_adam_step_scaled(int32_t n_tensors, const gstex_adam_tensor* tensors, 
  * data-parallel training so that every rank skips the same steps.  ABI 13. */
 int gstex_adam_step_guarded(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
                             double eps, int32_t flags, float grad_scale, const float* skip, void* stream);
-/* gstex_adam_step_guarded whose per-tensor step_size and bias_correction2_sqrt are read on the device (ABI 16): for
- * tensor i, row base[i] + *counter of table[i] (float pairs (step_size, bias_correction2_sqrt), rows[i] of them, the
- * row index clamped to the table).  For a hipGraph replayed many times (gstex_amd.graphs.StepGraphs): the host keeps
- * the tables (the same python-double bias corrections the per-call entry points take, one row per step t) and the
- * graph advances *counter once per replay, so replay r applies the bias corrections of step t0 + r.  The tensors'
- * step_size / bias_correction2_sqrt fields are ignored. */
-typedef struct gstex_adam_schedule {
-    const int32_t* counter;
-    const float* table[GSTEX_ADAM_MAX_TENSORS];
-    int32_t base[GSTEX_ADAM_MAX_TENSORS];
-    int32_t rows[GSTEX_ADAM_MAX_TENSORS];
-} gstex_adam_schedule;
-int gstex_adam_step_scheduled(int32_t n_tensors, const gstex_adam_tensor* tensors, double beta1, double beta2,
-                              double eps, int32_t flags, float grad_scale, const float* skip,
-                              const gstex_adam_schedule* schedule, void* stream);
 
 /* ---- training-step prologue (ABI 17; not in the reference) ------------------------------------------------------
  * One host call for the launches a photometric training render makes before its raster forward: the outputs of

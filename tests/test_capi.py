@@ -37,7 +37,7 @@ def test_every_header_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.gstex_abi_version() == _lib.ABI_VERSION == 17
+    assert lib.gstex_abi_version() == _lib.ABI_VERSION == 18
 
 
 def test_workspace_size_queries(lib):
@@ -169,7 +169,7 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
 
     structs = {"gstex_camera": _lib.GstexCamera, "gstex_pair_guard": _lib.GstexPairGuard,
-               "gstex_adam_tensor": _lib.GstexAdamTensor, "gstex_adam_schedule": _lib.GstexAdamSchedule,
+               "gstex_adam_tensor": _lib.GstexAdamTensor,
                "gstex_train_prologue_args": _lib.GstexTrainPrologueArgs,
                "gstex_train_epilogue_args": _lib.GstexTrainEpilogueArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gstex_hip.h"', "int main(void) {"]

@@ -379,6 +379,46 @@ def test_pair_capacity_overflow_skips_the_update_and_grows(request, det):
     assert any(not torch.equal(p, q.detach()) for p, q in zip(before, tr.parameters()))
 
 
+def test_fused_overflow_does_not_skip_later_steps():
+    """the fused training render's pair guard must reset the step's flag at its first render even when the
+    double-buffered texel gradient needs no zeroing (the previous backward zeroed it).  A fused step that overflows
+    is skipped; the eight fused steps after it -- including step s + 8, which reuses its step_control slot -- update."""
+    from gstex_amd import ops
+    from gstex_amd.model import GStexTrainer
+    from gstex_amd.scene import make_scene, sphere_view
+
+    dev = torch.device("cuda", 0)
+    sc = make_scene(3000, 60_000, seed=23)
+    view = sphere_view(0, 96, 96).to(dev)
+    gt = torch.rand((96, 96, 3), generator=torch.Generator().manual_seed(10)).to(dev)
+    tr = GStexTrainer(sc, dev, start_step=3000, defer_texture=True)
+    tr.pairs = ops.PairCapacity(dev, capacity=1000)  # far below this scene's ~20k pairs
+    assert tr._fused_ok(False, None) and tr._double_buffered()
+
+    def step():
+        tr.zero_grad()
+        tr.forward_backward(view, gt)
+        tr.optimizer_step()
+        tr.wait_texture()
+        torch.cuda.synchronize()
+
+    before = [p.detach().clone() for p in tr.parameters()]
+    step()  # step 3000: overflows on the fused path
+    for p, q in zip(before, tr.parameters()):
+        assert torch.equal(p, q.detach()), "an overflowed fused step changed a parameter"
+    with pytest.warns(UserWarning, match="exceeded the pair capacity"):
+        tr._poll_pairs()
+    assert tr.skipped_steps == [3000]
+    for k in range(1, 10):  # steps 3001 .. 3009; 3008 uses the overflowed step's flag slot
+        prev = [p.detach().clone() for p in tr.parameters()]
+        step()
+        assert float(tr.step_control[(tr.step - 1) % 8]) == 0.0, f"step {tr.step - 1}'s guard flag left set"
+        assert all(not torch.equal(p, q.detach()) for p, q in zip(prev, tr.parameters())
+                   if q.grad is not None), f"fused step {tr.step - 1} was skipped"
+    tr._poll_pairs()
+    assert tr.skipped_steps == [3000]
+
+
 def test_two_renders_per_step_under_overlapped_gradsync():
     """gradient accumulation over two views per step with the default overlapped exchange (a trainer that
     does not defer its texel update, the tail's collective started from the first raster backward): the second render
