@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("GSTEX_LIB") or os.path.join(os.path.dirname(os.path.a
 
 ABI_VERSION = 18
 REC_FLOATS = 32
+HP_DOUBLES = 12  # GSTEX_HP_DOUBLES: the fp64 row of a near-edge-on splat (gstex_raster_setup hp_records)
 PARTIAL_FLOATS = 32  # GSTEX_PARTIAL_FLOATS: floats between partial rows of a backward with geometry gradients
 PARTIAL_FLOATS_PHOTO = 24  # GSTEX_PARTIAL_FLOATS_PHOTO: ... without (the photometric training step)
 SETTING_AA_BLUR = 1 << 9
@@ -76,7 +77,7 @@ class GstexTrainPrologueArgs(ctypes.Structure):
         (name, c_void_p) for name in (
             "records", "tile_ranges", "sorted_ids", "sorted_slots", "tile_order", "bin_workspace")] + [
         ("bin_workspace_bytes", c_size_t), ("raster_aux", c_void_p), ("raster_aux_bytes", c_size_t),
-        ("raster_channels", c_int32)]
+        ("raster_channels", c_int32), ("hp_records", c_void_p)]
 
 
 class GstexTrainEpilogueArgs(ctypes.Structure):
@@ -129,7 +130,7 @@ SIGNATURES = {
     "gstex_event_destroy": (c_int32, [c_void_p]),
     "gstex_raster_setup": (
         c_int32,
-        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P],
+        [c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P, _P, _CAM, _P, _P, _P],
     ),
     "gstex_raster_fwd": (
         c_int32,
@@ -146,12 +147,12 @@ SIGNATURES = {
     "gstex_unit_order_scratch_words": (c_size_t, []),
     "gstex_raster_bwd": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, _P, _P, _P],
     ),
     "gstex_raster_bwd_zero": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, _P, _P, _P, c_int64, _P],
     ),
     "gstex_raster_setup_bwd": (

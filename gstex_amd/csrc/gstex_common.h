@@ -347,6 +347,19 @@ enum RecField {
 };
 constexpr int kCullPlanes = 3;  // record planes holding the cull fields
 
+// Near-edge-on splats (|normal . view direction| < kHpCos at the splat centre): their homogeneous point p = dx A + dy B +
+// (0, 0, Pz) is ill-conditioned in the fp32 record (p.z is a small difference of larger terms), and with it u = p.x / p.z,
+// v = p.y / p.z and every means / quats gradient through them.  When the caller passes a row buffer, the
+// setup marks such a splat by the sign bit of its record opacity (R_OPAC < 0; every reader takes |R_OPAC|) and writes
+// the fp64 values of its affine homography and depth row (HpField) into row g of that buffer; the backward re-evaluates
+// dx, dy, p, 1 / p.z, u, v, rho3 and z of those pairs in fp64 (every pair decision stays the fp32 forward's).
+#ifndef GSTEX_HP_COS
+#define GSTEX_HP_COS 0.1
+#endif
+constexpr double kHpCos = GSTEX_HP_COS;
+enum HpField { H_A = 0, H_B = 3, H_PZ = 6, H_XA = 7, H_YA = 8, H_TW = 9, H_FIELDS = 12 };
+static_assert(H_FIELDS == GSTEX_HP_DOUBLES, "gstex_hip.h GSTEX_HP_DOUBLES");
+
 // Screen box of the projected disc u^2 + v^2 <= c2 (compute_aabb with a general cutoff).
 // Returns false when the disc reaches the camera plane (unbounded projection).
 __device__ __forceinline__ bool ellipse_box(const Homog& h, float c2, float& x0, float& x1, float& y0,

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
                                                     const float* __restrict__ vmap,
                                                     const int32_t* __restrict__ tdims,
                                                     const int32_t* __restrict__ nth, CamArgs cam_args,
-                                                    float* __restrict__ rec_out) {
+                                                    float* __restrict__ rec_out, double* __restrict__ hp_out) {
     const Camera cam = load_camera(cam_args);
     int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
@@ -108,7 +108,8 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
     // the record, in fp64 (splat_math.h: the function the training prologue's fused kernel also calls)
     splat_record(cam, means[3 * g], means[3 * g + 1], means[3 * g + 2], scales[3 * g], scales[3 * g + 1], glob,
                  quats + 4 * g, rgbs + 3 * g, opacities[g], centers[2 * g], centers[2 * g + 1], uv0 + 2 * g,
-                 umap + 3 * g, vmap + 3 * g, tdims + 3 * g, rec_out + (size_t)g * GSTEX_REC_FLOATS);
+                 umap + 3 * g, vmap + 3 * g, tdims + 3 * g, rec_out + (size_t)g * GSTEX_REC_FLOATS,
+                 hp_out ? hp_out + (size_t)g * H_FIELDS : nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -136,7 +137,7 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.Pz = v[R_PZ];
     r.Tw = f3{v[R_TW], v[R_TW + 1], v[R_TW + 2]};
     r.x = v[R_XY]; r.y = v[R_XY + 1];
-    r.opac = v[R_OPAC];
+    r.opac = fabsf(v[R_OPAC]);  // (sign bit: the near-edge-on mark, gstex_common.h kHpCos)
     r.rgb[0] = v[R_RGB]; r.rgb[1] = v[R_RGB + 1]; r.rgb[2] = v[R_RGB + 2];
     r.tu0 = v[R_TU0]; r.auu = v[R_AUU]; r.auv = v[R_AUV]; r.tv0 = v[R_TV0]; r.avu = v[R_AVU]; r.avv = v[R_AVV];
     r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = __float_as_int(v[R_OFF]);
@@ -283,7 +284,7 @@ __device__ __forceinline__ bool conic_edge(float ax, float ay, float az, float q
 __device__ __forceinline__ bool may_hit_planes(float4 p0, float4 p1, float4 p2, float wx0, float wx1, float wy0,
                                                float wy1, bool aa) {
     const float v[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
-    const float opac = v[R_OPAC];
+    const float opac = fabsf(v[R_OPAC]);
     if (!(opac * 255.0f > 1.0f)) return false;
     const float rm = 2.0f * logf(255.0f * opac) * 1.01f + 1e-2f;
     const float x0 = wx0 - 0.05f, x1 = wx1 + 0.05f, y0 = wy0 - 0.05f, y1 = wy1 + 0.05f;
@@ -374,6 +375,47 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     h.a_raw = r.opac * h.G;
     h.alpha = fminf(kAlphaMax, h.a_raw);
     return ok && h.z >= kNear && h.alpha >= kAlphaMin;  // oracle/raster.py: nz & (zz >= near) & (alpha >= amin)
+}
+
+// A near-edge-on splat's pair re-evaluated from its fp64 setup row (gstex_common.h kHpCos): dx, dy, p, 1 / p.z, u, v,
+// rho3 and (GEO) the depth in fp64, each rounded once; G, alpha from the refined rho.  Every decision stays the fp32
+// evaluation's (the forward's): contributing or not, the low-pass branch (use3) and the alpha clamp.  The row is read
+// at a wave-uniform address (scalar loads).
+// (read as vector buffer loads: the row's 24 dwords would not fit beside the record in the kernel's SGPR budget)
+__device__ __forceinline__ double hp_load(__amdgpu_buffer_rsrc_t rs, int k) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, k * 8, 0, 0));
+}
+template <bool GEO>
+__device__ __forceinline__ void refine_hit_hp(const Rec& r, const double* __restrict__ row, float px, float py,
+                                              Hit& h) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(row), 0, H_FIELDS * 8,
+                                                                        0x00020000);
+    double hr[H_FIELDS];
+#pragma unroll
+    for (int k = 0; k < H_FIELDS; ++k) hr[k] = (GEO || k < H_TW) ? hp_load(rs, k) : 0.0;
+    const double dx = (double)px - hr[H_XA], dy = (double)py - hr[H_YA];
+    const double p0 = __builtin_fma(dx, hr[H_A], dy * hr[H_B]);
+    const double p1 = __builtin_fma(dx, hr[H_A + 1], dy * hr[H_B + 1]);
+    const double p2 = __builtin_fma(dy, hr[H_B + 2], __builtin_fma(dx, hr[H_A + 2], hr[H_PZ]));
+    const double ipz = 1.0 / p2;
+    const double u = p0 * ipz, v = p1 * ipz;
+    h.dx = (float)dx;
+    h.dy = (float)dy;
+    h.p = f3{(float)p0, (float)p1, (float)p2};
+    h.ipz = (float)ipz;
+    h.u = (float)u;
+    h.v = (float)v;
+    h.rho3 = (float)__builtin_fma(u, u, v * v);
+    if (GEO && h.use3) h.z = (float)__builtin_fma(u, hr[H_TW], __builtin_fma(v, hr[H_TW + 1], hr[H_TW + 2]));
+    const float rho = h.use3 ? h.rho3 : h.rho2;
+#if GSTEX_FAST_EVAL
+    h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);
+#else
+    h.G = exp_nonpos(-0.5f * rho);
+#endif
+    const bool clamped = !(h.a_raw < kAlphaMax);  // the fp32 decision (fminf(0.99, a_raw) took 0.99)
+    h.a_raw = clamped ? h.a_raw : fminf(r.opac * h.G, 0.98999995f);
+    h.alpha = clamped ? kAlphaMax : h.a_raw;
 }
 
 // One texel's channels: with C == 3 a single 12-B global_load_dwordx3 (the three channels share a cache
@@ -947,7 +989,7 @@ static_assert(kTexStage % (64 * kFlushU) == 0, "flush passes tile the staging ar
 template <int C, bool GEO>
 __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
-    const float4* __restrict__ records, const int2* __restrict__ tile_ranges,
+    const float4* __restrict__ records, const double* __restrict__ hp_records, const int2* __restrict__ tile_ranges,
     const int32_t* __restrict__ sorted_ids, const int32_t* __restrict__ sorted_slots, const float* __restrict__ texture,
     int n_texels, float tex_scale, float tex_bias, const float4* __restrict__ state, const float* __restrict__ v_img,
     const float* __restrict__ v_depth, const float* __restrict__ v_reg, const float* __restrict__ v_alpha,
@@ -1067,10 +1109,14 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             todo &= ~(1ull << j);
             const int rel = pos0 + j;
             const int gid = __builtin_amdgcn_readlane(my_gid, j);
-            const Rec r = read_rec_global(records + (size_t)gid * kRecF4);
+            const float4* rp = records + (size_t)gid * kRecF4;
+            const Rec r = read_rec_global(rp);
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
+            // a near-edge-on splat (the record opacity's sign bit): its pairs' values in fp64, the decisions kept
+            if (hp_records && __float_as_int(rp[2].w) < 0)
+                refine_hit_hp<GEO>(r, hp_records + (size_t)gid * H_FIELDS, px, py, h);
             GSTEX_STAT(1, 1);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
@@ -1696,7 +1742,7 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
                                   const float* quats, const float* rgbs, const float* opacities,
                                   const float* centers, const float* uv0, const float* umap, const float* vmap,
                                   const int32_t* texture_dims, const int32_t* num_tiles_hit,
-                                  const gstex_camera* cam, float* records, void* stream) {
+                                  const gstex_camera* cam, float* records, double* hp_records, void* stream) {
     GSTEX_REQUIRE(n >= 0 && cam, "gstex_raster_setup: invalid arguments");
     if (n == 0) return GSTEX_OK;
     GSTEX_REQUIRE(means && scales && quats && rgbs && opacities && centers && uv0 && umap && vmap &&
@@ -1704,7 +1750,8 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
                   "gstex_raster_setup: null pointer");
     setup_kernel<<<div_up(n, 256), 256, 0, as_stream(stream)>>>(n, means, scales, glob_scale, quats, rgbs, opacities,
                                                                  centers, uv0, umap, vmap, texture_dims,
-                                                                 num_tiles_hit, to_device_camera(*cam), records);
+                                                                 num_tiles_hit, to_device_camera(*cam), records,
+                                                                 hp_records);
     return launch_status("gstex_raster_setup");
 }
 
@@ -1775,7 +1822,7 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
 
 namespace {
 int raster_bwd_impl(const gstex_camera* cam, int32_t channels, int32_t settings, const float* background,
-                    const float* records, const int32_t* tile_ranges, const int32_t* sorted_ids,
+                    const float* records, const double* hp_records, const int32_t* tile_ranges, const int32_t* sorted_ids,
                     const int32_t* sorted_slots, const float* texture, int64_t n_texels, float tex_scale,
                     float tex_bias, const float* state, const float* v_img, const float* v_depth, const float* v_reg,
                     const float* v_alpha, const float* v_tex, const float* v_normal, int64_t n_isect, float* partials,
@@ -1806,8 +1853,8 @@ int raster_bwd_impl(const gstex_camera* cam, int32_t channels, int32_t settings,
     const bool geo = v_depth || v_normal || (v_reg && (settings & GSTEX_SETTING_DIST_REG));
 #define GSTEX_BWD(CC, GG)                                                                                      \
     raster_bwd_kernel<CC, GG><<<(unsigned)al.n_units, 64, 0, st>>>(                                            \
-        dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
-        sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
+        dc, tiles_x, settings, background, channels, (const float4*)records, hp_records,                      \
+        (const int2*)tile_ranges, sorted_ids, sorted_slots, texture, (int)n_texels, tex_scale, tex_bias, (const float4*)state,           \
         v_img, v_depth, v_reg, v_alpha, v_tex, v_normal, partials, (unsigned char*)row_flags, v_texture, ap,   \
         zbuf)
     if (channels == 3 && !geo) GSTEX_BWD(3, false);
@@ -1822,21 +1869,23 @@ int raster_bwd_impl(const gstex_camera* cam, int32_t channels, int32_t settings,
 }  // namespace
 
 extern "C" int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
-                                const float* background, const float* records, const int32_t* tile_ranges,
+                                const float* background, const float* records, const double* hp_records,
+                                const int32_t* tile_ranges,
                                 const int32_t* sorted_ids, const int32_t* sorted_slots,
                                 const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
                                 const float* state, const float* v_img,
                                 const float* v_depth, const float* v_reg, const float* v_alpha, const float* v_tex,
                                 const float* v_normal, int64_t n_isect, float* partials, uint32_t* row_flags,
                                 float* v_texture, void* aux, void* stream) {
-    return raster_bwd_impl(cam, channels, settings, background, records, tile_ranges, sorted_ids, sorted_slots,
+    return raster_bwd_impl(cam, channels, settings, background, records, hp_records, tile_ranges, sorted_ids, sorted_slots,
                            texture, n_texels, tex_scale, tex_bias, state, v_img, v_depth, v_reg, v_alpha, v_tex,
                            v_normal, n_isect, partials, row_flags, v_texture, aux, ZeroBufs{{nullptr, nullptr}, {0, 0}},
                            stream);
 }
 
 extern "C" int gstex_raster_bwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
-                                     const float* background, const float* records, const int32_t* tile_ranges,
+                                     const float* background, const float* records, const double* hp_records,
+                                     const int32_t* tile_ranges,
                                      const int32_t* sorted_ids, const int32_t* sorted_slots,
                                      const float* texture, int64_t n_texels, float tex_scale, float tex_bias,
                                      const float* state, const float* v_img,
@@ -1846,7 +1895,7 @@ extern "C" int gstex_raster_bwd_zero(const gstex_camera* cam, int32_t channels, 
                                      int64_t zero_floats, void* stream) {
     GSTEX_REQUIRE(zero_floats >= 0 && (zero_floats == 0 || zero_buf) && zero_buf != v_texture,
                   "gstex_raster_bwd_zero: invalid zero_buf / zero_floats (it must not be the gradient accumulated)");
-    return raster_bwd_impl(cam, channels, settings, background, records, tile_ranges, sorted_ids, sorted_slots,
+    return raster_bwd_impl(cam, channels, settings, background, records, hp_records, tile_ranges, sorted_ids, sorted_slots,
                            texture, n_texels, tex_scale, tex_bias, state, v_img, v_depth, v_reg, v_alpha, v_tex,
                            v_normal, n_isect, partials, row_flags, v_texture, aux,
                            ZeroBufs{{zero_floats > 0 ? zero_buf : nullptr, nullptr}, {zero_floats, 0}}, stream);

@@ -120,7 +120,8 @@ __device__ __forceinline__ Preprocessed preprocess_splat(const Camera& cam, f3 m
 __device__ __forceinline__ void splat_record(const Camera& cam, float mx, float my, float mz, float s0, float s1,
                                              float glob, const float* q4, const float* rgb, float opac, float cx,
                                              float cy, const float* uv0, const float* um3, const float* vm3,
-                                             const int32_t* td, float* __restrict__ rec_out) {
+                                             const int32_t* td, float* __restrict__ rec_out,
+                                             double* __restrict__ hp_out = nullptr) {
     const FrameT<double> fr = quat_frame_t<double>(q4);
     const double su = (double)s0 * (double)glob, sv = (double)s1 * (double)glob;
     const d3 mu = d3{(double)mx, (double)my, (double)mz};
@@ -137,6 +138,17 @@ __device__ __forceinline__ void splat_record(const Camera& cam, float mx, float 
     r[R_TW + 0] = (float)h.Tw.x; r[R_TW + 1] = (float)h.Tw.y; r[R_TW + 2] = (float)h.Tw.z;
     r[R_XY + 0] = cx; r[R_XY + 1] = cy;
     r[R_OPAC] = opac;
+    if (hp_out) {
+        // near edge-on (gstex_common.h kHpCos): the fp64 row for the backward, flagged by the opacity's sign bit
+        const double dn = sqrt(dot3(dir, dir));
+        if (fabs(dot3(fr.tw, dir)) < kHpCos * dn) {
+            r[R_OPAC] = -opac;
+            const double v[H_FIELDS] = {ah.A.x, ah.A.y, ah.A.z, ah.B.x, ah.B.y, ah.B.z, ah.Pz, h.xa, h.ya,
+                                        h.Tw.x, h.Tw.y, h.Tw.z};
+#pragma unroll
+            for (int k = 0; k < H_FIELDS; ++k) hp_out[k] = v[k];
+        }
+    }
     r[R_RGB + 0] = rgb[0]; r[R_RGB + 1] = rgb[1]; r[R_RGB + 2] = rgb[2];
     r[R_NRM + 0] = (float)(sgn * fr.tw.x); r[R_NRM + 1] = (float)(sgn * fr.tw.y); r[R_NRM + 2] = (float)(sgn * fr.tw.z);
     // the texture affine in texel units: the sample point (tu h, tv w) = (tu0 + auu u + auv v) h, ... is read as

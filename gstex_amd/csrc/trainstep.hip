@@ -42,7 +42,8 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
     float* __restrict__ opacities, float* __restrict__ uv0, float* __restrict__ umap, float* __restrict__ vmap,
     float* __restrict__ viewdirs, float* __restrict__ depths, float* __restrict__ centers,
     float* __restrict__ extents, int32_t* __restrict__ nth, float* __restrict__ rgbs,
-    const int32_t* __restrict__ tdims, float* __restrict__ records, int32_t* __restrict__ block_sums) {
+    const int32_t* __restrict__ tdims, float* __restrict__ records, double* __restrict__ hp_records,
+    int32_t* __restrict__ block_sums) {
     extern __shared__ float s_c[];
     __shared__ int s_wave[kSplatBlock / 64];
     const Camera cam = load_camera(cam_args);
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(kSplatBlock) void train_splat_kernel(
             const float uv[2] = {0.5f, 0.5f};
             const int32_t td[3] = {tdims[3 * i], tdims[3 * i + 1], tdims[3 * i + 2]};
             splat_record(cam, mx, my, mz, a.s0, a.s1, 1.0f, a.q, rgb, a.opacity, p.cx, p.cy, uv, a.um, a.vm, td,
-                         records + (size_t)i * GSTEX_REC_FLOATS);
+                         records + (size_t)i * GSTEX_REC_FLOATS, hp_records ? hp_records + (size_t)i * H_FIELDS : nullptr);
         }
     }
     int total;
@@ -171,7 +172,7 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
             a->n, a->sh_degree, a->n_rest, a->means, a->quats, a->log_scales, a->opac_logits, a->mappings,
             a->map_cols, a->campos, a->features_rest, to_device_camera(a->cam), tx, ty, pre.block, a->quats_n,
             a->scales, a->opacities, a->uv0, a->umap, a->vmap, a->viewdirs, a->depths, a->centers, a->extents,
-            a->num_tiles_hit, a->rgbs, a->texture_dims, a->records, sums);
+            a->num_tiles_hit, a->rgbs, a->texture_dims, a->records, a->hp_records, sums);
         const ScanGuard g{(long long)a->guard.capacity, a->guard.step_flag, a->guard.host_count,
                           a->guard.first ? 1 : 0};
         const ZeroSpan zb = bin_count_span(a->bin_workspace, tx * ty, a->capacity);
@@ -206,7 +207,8 @@ extern "C" int gstex_train_prologue(const gstex_train_prologue_args* a, void* st
     if (rc) return rc;
     if (!fused) {  // (the fused kernel wrote the records)
         rc = gstex_raster_setup(a->n, a->means, a->scales, 1.0f, a->quats_n, a->rgbs, a->opacities, a->centers, a->uv0,
-                                a->umap, a->vmap, a->texture_dims, a->num_tiles_hit, &a->cam, a->records, stream);
+                                a->umap, a->vmap, a->texture_dims, a->num_tiles_hit, &a->cam, a->records,
+                                a->hp_records, stream);
         if (rc) return rc;
     }
     if (fused)  // the tile counters were zeroed by train_scan_kernel

@@ -48,6 +48,7 @@ def _layout(n: int, n_rest: int, capacity: int, H: int, W: int, C: int):
         ("umap", 3 * n * f4), ("vmap", 3 * n * f4), ("viewdirs", 3 * n * f4), ("depths", n * f4),
         ("centers", 2 * n * f4), ("extents", 2 * n * f4), ("num_tiles_hit", n * 4), ("rgbs", 3 * n * f4),
         ("offsets", (n + 1) * 4), ("scan_ws", scan_ws), ("records", REC_FLOATS * n * f4),
+        ("hp", _lib.HP_DOUBLES * n * 8),
         ("tile_ranges", 2 * n_tiles * 4), ("sorted_ids", capacity * 4), ("sorted_slots", capacity * 4),
         ("tile_order", n_tiles * 4), ("bin_ws", bin_ws),
         ("img", 3 * H * W * f4), ("alpha", H * W * f4), ("tex", C * H * W * f4), ("state", 4 * H * W * f4),
@@ -113,7 +114,8 @@ class _TrainRender(torch.autograd.Function):
             scan_workspace_bytes=sizes["scan_ws"], records=P["records"], tile_ranges=P["tile_ranges"],
             sorted_ids=P["sorted_ids"], sorted_slots=P["sorted_slots"], tile_order=P["tile_order"],
             bin_workspace=P["bin_ws"], bin_workspace_bytes=sizes["bin_ws"],
-            raster_aux=P["aux"] if sizes["aux"] else None, raster_aux_bytes=sizes["aux"], raster_channels=C)
+            raster_aux=P["aux"] if sizes["aux"] else None, raster_aux_bytes=sizes["aux"], raster_channels=C,
+            hp_records=P["hp"] if ops.HP_RECORDS else None)
         _lib.call("gstex_train_prologue", ctypes.byref(a), st)
         pcap.commit(slot, cap, tr.step, dev)
         if texture_ready is not None:  # the deferred texel update waiting for its collective: the raster forward
@@ -149,7 +151,7 @@ class _TrainRender(torch.autograd.Function):
         v_img, v_alpha, v_tex = c(v_img), c(v_alpha), c(v_tex)
         texture = tr.texture_dc
         bwd_args = (cam, 3, int(tr.settings), ptr(tr._bg_zero),
-                    P["records"], P["tile_ranges"], P["sorted_ids"], P["sorted_slots"], ptr(texture),
+                    P["records"], P["hp"] if ops.HP_RECORDS else None, P["tile_ranges"], P["sorted_ids"], P["sorted_slots"], ptr(texture),
                     texture.shape[0], SH_C0, 0.5, P["state"], ptr(v_img), None, None, ptr(v_alpha), ptr(v_tex), None,
                     ctx.cap, P["partials"], None, ptr(ctx.sink), P["aux"] if ctx.has_aux else None)
         zn = ctx.zero_next

@@ -8,6 +8,7 @@ path: inputs must be HIP tensors, and a missing library raises (see gstex_amd/_l
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 from typing import NamedTuple, Tuple
 
@@ -17,6 +18,9 @@ from . import _lib
 from ._lib import PARTIAL_FLOATS, PARTIAL_FLOATS_PHOTO, REC_FLOATS, call, ptr
 
 BLOCK_WIDTH = 16
+# near-edge-on splats re-evaluated in fp64 by the raster backward (gstex_raster_setup / gstex_raster_bwd hp_records,
+# ABI 18); GSTEX_HP=0 evaluates every pair in fp32 (the round-5 numerics)
+HP_RECORDS = os.environ.get("GSTEX_HP", "1") != "0"
 
 # ----------------------------------------------------------------------------------------
 # optional per-kernel timing: HIP events recorded on the stream each kernel is launched on
@@ -527,9 +531,12 @@ class _TextureGaussians(torch.autograd.Function):
         # backward-only buffers only when a backward can follow: not under torch.no_grad() (eval renders of
         # trainable parameters), where apply() records no graph whatever the inputs' requires_grad
         needs_bwd = bool(grad_enabled) and any(ctx.needs_input_grad)
+        # the near-edge-on splats' fp64 rows (only when a backward can follow: it is their only reader)
+        hp = torch.empty((n, _lib.HP_DOUBLES), device=dev, dtype=torch.float64) if needs_bwd and HP_RECORDS else None
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
                 ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam,
-                ptr(records), st)
+                ptr(records), ptr(hp), st)
+        ctx.hp = hp
         ctx.v_texture = None
         ctx.sink = texture_grad_sink is not None
         ctx.on_texture_grad = on_texture_grad
@@ -650,12 +657,13 @@ class _TextureGaussians(torch.autograd.Function):
             row_flags = None
         v_texture = ctx.v_texture if ctx.v_texture is not None else torch.zeros_like(texture)
         ctx.v_texture = None
-        _launch("gstex_raster_bwd", cam, C, int(settings), ptr(bg), ptr(records),
+        _launch("gstex_raster_bwd", cam, C, int(settings), ptr(bg), ptr(records), ptr(ctx.hp),
                 ptr(tile_ranges),
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
                 ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)
         ctx.aux = None
+        ctx.hp = None
         if ctx.sink:
             if ctx.on_texture_grad is not None:
                 ctx.on_texture_grad()  # the texel gradient is complete in stream order
@@ -894,7 +902,8 @@ def texture_edit(texture_info, texture_dims, edit_rgb, edit_alpha, depth_lower, 
     records = torch.empty((n, REC_FLOATS), device=dev, dtype=torch.float32)
     zeros3 = torch.zeros((n, 3), device=dev, dtype=torch.float32)  # colours do not enter the edit
     _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(zeros3),
-            ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records), st)
+            ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam, ptr(records), None,
+            st)
     _launch("gstex_texture_edit", cam, int(settings), ptr(records), ptr(tile_ranges), ptr(order), ptr(sorted_ids),
             ptr(rgb), ptr(a), ptr(dlo), ptr(dhi), n_texels, ptr(out), st)
     return out

@@ -47,6 +47,8 @@ extern "C" {
 /* Per-(tile, splat, quadrant) gradient partial row written by gstex_raster_bwd (floats). */
 #define GSTEX_PARTIAL_FLOATS 32
 #define GSTEX_PARTIAL_FLOATS_PHOTO 24
+/* Per-splat fp64 row of a near-edge-on splat written by gstex_raster_setup into hp_records (doubles, ABI 18). */
+#define GSTEX_HP_DOUBLES 12
 
 /* settings bitfield (GStexModelConfig.settings, gstex.py:194-197) */
 #define GSTEX_SETTING_AA_BLUR (1 << 9)   /* 2DGS screen-space low-pass */
@@ -184,13 +186,18 @@ int gstex_bin_sort_capped(int32_t n, int64_t capacity, const float* centers, con
 int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int32_t* tile_order, void* stream);
 
 /* ---- rasterizer --------------------------------------------------------------------- */
-/* Builds the per-splat raster record table records[n][GSTEX_REC_FLOATS]. */
+/* Builds the per-splat raster record table records[n][GSTEX_REC_FLOATS].
+ * hp_records (ABI 18; nullable = none): a device double[n][GSTEX_HP_DOUBLES] buffer.  A splat whose normal is within
+ * ~6 degrees of edge-on to its view direction (|n . d| < 0.1) is then marked near edge-on -- the sign bit of its
+ * record opacity is set (every kernel reads the magnitude) -- and its row g receives the fp64 affine homography (A, B,
+ * Pz), anchor and depth row; other rows are not written.  Pass the same buffer to gstex_raster_bwd(_zero), which
+ * re-evaluates those splats' pairs from it in fp64 (their fp32 evaluation is ill-conditioned). */
 int gstex_raster_setup(int32_t n, const float* means, const float* scales, float glob_scale,
                        const float* quats, const float* rgbs, const float* opacities,
                        const float* centers, const float* uv0, const float* umap,
                        const float* vmap, const int32_t* texture_dims,
                        const int32_t* num_tiles_hit, const gstex_camera* cam, float* records,
-                       void* stream);
+                       double* hp_records, void* stream);
 /* Texel values: the texels are read as tex_scale * texture + tex_bias (1, 0 = as stored), so a caller
  * that keeps SH-DC coefficients (gstex.py:1119 passes SH2RGB(texture_dc) = 0.28209 x + 0.5) can pass the
  * store itself; the backward's v_texture is then the gradient w.r.t. the stored values. */
@@ -243,9 +250,12 @@ size_t gstex_unit_order_scratch_words(void);
  * row_flags == NULL (ABI 9, the fast mode): instead of rows, every (pair, quadrant) sum is added with float
  * atomics into partials[g * R ...], an (n_splats, R) accumulator the caller has zeroed -- no per-pair rows, no
  * summing pass in setup_bwd; the splat gradients then depend on the atomics' order in their last bits (as the
- * texel gradients always do).  With row_flags the splat gradients are bitwise reproducible. */
+ * texel gradients always do).  With row_flags the splat gradients are bitwise reproducible.
+ * hp_records (ABI 18, nullable): gstex_raster_setup's fp64 rows; the pairs of the splats it marked are then
+ * re-evaluated in fp64 for the gradient (NULL: every pair in fp32, the marks ignored). */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
-                     const float* background, const float* records, const int32_t* tile_ranges,
+                     const float* background, const float* records, const double* hp_records,
+                     const int32_t* tile_ranges,
                      const int32_t* sorted_ids, const int32_t* sorted_slots, const float* texture,
                      int64_t n_texels, float tex_scale, float tex_bias, const float* state,
                      const float* v_img, const float* v_depth, const float* v_reg, const float* v_alpha,
@@ -256,7 +266,8 @@ int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings
  * the other buffer, which the next step's backward accumulates into) -- instead of the forward's zeroing
  * (gstex_raster_fwd_zero).  zero_buf must not be v_texture. */
 int gstex_raster_bwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings, const float* background,
-                          const float* records, const int32_t* tile_ranges, const int32_t* sorted_ids,
+                          const float* records, const double* hp_records, const int32_t* tile_ranges,
+                          const int32_t* sorted_ids,
                           const int32_t* sorted_slots, const float* texture, int64_t n_texels, float tex_scale,
                           float tex_bias, const float* state, const float* v_img, const float* v_depth,
                           const float* v_reg, const float* v_alpha, const float* v_tex, const float* v_normal,
@@ -444,6 +455,7 @@ typedef struct gstex_train_prologue_args {
                                 GSTEX_SETTING_AUX_ZEROED to the forward that follows */
     size_t raster_aux_bytes;
     int32_t raster_channels;
+    double* hp_records;      /* nullable (ABI 18): gstex_raster_setup's near-edge-on fp64 rows, double[n][12] */
 } gstex_train_prologue_args;
 int gstex_train_prologue(const gstex_train_prologue_args* args, void* stream);
 /* Bytes of scan_workspace gstex_train_prologue needs for n splats (>= gstex_scan_workspace_size(n): the fused

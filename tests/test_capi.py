@@ -73,7 +73,7 @@ def test_raster_rejects_bad_channels_and_settings(lib):
                       1.0, 0.0, None, None, None, None, None, None, None, 0, None, None)
     assert rc == 3 and "unsupported settings" in msg
     bad = _cam(block=8)
-    rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, 0,
+    rc, msg = _status(lib, "gstex_raster_bwd", ctypes.byref(bad), 3, 0, None, None, None, None, None, None, None, 0,
                       1.0, 0.0, None, None, None, None, None, None, None, 0, None, None, None, None, None)
     assert rc == 1 and "block_width" in msg
 

@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-from helpers import DIFF, FLIP_MARGIN, grad_norm_err, grad_rel_err, make_window_case, upstream  # noqa: E402
+from helpers import DIFF, FLIP_MARGIN, grad_norm_err, grad_rel_err, make_case, make_window_case, upstream  # noqa: E402
 from oracle import raster as O  # noqa: E402
 
 F32, F64 = torch.float32, torch.float64
@@ -87,17 +87,25 @@ def main():
     ap.add_argument("--win", type=int, default=48)
     ap.add_argument("--cfg", type=int, default=3)
     ap.add_argument("--all-outputs", action="store_true")
+    ap.add_argument("--case", default=None,
+                    help="a tests/test_gpu_parity.py CASES entry, or cfg1 (tests/test_gpu_deep.py), instead of a window")
     ap.add_argument("--fp32-record", action="store_true", help="all-fp32 per-splat record (round-2 formulation)")
     ap.add_argument("--hp-cos", type=float, nargs="*", default=[],
                     help="also: the table of splats with |normal . view dir| < each value kept fp64 (raster.hip GSTEX_HP_COS)")
     args = ap.parse_args()
     O.RECORD_FP64 = not args.fp32_record
-    n, t = (200_000, 1e7) if args.cfg == 3 else (50_000, 1e6)
-    case = make_window_case(n, t, 800, 800, args.win)
     outputs = ("img", "depth", "reg", "alpha", "tex", "normal") if args.all_outputs else ("img", "alpha", "tex")
+    if args.case == "cfg1":
+        case = make_case(n=1000, n_texels=0, H=256, W=256, seed=42, opacity=0.1)
+    elif args.case:
+        from test_gpu_parity import CASES
+        case = make_case(**CASES[args.case])
+    else:
+        n, t = (200_000, 1e7) if args.cfg == 3 else (50_000, 1e6)
+        case = make_window_case(n, t, 800, 800, args.win)
     ref = grads(case, F64, F64, outputs)
     mixes = {"fp32": (F32, F32), "pair32/table64": (F32, F64), "pair64/table32": (F64, F32)}
-    print(f"cfg{args.cfg} {args.win}x{args.win} window, {case.inp.means.shape[0]} splats, outputs {outputs}")
+    print(f"{args.case or f'cfg{args.cfg} {args.win}x{args.win} window'}, {case.inp.means.shape[0]} splats, outputs {outputs}")
     print(f"{'mix':16s} " + " ".join(f"{k:>18s}" for k in DIFF))
     for name, (pd, td) in mixes.items():
         g = grads(case, pd, td, outputs)
