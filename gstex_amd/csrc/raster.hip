@@ -1114,6 +1114,9 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
             const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
+            // the texel sample point from the fp32 evaluation: the forward's texel cells and fractions
+            float xr, yr;
+            tex_coords(r, h.u, h.v, xr, yr);
             // a near-edge-on splat (the record opacity's sign bit): its pairs' values in fp64, the decisions kept
             if (hp_records && __float_as_int(rp[2].w) < 0)
                 refine_hit_hp<GEO>(r, hp_records + (size_t)gid * H_FIELDS, px, py, h);
@@ -1153,8 +1156,6 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 #pragma unroll
                 for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
                 if (has_tex) {
-                    float xr, yr;
-                    tex_coords(r, h.u, h.v, xr, yr);
                     // (converting h, w here measured faster than reading r.hf, r.wf)
                     b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's

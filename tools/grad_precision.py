@@ -47,6 +47,9 @@ def grads(case, pair_dtype, table_dtype, outputs):
     return out
 
 
+GRAD32 = False  # --grad32: the table's gradient (the per-splat sums the GPU reduces and accumulates) rounded to fp32
+
+
 def hp_mask_table(case, thr):
     """Precision analysis of raster.hip's near-edge-on path (GSTEX_HP_COS): in the gradient pass, the per-splat table of
     the splats with |normal . view direction| < thr stays fp64 while the others are rounded to fp32 -- what
@@ -72,6 +75,10 @@ def hp_mask_table(case, thr):
         if dtype != F32 or not state["grad"]:
             return orig_table(inp_, dtype)
         t64 = orig_table(inp_, F64)
+        if GRAD32:
+            for v in t64.values():
+                if v.is_floating_point() and v.requires_grad:
+                    v.register_hook(lambda g: g.float().double())
         return {k: (torch.where(mask.view(-1, *([1] * (v.dim() - 1))), v, v.float().double()) if v.is_floating_point()
                     else v) for k, v in t64.items()}
 
@@ -92,7 +99,11 @@ def main():
     ap.add_argument("--fp32-record", action="store_true", help="all-fp32 per-splat record (round-2 formulation)")
     ap.add_argument("--hp-cos", type=float, nargs="*", default=[],
                     help="also: the table of splats with |normal . view dir| < each value kept fp64 (raster.hip GSTEX_HP_COS)")
+    ap.add_argument("--grad32", action="store_true",
+                    help="with --hp-cos: the per-splat table gradient rounded to fp32 (the GPU's fp32 sums)")
     args = ap.parse_args()
+    global GRAD32
+    GRAD32 = args.grad32
     O.RECORD_FP64 = not args.fp32_record
     outputs = ("img", "depth", "reg", "alpha", "tex", "normal") if args.all_outputs else ("img", "alpha", "tex")
     if args.case == "cfg1":
