@@ -43,6 +43,9 @@ constexpr int kThreads = kTilePixels;  // 256
 #ifndef GSTEX_FAST_EVAL
 #define GSTEX_FAST_EVAL 1  // hardware v_exp_f32 / v_rcp_f32 in the pair evaluation (0: expf sequence, IEEE division)
 #endif
+#ifndef GSTEX_HP_ALPHA
+#define GSTEX_HP_ALPHA 1  // near-edge-on refinement: also G and alpha from the refined rho (0: the forward's fp32 values)
+#endif
 #ifndef GSTEX_UNIT_COARSE
 #define GSTEX_UNIT_COARSE 3  // backward unit-order cost buckets of 2^k visits (inside a bucket: about slot order,
                              // better L2 reuse of texel blocks). Measured: 3 same time, bwd fetch -18 %; 5, 6 slower
@@ -407,6 +410,7 @@ __device__ __forceinline__ void refine_hit_hp(const Rec& r, const double* __rest
     h.v = (float)v;
     h.rho3 = (float)__builtin_fma(u, u, v * v);
     if (GEO && h.use3) h.z = (float)__builtin_fma(u, hr[H_TW], __builtin_fma(v, hr[H_TW + 1], hr[H_TW + 2]));
+#if GSTEX_HP_ALPHA
     const float rho = h.use3 ? h.rho3 : h.rho2;
 #if GSTEX_FAST_EVAL
     h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);
@@ -416,6 +420,7 @@ __device__ __forceinline__ void refine_hit_hp(const Rec& r, const double* __rest
     const bool clamped = !(h.a_raw < kAlphaMax);  // the fp32 decision (fminf(0.99, a_raw) took 0.99)
     h.a_raw = clamped ? h.a_raw : fminf(r.opac * h.G, 0.98999995f);
     h.alpha = clamped ? kAlphaMax : h.a_raw;
+#endif
 }
 
 // One texel's channels: with C == 3 a single 12-B global_load_dwordx3 (the three channels share a cache
@@ -1118,8 +1123,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             float xr, yr;
             tex_coords(r, h.u, h.v, xr, yr);
             // a near-edge-on splat (the record opacity's sign bit): its pairs' values in fp64, the decisions kept
-            if (hp_records && __float_as_int(rp[2].w) < 0)
-                refine_hit_hp<GEO>(r, hp_records + (size_t)gid * H_FIELDS, px, py, h);
+            const bool hp_vis = hp_records && __float_as_int(rp[2].w) < 0;
+            if (hp_vis) refine_hit_hp<GEO>(r, hp_records + (size_t)gid * H_FIELDS, px, py, h);
             GSTEX_STAT(1, 1);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
@@ -1158,6 +1163,15 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if (has_tex) {
                     // (converting h, w here measured faster than reading r.hf, r.wf)
                     b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
+                    if (hp_vis) {
+                        // the fractions at the refined sample point, in the forward's cells (the oracle's x = xr inside
+                        // the cell range, else the clamped value; ax = x - i0)
+                        float xf, yf;
+                        tex_coords(r, h.u, h.v, xf, yf);
+                        const float hm1 = (float)r.h - 1.0f, wm1 = (float)r.w - 1.0f;
+                        b.ax = (b.in_u ? xf : __builtin_amdgcn_fmed3f(xf, 0.0f, hm1)) - (float)b.i0;
+                        b.ay = (b.in_v ? yf : __builtin_amdgcn_fmed3f(yf, 0.0f, wm1)) - (float)b.j0;
+                    }
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
                     // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
                     if constexpr (CM == 3) {

@@ -302,6 +302,10 @@ class RasterInputs:
 # means / quats gradient error (tools/grad_precision.py).  False restores the all-fp32 record
 # (precision analysis only).
 RECORD_FP64 = True
+# Precision analysis only (tools/grad_precision.py --hp-gpu): {"mask": (N,) bool, "tab": fp64 table} -- in an fp32
+# gradient pass, the homogeneous point p of the masked (near-edge-on) splats' pairs is evaluated in fp64 from the
+# fp64 table and rounded to fp32, the rest of the pair in fp32: raster.hip refine_hit_hp's model.  None = off.
+HP_PAIR = None
 
 
 def _splat_table(inp: RasterInputs, dtype):
@@ -418,6 +422,17 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         pxc = _fma(ddx, A[..., 0], ddy * B[..., 0])
         pyc = _fma(ddx, A[..., 1], ddy * B[..., 1])
         pzc = _fma(ddy, B[..., 2], _fma(ddx, A[..., 2], g["Pz"][:, None]))
+        if HP_PAIR is not None and decisions is not None and dtype == F32:
+            hm = HP_PAIR["mask"][ids][:, None]
+            t64 = {k: v[ids] for k, v in HP_PAIR["tab"].items() if k in ("A", "B", "Pz", "xa", "ya")}
+            dx64 = px.double() - t64["xa"][:, None]
+            dy64 = py.double() - t64["ya"][:, None]
+            A64, B64 = t64["A"][:, None, :], t64["B"][:, None, :]
+            p64 = [dx64 * A64[..., 0] + dy64 * B64[..., 0], dx64 * A64[..., 1] + dy64 * B64[..., 1],
+                   dy64 * B64[..., 2] + (dx64 * A64[..., 2] + t64["Pz"][:, None])]
+            pxc = torch.where(hm, p64[0].float(), pxc)
+            pyc = torch.where(hm, p64[1].float(), pyc)
+            pzc = torch.where(hm, p64[2].float(), pzc)
         if decisions is None:
             nz = pzc != 0
         else:

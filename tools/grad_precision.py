@@ -89,6 +89,32 @@ def hp_mask_table(case, thr):
     return float(mask.double().mean()), restore
 
 
+def hp_gpu_model(case, thr):
+    """raster.hip's near-edge-on path as built: the table of the splats with |normal . view direction| < thr kept fp64 for
+    the homogeneous point p only (evaluated in fp64, rounded to fp32), every other per-pair value fp32 (oracle HP_PAIR).
+    Returns (fraction of splats, restore)."""
+    inp = case.inp
+    with torch.no_grad():
+        _, _, tw = O.quat_frame(inp.quats.double())
+        _, cp, *_ = inp.cam.cast(F64)
+        d = cp[None] - inp.means.double()
+        mask = O._dot3(tw, d / d.norm(dim=-1, keepdim=True)).abs() < thr
+    orig_table = O._splat_table
+
+    def table(inp_, dtype):
+        t = orig_table(inp_, dtype)
+        if dtype == F32:
+            O.HP_PAIR = {"mask": mask, "tab": orig_table(inp_, F64)}
+        return t
+
+    O._splat_table = table
+
+    def restore():
+        O._splat_table = orig_table
+        O.HP_PAIR = None
+    return float(mask.double().mean()), restore
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--win", type=int, default=48)
@@ -99,6 +125,8 @@ def main():
     ap.add_argument("--fp32-record", action="store_true", help="all-fp32 per-splat record (round-2 formulation)")
     ap.add_argument("--hp-cos", type=float, nargs="*", default=[],
                     help="also: the table of splats with |normal . view dir| < each value kept fp64 (raster.hip GSTEX_HP_COS)")
+    ap.add_argument("--hp-gpu", action="store_true",
+                    help="with --hp-cos: only p in fp64 for those splats, every other pair value fp32 (as raster.hip)")
     ap.add_argument("--grad32", action="store_true",
                     help="with --hp-cos: the per-splat table gradient rounded to fp32 (the GPU's fp32 sums)")
     args = ap.parse_args()
@@ -125,8 +153,12 @@ def main():
             cells.append(f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}")
         print(f"{name:16s} " + " ".join(f"{c:>18s}" for c in cells))
     for thr in args.hp_cos:
-        frac, restore = hp_mask_table(case, thr)
-        g = grads(case, F64, F32, outputs)
+        if args.hp_gpu:  # the fp32 pass with p of the masked splats from the fp64 table (raster.hip refine_hit_hp)
+            frac, restore = hp_gpu_model(case, thr)
+            g = grads(case, F32, F32, outputs)
+        else:
+            frac, restore = hp_mask_table(case, thr)
+            g = grads(case, F64, F32, outputs)
         restore()
         cells = [f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}" for k in DIFF]
         print(f"{'hp<' + str(thr) + f' ({100 * frac:.1f}%)':16s} " + " ".join(f"{c:>18s}" for c in cells))
