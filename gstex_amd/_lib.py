@@ -134,12 +134,12 @@ SIGNATURES = {
     ),
     "gstex_raster_fwd": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P],
     ),
     "gstex_raster_fwd_zero": (
         c_int32,
-        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+        [_CAM, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
          c_int64, _P, _P, c_int64, _P, c_int64, _P],
     ),
     "gstex_raster_aux_bytes": (c_size_t, [c_int64, c_int32, c_int32]),

@@ -43,9 +43,7 @@ constexpr int kThreads = kTilePixels;  // 256
 #ifndef GSTEX_FAST_EVAL
 #define GSTEX_FAST_EVAL 1  // hardware v_exp_f32 / v_rcp_f32 in the pair evaluation (0: expf sequence, IEEE division)
 #endif
-#ifndef GSTEX_HP_ALPHA
-#define GSTEX_HP_ALPHA 1  // near-edge-on refinement: also G and alpha from the refined rho (0: the forward's fp32 values)
-#endif
+
 #ifndef GSTEX_UNIT_COARSE
 #define GSTEX_UNIT_COARSE 3  // backward unit-order cost buckets of 2^k visits (inside a bucket: about slot order,
                              // better L2 reuse of texel blocks). Measured: 3 same time, bwd fetch -18 %; 5, 6 slower
@@ -121,7 +119,7 @@ __global__ __launch_bounds__(256) void setup_kernel(int n, const float* __restri
 struct Rec {
     f3 A, B, Tw;
     float Pz;
-    float x, y, opac;
+    float x, y, opac, mark;  // opac = |R_OPAC|; mark = the raw word (sign bit: near edge-on, gstex_common.h kHpCos)
     float rgb[3], nrm[3];
     float tu0, auu, auv, tv0, avu, avv;
     int h, w, off;
@@ -140,7 +138,8 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
     r.Pz = v[R_PZ];
     r.Tw = f3{v[R_TW], v[R_TW + 1], v[R_TW + 2]};
     r.x = v[R_XY]; r.y = v[R_XY + 1];
-    r.opac = fabsf(v[R_OPAC]);  // (sign bit: the near-edge-on mark, gstex_common.h kHpCos)
+    r.opac = fabsf(v[R_OPAC]);
+    r.mark = v[R_OPAC];
     r.rgb[0] = v[R_RGB]; r.rgb[1] = v[R_RGB + 1]; r.rgb[2] = v[R_RGB + 2];
     r.tu0 = v[R_TU0]; r.auu = v[R_AUU]; r.auv = v[R_AUV]; r.tv0 = v[R_TV0]; r.avu = v[R_AVU]; r.avv = v[R_AVV];
     r.h = __float_as_int(v[R_H]); r.w = __float_as_int(v[R_W]); r.off = __float_as_int(v[R_OFF]);
@@ -346,16 +345,38 @@ __device__ __forceinline__ int wave_max_i(int v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return __builtin_amdgcn_readfirstlane(v);
 }
-// Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).
-__device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool aa, Hit& h) {
-    // branch-free: a skipped pair's values are computed anyway (possibly inf/NaN) and never used, so
-    // the callers see one predicate instead of three divergent exits (fewer exec-mask joins)
+// The pair's offset from the anchor and homogeneous point p = k x l in affine form (gstex_common.h affine_homog):
+// explicit fused multiply-adds (oracle/raster.py restates them: exact product, one rounding)
+__device__ __forceinline__ void hit_p(const Rec& r, float px, float py, Hit& h) {
     h.dx = px - r.xa;
     h.dy = py - r.ya;
-    // p = k x l in affine form (gstex_common.h affine_homog)
-    // explicit fused multiply-adds (oracle/raster.py restates them: exact product, one rounding)
     h.p = f3{__builtin_fmaf(h.dx, r.A.x, h.dy * r.B.x), __builtin_fmaf(h.dx, r.A.y, h.dy * r.B.y),
              __builtin_fmaf(h.dy, r.B.z, __builtin_fmaf(h.dx, r.A.z, r.Pz))};
+}
+// The same for a near-edge-on splat (gstex_common.h kHpCos) from its fp64 setup row (A, B, Pz, anchor), each value
+// rounded once: p is a small difference of larger terms there, and every value derived from it (u, v, the depth, the
+// weights and all gradients through them) inherits the fp32 record's rounding amplified.  Used by every kernel that
+// evaluates pairs of records carrying the mark (forward and backward alike, so both take the same decisions).
+// The row is read with vector buffer loads (its 18 dwords would not fit beside the record in the kernels' SGPRs).
+__device__ __forceinline__ double hp_load(__amdgpu_buffer_rsrc_t rs, int k) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, k * 8, 0, 0));
+}
+__device__ __forceinline__ void hit_p_hp(const double* __restrict__ row, float px, float py, Hit& h) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(row), 0, H_TW * 8,
+                                                                        0x00020000);
+    const double dx = (double)px - hp_load(rs, H_XA), dy = (double)py - hp_load(rs, H_YA);
+    h.dx = (float)dx;
+    h.dy = (float)dy;
+    h.p = f3{(float)__builtin_fma(dx, hp_load(rs, H_A), dy * hp_load(rs, H_B)),
+             (float)__builtin_fma(dx, hp_load(rs, H_A + 1), dy * hp_load(rs, H_B + 1)),
+             (float)__builtin_fma(dy, hp_load(rs, H_B + 2), __builtin_fma(dx, hp_load(rs, H_A + 2), hp_load(rs, H_PZ)))};
+}
+
+// Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).  h.dx, h.dy, h.p from
+// hit_p / hit_p_hp.
+__device__ __forceinline__ bool eval_rest(const Rec& r, float px, float py, bool aa, Hit& h) {
+    // branch-free: a skipped pair's values are computed anyway (possibly inf/NaN) and never used, so
+    // the callers see one predicate instead of three divergent exits (fewer exec-mask joins)
     const bool ok = h.p.z != 0.0f;
 #if GSTEX_FAST_EVAL
     h.ipz = __builtin_amdgcn_rcpf(h.p.z);
@@ -379,48 +400,9 @@ __device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool 
     h.alpha = fminf(kAlphaMax, h.a_raw);
     return ok && h.z >= kNear && h.alpha >= kAlphaMin;  // oracle/raster.py: nz & (zz >= near) & (alpha >= amin)
 }
-
-// A near-edge-on splat's pair re-evaluated from its fp64 setup row (gstex_common.h kHpCos): dx, dy, p, 1 / p.z, u, v,
-// rho3 and (GEO) the depth in fp64, each rounded once; G, alpha from the refined rho.  Every decision stays the fp32
-// evaluation's (the forward's): contributing or not, the low-pass branch (use3) and the alpha clamp.  The row is read
-// at a wave-uniform address (scalar loads).
-// (read as vector buffer loads: the row's 24 dwords would not fit beside the record in the kernel's SGPR budget)
-__device__ __forceinline__ double hp_load(__amdgpu_buffer_rsrc_t rs, int k) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, k * 8, 0, 0));
-}
-template <bool GEO>
-__device__ __forceinline__ void refine_hit_hp(const Rec& r, const double* __restrict__ row, float px, float py,
-                                              Hit& h) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(row), 0, H_FIELDS * 8,
-                                                                        0x00020000);
-    double hr[H_FIELDS];
-#pragma unroll
-    for (int k = 0; k < H_FIELDS; ++k) hr[k] = (GEO || k < H_TW) ? hp_load(rs, k) : 0.0;
-    const double dx = (double)px - hr[H_XA], dy = (double)py - hr[H_YA];
-    const double p0 = __builtin_fma(dx, hr[H_A], dy * hr[H_B]);
-    const double p1 = __builtin_fma(dx, hr[H_A + 1], dy * hr[H_B + 1]);
-    const double p2 = __builtin_fma(dy, hr[H_B + 2], __builtin_fma(dx, hr[H_A + 2], hr[H_PZ]));
-    const double ipz = 1.0 / p2;
-    const double u = p0 * ipz, v = p1 * ipz;
-    h.dx = (float)dx;
-    h.dy = (float)dy;
-    h.p = f3{(float)p0, (float)p1, (float)p2};
-    h.ipz = (float)ipz;
-    h.u = (float)u;
-    h.v = (float)v;
-    h.rho3 = (float)__builtin_fma(u, u, v * v);
-    if (GEO && h.use3) h.z = (float)__builtin_fma(u, hr[H_TW], __builtin_fma(v, hr[H_TW + 1], hr[H_TW + 2]));
-#if GSTEX_HP_ALPHA
-    const float rho = h.use3 ? h.rho3 : h.rho2;
-#if GSTEX_FAST_EVAL
-    h.G = __builtin_amdgcn_exp2f(-0.72134752f * rho);
-#else
-    h.G = exp_nonpos(-0.5f * rho);
-#endif
-    const bool clamped = !(h.a_raw < kAlphaMax);  // the fp32 decision (fminf(0.99, a_raw) took 0.99)
-    h.a_raw = clamped ? h.a_raw : fminf(r.opac * h.G, 0.98999995f);
-    h.alpha = clamped ? kAlphaMax : h.a_raw;
-#endif
+__device__ __forceinline__ bool eval_hit(const Rec& r, float px, float py, bool aa, Hit& h) {
+    hit_p(r, px, py, h);
+    return eval_rest(r, px, py, aa, h);
 }
 
 // One texel's channels: with C == 3 a single 12-B global_load_dwordx3 (the three channels share a cache
@@ -558,7 +540,8 @@ __device__ __forceinline__ float tex_accum(float acc, float v00, float v01, floa
 template <int C, bool GEOF>
 __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     CamArgs cam_args, int tiles_x, int settings, const float* __restrict__ bg, int Cdyn,
-    const float4* __restrict__ records, const int2* __restrict__ tile_ranges, const int32_t* __restrict__ tile_order,
+    const float4* __restrict__ records, const double* __restrict__ hp_records, const int2* __restrict__ tile_ranges,
+    const int32_t* __restrict__ tile_order,
     const int32_t* __restrict__ sorted_ids, const float* __restrict__ texture, int n_texels, float tex_scale,
     float tex_bias, float* __restrict__ out_img,
     float* __restrict__ out_depth, float* __restrict__ out_reg, float* __restrict__ out_alpha,
@@ -571,6 +554,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     const int Cn = (C > 0) ? C : Cdyn;
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
+    __shared__ int s_gid[kFwdBatch];  // the batch's splat ids (the near-edge-on splats' fp64 rows are read by id)
     const int ti = (int)blockIdx.x;
     const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
@@ -675,7 +659,11 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         if (__syncthreads_count(GSTEX_FWD_DONE ? 1 : 0) == kThreads) break;
         for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
             const int j = q / kRecF4, k = q % kRecF4;
-            if (b0 + j < rng.y) s_rec[k * kFwdBatch + j] = records[(size_t)sorted_ids[b0 + j] * kRecF4 + k];
+            if (b0 + j < rng.y) {
+                const int gid = sorted_ids[b0 + j];
+                s_rec[k * kFwdBatch + j] = records[(size_t)gid * kRecF4 + k];
+                if (k == 0) s_gid[j] = gid;
+            }
         }
         __syncthreads();
         // the batch splats whose contribution region meets this wave's 8x8 block, tested all at once
@@ -703,7 +691,11 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             const Rec r = read_rec<kFwdBatch>(s_rec, j);
             ++seg_visits;
             Hit h;
-            const bool ok = eval_hit(r, px, py, aa, h) && alive != 0.0f;
+            hit_p(r, px, py, h);
+            // a near-edge-on splat (the record opacity's sign bit, wave-uniform): p from its fp64 row
+            if (hp_records && __builtin_amdgcn_readfirstlane(__float_as_int(r.mark)) < 0)
+                hit_p_hp(hp_records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * H_FIELDS, px, py, h);
+            const bool ok = eval_rest(r, px, py, aa, h) && alive != 0.0f;
             const float test_T = T * (1.0f - h.alpha);
             const bool stop = ok && test_T < kTMin;
             GSTEX_STAT(10, 1);                                    // visits (the wave evaluates a splat)
@@ -1118,13 +1110,10 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
             const Rec r = read_rec_global(rp);
             // one predicate for the whole heavy path (a single exec-mask region)
             Hit h;
-            const bool contrib = eval_hit(r, px, py, aa, h) && rel <= last;
-            // the texel sample point from the fp32 evaluation: the forward's texel cells and fractions
-            float xr, yr;
-            tex_coords(r, h.u, h.v, xr, yr);
-            // a near-edge-on splat (the record opacity's sign bit): its pairs' values in fp64, the decisions kept
-            const bool hp_vis = hp_records && __float_as_int(rp[2].w) < 0;
-            if (hp_vis) refine_hit_hp<GEO>(r, hp_records + (size_t)gid * H_FIELDS, px, py, h);
+            hit_p(r, px, py, h);
+            // a near-edge-on splat (the record opacity's sign bit): p from its fp64 row, as in the forward
+            if (hp_records && __float_as_int(rp[2].w) < 0) hit_p_hp(hp_records + (size_t)gid * H_FIELDS, px, py, h);
+            const bool contrib = eval_rest(r, px, py, aa, h) && rel <= last;
             GSTEX_STAT(1, 1);
             GSTEX_STAT(3, __popcll(__ballot(contrib)));
             GSTEX_STAT(13, __popcll(__ballot(rel <= last)));           // lanes not yet past their last contributor
@@ -1161,17 +1150,10 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
 #pragma unroll
                 for (int c = 0; c < CM; ++c) t00[c] = t01[c] = t10[c] = t11[c] = 0.f;
                 if (has_tex) {
+                    float xr, yr;
+                    tex_coords(r, h.u, h.v, xr, yr);
                     // (converting h, w here measured faster than reading r.hf, r.wf)
                     b = bilerp_xy(xr, yr, r.h, r.w, (float)r.h - 1.0f, (float)r.w - 1.0f);
-                    if (hp_vis) {
-                        // the fractions at the refined sample point, in the forward's cells (the oracle's x = xr inside
-                        // the cell range, else the clamped value; ax = x - i0)
-                        float xf, yf;
-                        tex_coords(r, h.u, h.v, xf, yf);
-                        const float hm1 = (float)r.h - 1.0f, wm1 = (float)r.w - 1.0f;
-                        b.ax = (b.in_u ? xf : __builtin_amdgcn_fmed3f(xf, 0.0f, hm1)) - (float)b.i0;
-                        b.ay = (b.in_v ? yf : __builtin_amdgcn_fmed3f(yf, 0.0f, wm1)) - (float)b.j0;
-                    }
                     // (far corners unclamped: at a clamped edge their weight is 0 in the value and the edge's
                     // in_u / in_v = false drops the coordinate gradient, so the results are bit-identical)
                     if constexpr (CM == 3) {
@@ -1771,17 +1753,20 @@ extern "C" int gstex_raster_setup(int32_t n, const float* means, const float* sc
 }
 
 extern "C" int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
-                                const float* background, const float* records, const int32_t* tile_ranges,
+                                const float* background, const float* records, const double* hp_records,
+                                const int32_t* tile_ranges,
                                 const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                                 int64_t n_texels, float tex_scale, float tex_bias, float* out_img, float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
                                 float* out_normal, float* state, int64_t n_isect, void* aux, void* stream) {
-    return gstex_raster_fwd_zero(cam, channels, settings, background, records, tile_ranges, tile_order, sorted_ids,
+    return gstex_raster_fwd_zero(cam, channels, settings, background, records, hp_records, tile_ranges, tile_order,
+                                 sorted_ids,
                                  texture, n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg, out_alpha,
                                  out_tex, out_normal, state, n_isect, aux, nullptr, 0, nullptr, 0, stream);
 }
 
 extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
-                                     const float* background, const float* records, const int32_t* tile_ranges,
+                                     const float* background, const float* records, const double* hp_records,
+                                     const int32_t* tile_ranges,
                                      const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                                      int64_t n_texels, float tex_scale, float tex_bias, float* out_img,
                                      float* out_depth, float* out_reg, float* out_alpha, float* out_tex,
@@ -1822,8 +1807,8 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     int fgrid = fwd_grid(tiles_x, tiles_y);
 #define GSTEX_FWD(CC, GG)                                                                                      \
     raster_fwd_kernel<CC, GG><<<fgrid, kThreads, 0, st>>>(                                                    \
-        dc, tiles_x, settings, background, channels, (const float4*)records, (const int2*)tile_ranges,        \
-        tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg,     \
+        dc, tiles_x, settings, background, channels, (const float4*)records, hp_records,                      \
+        (const int2*)tile_ranges, tile_order, sorted_ids, texture, (int)n_texels, tex_scale, tex_bias, out_img, out_depth, out_reg,     \
         out_alpha, out_tex, out_normal, (float4*)state, ap, nblk, zbuf)
     if (channels == 3 && geo) GSTEX_FWD(3, true);
     else if (channels == 3) GSTEX_FWD(3, false);

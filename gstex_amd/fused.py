@@ -124,7 +124,7 @@ class _TrainRender(torch.autograd.Function):
         zn = sink.numel() if zero_sink else 0
         aux_zeroed = _lib.SETTING_AUX_ZEROED if sizes["aux"] else 0  # (zeroed by the prologue's scan kernel)
         ops._launch("gstex_raster_fwd_zero", cam, C, int(tr.settings) | aux_zeroed, ptr(tr._bg_zero), P["records"],
-                    P["tile_ranges"], P["tile_order"], P["sorted_ids"], ptr(texture), texture.shape[0],
+                    P["hp"] if ops.HP_RECORDS else None, P["tile_ranges"], P["tile_order"], P["sorted_ids"], ptr(texture), texture.shape[0],
                     SH_C0, 0.5, P["img"], None, None, P["alpha"], P["tex"], None, P["state"], cap,
                     P["aux"] if sizes["aux"] else None, ptr(sink) if zero_sink else None, zn, P["partials"],
                     PARTIAL_FLOATS * n, st)

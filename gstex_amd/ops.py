@@ -531,8 +531,8 @@ class _TextureGaussians(torch.autograd.Function):
         # backward-only buffers only when a backward can follow: not under torch.no_grad() (eval renders of
         # trainable parameters), where apply() records no graph whatever the inputs' requires_grad
         needs_bwd = bool(grad_enabled) and any(ctx.needs_input_grad)
-        # the near-edge-on splats' fp64 rows (only when a backward can follow: it is their only reader)
-        hp = torch.empty((n, _lib.HP_DOUBLES), device=dev, dtype=torch.float64) if needs_bwd and HP_RECORDS else None
+        # the near-edge-on splats' fp64 rows (read by the forward and the backward)
+        hp = torch.empty((n, _lib.HP_DOUBLES), device=dev, dtype=torch.float64) if HP_RECORDS else None
         _launch("gstex_raster_setup", n, ptr(means), ptr(scales), float(glob_scale), ptr(quats), ptr(rgbs),
                 ptr(opacities), ptr(centers_c), ptr(uv0), ptr(umap), ptr(vmap), ptr(dims), ptr(nth), cam,
                 ptr(records), ptr(hp), st)
@@ -599,7 +599,8 @@ class _TextureGaussians(torch.autograd.Function):
         # sums (PARTIAL_FLOATS per splat: room for either row width)
         zbuf = ctx.v_texture if (not ctx.sink or zero_sink) else None
         ctx.partials = torch.empty((n * PARTIAL_FLOATS,), device=dev, dtype=torch.float32) if needs_bwd else None
-        _launch("gstex_raster_fwd_zero", cam, C, int(settings), ptr(bg), ptr(records), ptr(tile_ranges), ptr(order),
+        _launch("gstex_raster_fwd_zero", cam, C, int(settings), ptr(bg), ptr(records), ptr(hp), ptr(tile_ranges),
+                ptr(order),
              ptr(sorted_ids),
              ptr(texture), texture.shape[0], ctx_scale, ctx_bias, ptr(img), geo_ptrs[0], geo_ptrs[1], ptr(alpha),
              ptr(tex), geo_ptrs[2],

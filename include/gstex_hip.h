@@ -190,8 +190,10 @@ int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int32_t* tile_
  * hp_records (ABI 18; nullable = none): a device double[n][GSTEX_HP_DOUBLES] buffer.  A splat whose normal is within
  * ~6 degrees of edge-on to its view direction (|n . d| < 0.1) is then marked near edge-on -- the sign bit of its
  * record opacity is set (every kernel reads the magnitude) -- and its row g receives the fp64 affine homography (A, B,
- * Pz), anchor and depth row; other rows are not written.  Pass the same buffer to gstex_raster_bwd(_zero), which
- * re-evaluates those splats' pairs from it in fp64 (their fp32 evaluation is ill-conditioned). */
+ * Pz), anchor and depth row; other rows are not written.  Pass the same buffer to gstex_raster_fwd(_zero) and
+ * gstex_raster_bwd(_zero), which evaluate those splats' pairs from it (the offset from the anchor and the homogeneous
+ * point in fp64, rounded once: their fp32 evaluation is ill-conditioned).  gstex_texture_edit ignores
+ * the marks (pass records built without hp_records). */
 int gstex_raster_setup(int32_t n, const float* means, const float* scales, float glob_scale,
                        const float* quats, const float* rgbs, const float* opacities,
                        const float* centers, const float* uv0, const float* umap,
@@ -209,9 +211,13 @@ int gstex_raster_setup(int32_t n, const float* means, const float* scales, float
  * forward fills for the backward -- its per-wave cull bits (per tile, 8x8 pixel quadrant and tile-list position),
  * per backward unit (tile, quadrant, segment of 256 list positions) the number of splats it evaluated, and
  * per-pixel checkpoints (transmittance and accumulators) at the segment boundaries of deep lists.  Pass the same
- * aux, untouched, to gstex_raster_bwd. */
+ * aux, untouched, to gstex_raster_bwd.
+ * hp_records (ABI 18, nullable): gstex_raster_setup's near-edge-on rows -- the marked splats' pairs are then evaluated
+ * from them (p in fp64, rounded once); pass the same buffer to the backward, which must take the same decisions.
+ * NULL: every pair from the fp32 record (the marks ignored). */
 int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings,
-                     const float* background, const float* records, const int32_t* tile_ranges,
+                     const float* background, const float* records, const double* hp_records,
+                     const int32_t* tile_ranges,
                      const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                      int64_t n_texels, float tex_scale, float tex_bias,
                      float* out_img, float* out_depth, float* out_reg, float* out_alpha,
@@ -221,7 +227,8 @@ int gstex_raster_fwd(const gstex_camera* cam, int32_t channels, int32_t settings
  * buffers the backward accumulates into (the texel gradient, the fast mode's per-splat partials), cleared by the
  * forward's grid with streaming stores the raster work hides (no separate fills). */
 int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, int32_t settings,
-                          const float* background, const float* records, const int32_t* tile_ranges,
+                          const float* background, const float* records, const double* hp_records,
+                          const int32_t* tile_ranges,
                           const int32_t* tile_order, const int32_t* sorted_ids, const float* texture,
                           int64_t n_texels, float tex_scale, float tex_bias,
                           float* out_img, float* out_depth, float* out_reg, float* out_alpha,
@@ -251,8 +258,7 @@ size_t gstex_unit_order_scratch_words(void);
  * atomics into partials[g * R ...], an (n_splats, R) accumulator the caller has zeroed -- no per-pair rows, no
  * summing pass in setup_bwd; the splat gradients then depend on the atomics' order in their last bits (as the
  * texel gradients always do).  With row_flags the splat gradients are bitwise reproducible.
- * hp_records (ABI 18, nullable): gstex_raster_setup's fp64 rows; the pairs of the splats it marked are then
- * re-evaluated in fp64 for the gradient (NULL: every pair in fp32, the marks ignored). */
+ * hp_records (ABI 18, nullable): the forward's hp_records (the same pairs evaluated the same way). */
 int gstex_raster_bwd(const gstex_camera* cam, int32_t channels, int32_t settings,
                      const float* background, const float* records, const double* hp_records,
                      const int32_t* tile_ranges,

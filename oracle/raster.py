@@ -295,6 +295,10 @@ class RasterInputs:
     cam: Camera
     settings: int = SETTING_AA_BLUR | SETTING_DIST_REG
     background: torch.Tensor | None = None  # (3,)
+    # near-edge-on splats (|normal . view direction| < K_HP_COS) evaluated with their homogeneous point p from the
+    # fp64 record (raster.hip hit_p_hp, gstex_raster_setup's hp_records): what texture_gaussians does; texture_edit
+    # (records without hp rows) does not
+    hp: bool = True
 
 
 # raster.hip setup_kernel evaluates the per-splat record in fp64 and rounds each value to fp32 once (and
@@ -302,10 +306,8 @@ class RasterInputs:
 # means / quats gradient error (tools/grad_precision.py).  False restores the all-fp32 record
 # (precision analysis only).
 RECORD_FP64 = True
-# Precision analysis only (tools/grad_precision.py --hp-gpu): {"mask": (N,) bool, "tab": fp64 table} -- in an fp32
-# gradient pass, the homogeneous point p of the masked (near-edge-on) splats' pairs is evaluated in fp64 from the
-# fp64 table and rounded to fp32, the rest of the pair in fp32: raster.hip refine_hit_hp's model.  None = off.
-HP_PAIR = None
+# gstex_common.h kHpCos: splats with |normal . unit view direction| below it are near edge-on
+K_HP_COS = 0.1
 
 
 def _splat_table(inp: RasterInputs, dtype):
@@ -321,6 +323,9 @@ def _splat_table(inp: RasterInputs, dtype):
     mu = inp.means.to(dtype)
     dirv = campos[None, :] - mu
     sgn = torch.where(_dot3(tw, dirv) < 0, -1.0, 1.0).to(dtype).detach()
+    # splat_math.h splat_record: |tw . dir| < kHpCos |dir| (fp64)
+    with torch.no_grad():
+        hp = _dot3(tw, dirv).abs() < K_HP_COS * torch.sqrt(_dot3(dirv, dirv))
     um = inp.umap[:, 0, :].to(dtype).detach()
     vm = inp.vmap[:, 0, :].to(dtype).detach()
     # the texture affine prescaled to texel units (raster.hip setup_kernel): the sample point (tu h, tv w)
@@ -339,7 +344,7 @@ def _splat_table(inp: RasterInputs, dtype):
         tu0=inp.uv0[:, 0, 0].to(dtype) * hd, tv0=inp.uv0[:, 0, 1].to(dtype) * wd,
         auu=su * _dot3(tu, um) * hd, auv=sv * _dot3(tv, um) * hd,
         avu=su * _dot3(tu, vm) * wd, avv=sv * _dot3(tv, vm) * wd,
-        sgn=sgn,
+        sgn=sgn, hp=hp,
     )
 
 
@@ -368,7 +373,12 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
     C = inp.texture.shape[1]
     aa = bool(inp.settings & SETTING_AA_BLUR)
     dreg = bool(inp.settings & SETTING_DIST_REG)
-    if table_dtype is None or table_dtype == dtype:
+    tab64 = None
+    if inp.hp and dtype == F32 and RECORD_FP64 and table_dtype in (None, F32):
+        # the fp32 record is the fp64 one rounded (setup_kernel); near-edge-on splats' p comes from the fp64 one
+        tab64 = _splat_table(inp, F64)
+        tab = {k: (v.to(F32) if v.is_floating_point() else v) for k, v in tab64.items()}
+    elif table_dtype is None or table_dtype == dtype:
         tab = _splat_table(inp, dtype)
     else:  # mixed precision: table in table_dtype, cast (differentiably) to the per-pair dtype
         tab = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in _splat_table(inp, table_dtype).items()}
@@ -414,7 +424,7 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         # depths_to_points (gstex.py:138-139, ray through (j - cx + 0.5) / fx), DESIGN.md §1 lineage table
         px = (torch.from_numpy(pxi.astype(np.float32)) + 0.5).to(dtype)[None, :]  # exact in fp32
         py = (torch.from_numpy(pyi.astype(np.float32)) + 0.5).to(dtype)[None, :]
-        g = {k: v[ids] for k, v in tab.items() if k != "sgn"}
+        g = {k: v[ids] for k, v in tab.items() if k not in ("sgn", "hp")}
         A, B, Tw = g["A"][:, None, :], g["B"][:, None, :], g["Tw"][:, None, :]
         ddx = px - g["xa"][:, None]
         ddy = py - g["ya"][:, None]
@@ -422,14 +432,16 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
         pxc = _fma(ddx, A[..., 0], ddy * B[..., 0])
         pyc = _fma(ddx, A[..., 1], ddy * B[..., 1])
         pzc = _fma(ddy, B[..., 2], _fma(ddx, A[..., 2], g["Pz"][:, None]))
-        if HP_PAIR is not None and decisions is not None and dtype == F32:
-            hm = HP_PAIR["mask"][ids][:, None]
-            t64 = {k: v[ids] for k, v in HP_PAIR["tab"].items() if k in ("A", "B", "Pz", "xa", "ya")}
-            dx64 = px.double() - t64["xa"][:, None]
-            dy64 = py.double() - t64["ya"][:, None]
-            A64, B64 = t64["A"][:, None, :], t64["B"][:, None, :]
+        if tab64 is not None and bool(tab64["hp"][ids].any()):
+            # raster.hip hit_p_hp: dx, dy and p of a near-edge-on splat's pairs from its fp64 record, rounded once
+            hm = tab64["hp"][ids][:, None]
+            x64 = tab64["xa"][ids][:, None]
+            y64 = tab64["ya"][ids][:, None]
+            A64, B64 = tab64["A"][ids][:, None, :], tab64["B"][ids][:, None, :]
+            dx64 = px.double() - x64
+            dy64 = py.double() - y64
             p64 = [dx64 * A64[..., 0] + dy64 * B64[..., 0], dx64 * A64[..., 1] + dy64 * B64[..., 1],
-                   dy64 * B64[..., 2] + (dx64 * A64[..., 2] + t64["Pz"][:, None])]
+                   dy64 * B64[..., 2] + (dx64 * A64[..., 2] + tab64["Pz"][ids][:, None])]
             pxc = torch.where(hm, p64[0].float(), pxc)
             pyc = torch.where(hm, p64[1].float(), pyc)
             pzc = torch.where(hm, p64[2].float(), pzc)
@@ -617,7 +629,8 @@ def texture_edit(inp: RasterInputs, edit_rgb, edit_alpha, depth_lo, depth_hi, bi
     n_tex = inp.texture.shape[0]
     edit = dict(rgb=edit_rgb, a=edit_alpha, lo=depth_lo, hi=depth_hi,
                 out=torch.zeros((n_tex, 5), dtype=torch.float64))
-    _render(inp, F32, bins[1], bins[2], None, edit=edit)
+    from dataclasses import replace
+    _render(replace(inp, hp=False), F32, bins[1], bins[2], None, edit=edit)  # (its records carry no hp rows)
     return edit["out"]
 
 

@@ -66,10 +66,10 @@ def test_bin_sort_rejects_non16_block(lib):
 
 def test_raster_rejects_bad_channels_and_settings(lib):
     cam = _cam()
-    rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 9, 0, None, None, None, None, None, None, 0, 1.0,
+    rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 9, 0, None, None, None, None, None, None, None, 0, 1.0,
                       0.0, None, None, None, None, None, None, None, 0, None, None)
     assert rc == 1 and "channels" in msg
-    rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 3, 1 << 2, None, None, None, None, None, None, 0,
+    rc, msg = _status(lib, "gstex_raster_fwd", ctypes.byref(cam), 3, 1 << 2, None, None, None, None, None, None, None, 0,
                       1.0, 0.0, None, None, None, None, None, None, None, 0, None, None)
     assert rc == 3 and "unsupported settings" in msg
     bad = _cam(block=8)

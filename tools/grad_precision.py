@@ -10,8 +10,9 @@ gradient's norm-wise and max relative error against the all-fp64 evaluation:
   table32     table fp32, per-pair fp64;
 With the fp64 record (default) "table32" means the fp64 record rounded to fp32, so pair64/table32 isolates the
 rounding of the stored record: exact arithmetic everywhere else -- the conditioning floor of an fp32 record.
+  fp32+hp     the build: fp32, with the near-edge-on splats' (|normal . view| < 0.1) homogeneous point p evaluated from
+              their fp64 record (raster.hip hit_p_hp; the oracle's RasterInputs.hp)
   hp<c        --hp-cos c: as pair64/table32, but the table of the near-edge-on splats (|normal . view| < c) kept fp64
-              (raster.hip's GSTEX_HP_COS path)
 Test infrastructure only (imports oracle/).  Usage: python tools/grad_precision.py [--win 48] [--cfg 3] [--hp-cos 0.05]
 """
 import argparse
@@ -89,32 +90,6 @@ def hp_mask_table(case, thr):
     return float(mask.double().mean()), restore
 
 
-def hp_gpu_model(case, thr):
-    """raster.hip's near-edge-on path as built: the table of the splats with |normal . view direction| < thr kept fp64 for
-    the homogeneous point p only (evaluated in fp64, rounded to fp32), every other per-pair value fp32 (oracle HP_PAIR).
-    Returns (fraction of splats, restore)."""
-    inp = case.inp
-    with torch.no_grad():
-        _, _, tw = O.quat_frame(inp.quats.double())
-        _, cp, *_ = inp.cam.cast(F64)
-        d = cp[None] - inp.means.double()
-        mask = O._dot3(tw, d / d.norm(dim=-1, keepdim=True)).abs() < thr
-    orig_table = O._splat_table
-
-    def table(inp_, dtype):
-        t = orig_table(inp_, dtype)
-        if dtype == F32:
-            O.HP_PAIR = {"mask": mask, "tab": orig_table(inp_, F64)}
-        return t
-
-    O._splat_table = table
-
-    def restore():
-        O._splat_table = orig_table
-        O.HP_PAIR = None
-    return float(mask.double().mean()), restore
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--win", type=int, default=48)
@@ -125,8 +100,6 @@ def main():
     ap.add_argument("--fp32-record", action="store_true", help="all-fp32 per-splat record (round-2 formulation)")
     ap.add_argument("--hp-cos", type=float, nargs="*", default=[],
                     help="also: the table of splats with |normal . view dir| < each value kept fp64 (raster.hip GSTEX_HP_COS)")
-    ap.add_argument("--hp-gpu", action="store_true",
-                    help="with --hp-cos: only p in fp64 for those splats, every other pair value fp32 (as raster.hip)")
     ap.add_argument("--grad32", action="store_true",
                     help="with --hp-cos: the per-splat table gradient rounded to fp32 (the GPU's fp32 sums)")
     args = ap.parse_args()
@@ -142,6 +115,7 @@ def main():
     else:
         n, t = (200_000, 1e7) if args.cfg == 3 else (50_000, 1e6)
         case = make_window_case(n, t, 800, 800, args.win)
+    case.inp.hp = False  # the historical mixes: no near-edge-on path (the "fp32+hp" row below is the build)
     ref = grads(case, F64, F64, outputs)
     mixes = {"fp32": (F32, F32), "pair32/table64": (F32, F64), "pair64/table32": (F64, F32)}
     print(f"{args.case or f'cfg{args.cfg} {args.win}x{args.win} window'}, {case.inp.means.shape[0]} splats, outputs {outputs}")
@@ -152,13 +126,16 @@ def main():
         for k in DIFF:
             cells.append(f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}")
         print(f"{name:16s} " + " ".join(f"{c:>18s}" for c in cells))
+    # the build: fp32, with the near-edge-on splats' homogeneous point from their fp64 record (raster.hip hit_p_hp)
+    case.inp.hp = True
+    g = grads(case, F32, F32, outputs)
+    frac = float(O._splat_table(case.inp, F64)["hp"].double().mean())
+    cells = [f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}" for k in DIFF]
+    print(f"{'fp32+hp (' + f'{100 * frac:.1f}%)':16s} " + " ".join(f"{c:>18s}" for c in cells))
+    case.inp.hp = False
     for thr in args.hp_cos:
-        if args.hp_gpu:  # the fp32 pass with p of the masked splats from the fp64 table (raster.hip refine_hit_hp)
-            frac, restore = hp_gpu_model(case, thr)
-            g = grads(case, F32, F32, outputs)
-        else:
-            frac, restore = hp_mask_table(case, thr)
-            g = grads(case, F64, F32, outputs)
+        frac, restore = hp_mask_table(case, thr)
+        g = grads(case, F64, F32, outputs)
         restore()
         cells = [f"{grad_norm_err(g[k], ref[k]):.2e}/{grad_rel_err(g[k], ref[k])[0]:.2e}" for k in DIFF]
         print(f"{'hp<' + str(thr) + f' ({100 * frac:.1f}%)':16s} " + " ".join(f"{c:>18s}" for c in cells))
