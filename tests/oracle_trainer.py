@@ -49,6 +49,10 @@ class OracleTrainer:
     def parameters(self):
         return [p for ps in self.param_groups().values() for p in ps]
 
+    def sh_degree_now(self) -> int:
+        """min(step // sh_degree_interval, sh_degree) (gstex.py:1103)."""
+        return min(self.step // self.sh_degree_interval, self.sh_degree)
+
     def render(self, view: View):
         quats = self.quats / self.quats.norm(dim=-1, keepdim=True)
         s = torch.exp(self.scales[:, :-1]).clamp(min=1e-9)
@@ -61,7 +65,7 @@ class OracleTrainer:
         cam = O.Camera(view.viewmat, view.fx, view.fy, view.cx, view.cy, view.H, view.W, 16, campos)
         centers, extents = O.aabb_2d(self.means, scales, 1.0, quats, cam)
         _, depths = O.project_points(self.means.detach(), cam)
-        deg = min(self.step // self.sh_degree_interval, self.sh_degree)
+        deg = self.sh_degree_now()
         coeffs = torch.cat([torch.zeros_like(self.features_rest[:, :1, :]), self.features_rest], 1)
         rgbs = O.spherical_harmonics(deg, viewdirs, coeffs)
         texture = SH2RGB(self.texture_dc)

@@ -5,10 +5,11 @@ trainers on the same synthetic task:
     texel update, capacity-sized pair buffers, float-atomic gradient sums);
   * an oracle-driven trainer (tests/oracle_trainer.py): the CPU oracle's fp32 forward and torch autograd backward,
     eager loss, torch.optim.Adam -- the same views, learning rates, rechart schedule and seed.
-Both start from the same random-init scene (1,000 splats, 20,000 texels) and fit the images a different seeded scene
-renders (the oracle, 48 x 48, eight sphere poses), one pose per step for 150 steps, with a rechart after step 100
-(build_chart_every = 100, gstex.py:202, 890-895).  Every 10 steps both render a held-out pose and the PSNR is taken as
-the reference's metric does (torchmetrics PeakSignalNoiseRatio(data_range=1.0) on the composited rgb,
+Both start from the same random-init scene (1,500 splats, 30,000 texels) and fit the images a different seeded scene
+renders (the oracle, 48 x 48, eight sphere poses), one pose per step for 200 steps from step 0, so the SH degree ramp
+min(step // interval, 3) (gstex.py:1103, sh_degree_interval 1000 in the reference, 30 here) runs through degrees
+0, 1, 2 and 3, with recharts after steps 80 and 160 (build_chart_every, gstex.py:202, 890-895; 100 in the
+reference).  Every 10 steps both render a held-out pose and the PSNR is taken as the reference's metric does (torchmetrics PeakSignalNoiseRatio(data_range=1.0) on the composited rgb,
 gstex.py:350, 1262-1272): 10 log10(1 / MSE).  Pass: |PSNR_hip - PSNR_oracle| <= 0.05 dB at every logged step, and the
 task must actually train (PSNR up by >= 1 dB).  The per-group parameter drift between the two trainers is printed.
 """
@@ -24,7 +25,7 @@ from oracle_trainer import OracleTrainer
 
 pytestmark = pytest.mark.gpu
 
-N, T, HW, STEPS, EVERY, RECHART, POSES = 1000, 20000, 48, 150, 10, 100, 8
+N, T, HW, STEPS, EVERY, RECHARTS, POSES, SH_EVERY = 1500, 30000, 48, 200, 10, (80, 160), 8, 30
 
 
 def psnr(rgb, gt):
@@ -61,8 +62,8 @@ def test_training_trajectory_psnr_matches_the_oracle_trainer():
     gts = teacher_images(views)
     train_views, eval_view, eval_gt = views[:POSES], views[POSES], gts[POSES]
     scene = make_scene(N, T, seed=5)
-    hip = GStexTrainer(scene, dev, start_step=3000, defer_texture=True)
-    ref = OracleTrainer(scene, start_step=3000)
+    hip = GStexTrainer(scene, dev, start_step=0, sh_degree_interval=SH_EVERY, defer_texture=True)
+    ref = OracleTrainer(scene, start_step=0, sh_degree_interval=SH_EVERY)
     dviews = [v.to(dev) for v in views]
     dgts = [g.to(dev) for g in gts]
     log = []
@@ -85,19 +86,21 @@ def test_training_trajectory_psnr_matches_the_oracle_trainer():
         ref.zero_grad()
         ref.forward_backward(train_views[k], gts[k])
         ref.optimizer_step()
-        if step + 1 == RECHART:
+        if step + 1 in RECHARTS:
             hip.recharge()
             ref.recharge()
             # each trainer charts its own scales (build_charts is deterministic): after 100 steps of float-atomic
             # noise a few splats sit on the other side of a ceil() and get another texel count, which the PSNR absorbs
             dh = hip.texture_dims.cpu()
             n_diff = int((dh[:, :2] != ref.texture_dims[:, :2]).any(-1).sum())
-            print(f"rechart after step {RECHART}: {n_diff} of {N} splats charted differently; texels "
+            print(f"rechart after step {step + 1}: {n_diff} of {N} splats charted differently; texels "
                   f"{int(dh[:, 0].long().mul(dh[:, 1].long()).sum())} (hip) vs "
                   f"{int(ref.texture_dims[:, 0].long().mul(ref.texture_dims[:, 1].long()).sum())} (oracle)")
             assert n_diff <= N // 50, "the recharts diverged"
         if (step + 1) % EVERY == 0:
             measure(step + 1)
+        if (step + 1) % SH_EVERY == 0 and step + 1 <= 3 * SH_EVERY:
+            assert hip.sh_degree_now() == ref.sh_degree_now() == (step + 1) // SH_EVERY
     hip.wait_texture()
     torch.cuda.synchronize()
     dh, dr = hip.texture_dims.cpu().long(), ref.texture_dims.long()
