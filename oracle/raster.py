@@ -308,6 +308,32 @@ class RasterInputs:
 RECORD_FP64 = True
 # gstex_common.h kHpCos: splats with |normal . unit view direction| below it are near edge-on
 K_HP_COS = 0.1
+# Precision analysis only (tools/grad_precision.py --hp-sum32): the gradient of a near-edge-on splat's fp64 homogeneous
+# point p w.r.t. its fp64 record (A, B, Pz) formed as the HIP backward forms it -- fp32 products dp * dx summed over a
+# tile's pixels in fp32, the anchor held constant -- instead of autograd's fp64 products and sums.
+HP_SUM32 = False
+# Precision analysis only (tools/hp_sum_model.py): a list that the fp32 gradient pass appends, per tile, the pairs'
+# splat ids, pixel offsets from the anchor (fp32 and fp64) and -- through hooks -- dL/dp.  None = off.
+CAPTURE = None
+
+
+class _HpPoint(torch.autograd.Function):
+    """p = dx A + dy B + (0, 0, Pz) in fp64, rounded to fp32; backward in fp32 per tile (HP_SUM32)."""
+
+    @staticmethod
+    def forward(ctx, dx64, dy64, A64, B64, Pz64):
+        ctx.save_for_backward(dx64.float(), dy64.float())
+        p = torch.stack([dx64 * A64[..., 0] + dy64 * B64[..., 0], dx64 * A64[..., 1] + dy64 * B64[..., 1],
+                         dy64 * B64[..., 2] + (dx64 * A64[..., 2] + Pz64)], -1)
+        return p.float()
+
+    @staticmethod
+    def backward(ctx, gp):
+        dx, dy = ctx.saved_tensors
+        gA = (gp * dx[..., None]).sum(1, keepdim=True)
+        gB = (gp * dy[..., None]).sum(1, keepdim=True)
+        gP = gp[..., 2].sum(1, keepdim=True)
+        return None, None, gA.double(), gB.double(), gP.double()
 
 
 def _splat_table(inp: RasterInputs, dtype):
@@ -440,11 +466,25 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
             A64, B64 = tab64["A"][ids][:, None, :], tab64["B"][ids][:, None, :]
             dx64 = px.double() - x64
             dy64 = py.double() - y64
-            p64 = [dx64 * A64[..., 0] + dy64 * B64[..., 0], dx64 * A64[..., 1] + dy64 * B64[..., 1],
-                   dy64 * B64[..., 2] + (dx64 * A64[..., 2] + tab64["Pz"][ids][:, None])]
+            if HP_SUM32:
+                p32 = _HpPoint.apply(dx64.detach(), dy64.detach(), A64, B64, tab64["Pz"][ids][:, None])
+                p64 = [p32[..., 0], p32[..., 1], p32[..., 2]]
+            else:
+                p64 = [dx64 * A64[..., 0] + dy64 * B64[..., 0], dx64 * A64[..., 1] + dy64 * B64[..., 1],
+                       dy64 * B64[..., 2] + (dx64 * A64[..., 2] + tab64["Pz"][ids][:, None])]
             pxc = torch.where(hm, p64[0].float(), pxc)
             pyc = torch.where(hm, p64[1].float(), pyc)
             pzc = torch.where(hm, p64[2].float(), pzc)
+        if CAPTURE is not None and decisions is not None:
+            src = tab64 if tab64 is not None else tab
+            rec = dict(ids=ids, pxi=pxi, pyi=pyi, dx32=ddx.detach(), dy32=ddy.detach(),
+                       dx64=(px.double() - src["xa"][ids][:, None].double()).detach(),
+                       dy64=(py.double() - src["ya"][ids][:, None].double()).detach(),
+                       hp=(tab64["hp"][ids] if tab64 is not None else torch.zeros(K, dtype=torch.bool)))
+            for nm, tt in (("gx", pxc), ("gy", pyc), ("gz", pzc)):
+                if tt.requires_grad:
+                    tt.register_hook(lambda gr, nm=nm, rec=rec: rec.__setitem__(nm, gr.detach().clone()))
+            CAPTURE.append(rec)
         if decisions is None:
             nz = pzc != 0
         else:

@@ -102,7 +102,10 @@ def main():
                     help="also: the table of splats with |normal . view dir| < each value kept fp64 (raster.hip GSTEX_HP_COS)")
     ap.add_argument("--grad32", action="store_true",
                     help="with --hp-cos: the per-splat table gradient rounded to fp32 (the GPU's fp32 sums)")
+    ap.add_argument("--hp-sum32", action="store_true",
+                    help="the fp32+hp row with the near-edge-on splats' p gradient summed in fp32 (as the HIP backward)")
     args = ap.parse_args()
+    O.HP_SUM32 = args.hp_sum32
     global GRAD32
     GRAD32 = args.grad32
     O.RECORD_FP64 = not args.fp32_record
