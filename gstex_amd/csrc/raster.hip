@@ -150,16 +150,20 @@ __device__ __forceinline__ Rec rec_from_planes(float4 a, float4 b, float4 c, flo
 }
 
 // Pixel of thread tid inside a 16x16 tile and the wave's block of pixel centres.
-struct WaveBlock { int px, py; float wx0, wx1, wy0, wy1; };
+struct WaveBlock { int px, py; float wx0, wx1, wy0, wy1; };  // w*: the cull box (pixel centres +- 0.05)
 __device__ __forceinline__ WaveBlock wave_block(int tx, int ty, int tid) {
     WaveBlock b;
     const int w = tid >> 6, l = tid & 63;
     b.px = tx * kTile + (w & 1) * 8 + (l & 7);  // wave w covers the 8x8 quadrant (w & 1, w >> 1)
     b.py = ty * kTile + (w >> 1) * 8 + (l >> 3);
-    b.wx0 = (float)(tx * kTile + (w & 1) * 8) + 0.5f;
-    b.wy0 = (float)(ty * kTile + (w >> 1) * 8) + 0.5f;
-    b.wx1 = b.wx0 + 7.0f;
-    b.wy1 = b.wy0 + 7.0f;
+    // the cull box is wave-uniform: held in SGPRs (as VGPRs its four bounds were the allocator's first spill
+    // candidates, reloaded from scratch by every record's cull test)
+    auto uni = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
+    const float x0 = (float)(tx * kTile + (w & 1) * 8) + 0.5f, y0 = (float)(ty * kTile + (w >> 1) * 8) + 0.5f;
+    b.wx0 = uni(x0 - 0.05f);
+    b.wy0 = uni(y0 - 0.05f);
+    b.wx1 = uni((x0 + 7.0f) + 0.05f);
+    b.wy1 = uni((y0 + 7.0f) + 0.05f);
     return b;
 }
 
@@ -292,7 +296,7 @@ __device__ __forceinline__ bool may_hit_planes(float4 p0, float4 p1, float4 p2, 
     const float opac = fabsf(v[R_OPAC]);
     if (!(opac * 255.0f > 1.0f)) return false;
     const float rm = 2.0f * logf(255.0f * opac) * 1.01f + 1e-2f;
-    const float x0 = wx0 - 0.05f, x1 = wx1 + 0.05f, y0 = wy0 - 0.05f, y1 = wy1 + 0.05f;
+    const float x0 = wx0, x1 = wx1, y0 = wy0, y1 = wy1;  // (wave_block's cull box: already widened by 0.05)
     const float cx = v[R_XY], cy = v[R_XY + 1];
     if (aa) {
         const float ex = cx - fminf(fmaxf(cx, x0), x1), ey = cy - fminf(fmaxf(cy, y0), y1);
@@ -370,9 +374,23 @@ __device__ __forceinline__ void hit_p_hp(const double* __restrict__ row, float p
     const double dx = (double)px - hp_load(rs, H_XA), dy = (double)py - hp_load(rs, H_YA);
     h.dx = (float)dx;
     h.dy = (float)dy;
-    h.p = f3{(float)__builtin_fma(dx, hp_load(rs, H_A), dy * hp_load(rs, H_B)),
-             (float)__builtin_fma(dx, hp_load(rs, H_A + 1), dy * hp_load(rs, H_B + 1)),
-             (float)__builtin_fma(dy, hp_load(rs, H_B + 2), __builtin_fma(dx, hp_load(rs, H_A + 2), hp_load(rs, H_PZ)))};
+    // one component at a time (the empty asm statements keep the row loads from being hoisted together): the
+    // fp64 temporaries stay few, so the forward's visit loop keeps its register budget without spills
+    h.p.x = (float)__builtin_fma(dx, hp_load(rs, H_A), dy * hp_load(rs, H_B));
+    asm volatile("" : "+v"(h.p.x));
+    h.p.y = (float)__builtin_fma(dx, hp_load(rs, H_A + 1), dy * hp_load(rs, H_B + 1));
+    asm volatile("" : "+v"(h.p.y));
+    h.p.z = (float)__builtin_fma(dy, hp_load(rs, H_B + 2), __builtin_fma(dx, hp_load(rs, H_A + 2), hp_load(rs, H_PZ)));
+}
+// The forward's copy: the row address is wave-uniform there, so plain loads become scalar loads and the row's
+// doubles sit in SGPRs (fused multiply-adds take them as the scalar operand) -- the forward's visit loop is at its
+// VGPR budget, and fp64 row values in VGPRs made the allocator spill the cull's loop-carried bounds
+__device__ __forceinline__ void hit_p_hp_uniform(const double* __restrict__ row, float px, float py, Hit& h) {
+    const double dx = (double)px - row[H_XA], dy = (double)py - row[H_YA];
+    h.dx = (float)dx;
+    h.dy = (float)dy;
+    h.p = f3{(float)__builtin_fma(dx, row[H_A], dy * row[H_B]), (float)__builtin_fma(dx, row[H_A + 1], dy * row[H_B + 1]),
+             (float)__builtin_fma(dy, row[H_B + 2], __builtin_fma(dx, row[H_A + 2], row[H_PZ]))};
 }
 
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).  h.dx, h.dy, h.p from
@@ -696,8 +714,10 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             Hit h;
             hit_p(r, px, py, h);
             // a near-edge-on splat (the record opacity's sign bit, wave-uniform): p from its fp64 row
+#ifndef GSTEX_HP_FWD_OFF  // (timing experiment only: the forward without its near-edge-on branch)
             if (hp_records && __builtin_amdgcn_readfirstlane(__float_as_int(r.mark)) < 0)
-                hit_p_hp(hp_records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * H_FIELDS, px, py, h);
+                hit_p_hp_uniform(hp_records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * H_FIELDS, px, py, h);
+#endif
             const bool ok = eval_rest(r, px, py, aa, h) && alive != 0.0f;
             const float test_T = T * (1.0f - h.alpha);
             const bool stop = ok && test_T < kTMin;
@@ -1227,6 +1247,8 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                     P[P_OPAC] = dL_dalpha * h.G;
                     drho = dL_dalpha * h.a_raw * -0.5f;
                 }
+                GSTEX_PAIR(__int_as_float(gid), px, py, __int_as_float((h.use3 ? 1 : 0) | (h.a_raw < kAlphaMax ? 0 : 2)), T,
+                           w, dL_dalpha, drho, h.u, h.v, h.ipz, h.z, h.alpha, h.G, h.dx, h.dy);
                 // texture coordinates
                 dtu *= tex_scale;  // the raw-value differences above, in value units
                 dtv *= tex_scale;

@@ -44,3 +44,22 @@ struct GstexWgStamp {
 #else
 #define GSTEX_WG_STAMP(depth, wl) do { } while (0)
 #endif
+// GSTEX_PAIR_DUMP (tools/hp_pairs.py): every contributing pair of the backward appends one 16-float record
+//   gid (bits), px, py, flags (use3 | aclamp << 1, bits), T, w, dL/dalpha, drho, u, v, 1 / p.z, z, alpha, G, dx, dy
+// to the buffer gstex_debug_pair_dump installed (vector atomics on the count; records past `cap` are dropped).
+#ifdef GSTEX_PAIR_DUMP
+__device__ float* g_pair_buf;
+__device__ int* g_pair_count;
+__device__ int g_pair_cap;
+extern "C" int gstex_debug_pair_dump(float* buf, int cap, int* count) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pair_buf), &buf, sizeof(buf)) != hipSuccess) return 2;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pair_count), &count, sizeof(count)) != hipSuccess) return 2;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pair_cap), &cap, sizeof(cap)) == hipSuccess ? 0 : 2;
+}
+#define GSTEX_PAIR(...) do { \
+    const float v_[16] = {__VA_ARGS__}; \
+    if (g_pair_buf) { const int k_ = atomicAdd(g_pair_count, 1); \
+        if (k_ < g_pair_cap) for (int i_ = 0; i_ < 16; ++i_) g_pair_buf[16 * (size_t)k_ + i_] = v_[i_]; } } while (0)
+#else
+#define GSTEX_PAIR(...) do { } while (0)
+#endif

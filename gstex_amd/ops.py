@@ -21,6 +21,8 @@ BLOCK_WIDTH = 16
 # near-edge-on splats re-evaluated in fp64 by the raster backward (gstex_raster_setup / gstex_raster_bwd hp_records,
 # ABI 18); GSTEX_HP=0 evaluates every pair in fp32 (the round-5 numerics)
 HP_RECORDS = os.environ.get("GSTEX_HP", "1") != "0"
+# diagnostics: called with (partials, row_flags, records, hp rows) after each raster backward (tools/hp_partials.py)
+PARTIALS_HOOK = None
 
 # ----------------------------------------------------------------------------------------
 # optional per-kernel timing: HIP events recorded on the stream each kernel is launched on
@@ -663,6 +665,8 @@ class _TextureGaussians(torch.autograd.Function):
                 ptr(sorted_ids), ptr(sorted_slots), ptr(texture), texture.shape[0], ctx.tex_affine[0],
                 ctx.tex_affine[1], ptr(state), ptr(v_img), ptr(v_depth), ptr(v_reg), ptr(v_alpha), ptr(v_tex),
                 ptr(v_normal), n_isect, ptr(partials), ptr(row_flags), ptr(v_texture), ptr(ctx.aux), st)
+        if PARTIALS_HOOK is not None:  # diagnostics (tools/hp_partials.py): the per-splat sums before the chain
+            PARTIALS_HOOK(partials, row_flags, records, ctx.hp)
         ctx.aux = None
         ctx.hp = None
         if ctx.sink:

@@ -46,6 +46,14 @@ def _c(v, dtype):
     return torch.tensor(float(v), dtype=dtype)
 
 
+def _arg32(v, dtype):
+    """A scalar kernel argument (fx, fy, cx, cy, glob_scale): the reference's extension takes them as C `float`
+    (gsplat-0.1's bindings, which gstex_cuda extends: `const float fx, ... const float glob_scale`; gstex.py:1142-1160
+    passes Python floats), so every precision evaluates with the fp32-rounded value -- also include/gstex_hip.h's
+    gstex_camera and glob_scale arguments."""
+    return torch.tensor(float(np.float32(v)), dtype=dtype)
+
+
 def _div(a, b):
     """fp32 a / b correctly rounded on any host (torch's vectorised fp32 division/sqrt are not
     correctly rounded on every CPU; the GPU's are).  Exact: fp64 has > 2*24+2 bits."""
@@ -117,7 +125,7 @@ class Camera:
     def cast(self, dtype):
         V = self.viewmat.to(dtype)
         cp = self.campos.to(dtype) if self.campos is not None else -(V[:, :3].T @ V[:, 3])
-        return V, cp, _c(self.fx, dtype), _c(self.fy, dtype), _c(self.cx, dtype), _c(self.cy, dtype)
+        return V, cp, _arg32(self.fx, dtype), _arg32(self.fy, dtype), _arg32(self.cx, dtype), _arg32(self.cy, dtype)
 
 
 def splat_homography(means, scales, glob_scale, quats, cam: Camera, dtype=F32):
@@ -125,7 +133,7 @@ def splat_homography(means, scales, glob_scale, quats, cam: Camera, dtype=F32):
     gstex_common.h:splat_homography."""
     V, _, fx, fy, cx, cy = cam.cast(dtype)
     tu, tv, _ = quat_frame(quats.to(dtype))
-    glob = _c(glob_scale, dtype)
+    glob = _arg32(glob_scale, dtype)
     su = scales[:, 0].to(dtype) * glob
     sv = scales[:, 1].to(dtype) * glob
     a = tu * su[:, None]
@@ -145,7 +153,7 @@ def splat_anchored(means, scales, glob_scale, quats, cam: Camera, dtype=F32):
     the anchor (xa, ya) = projection of the splat centre; returns (Tu', Tv', Tw, xa, ya)."""
     V, _, fx, fy, cx, cy = cam.cast(dtype)
     tu, tv, _ = quat_frame(quats.to(dtype))
-    glob = _c(glob_scale, dtype)
+    glob = _arg32(glob_scale, dtype)
     su = scales[:, 0].to(dtype) * glob
     sv = scales[:, 1].to(dtype) * glob
     a = tu * su[:, None]
@@ -343,7 +351,7 @@ def _splat_table(inp: RasterInputs, dtype):
     V, campos, fx, fy, cx, cy = inp.cam.cast(dtype)
     Tu, Tv, Tw, xa, ya = splat_anchored(inp.means, inp.scales, inp.glob_scale, inp.quats, inp.cam, dtype)
     tu, tv, tw = quat_frame(inp.quats.to(dtype))
-    glob = _c(inp.glob_scale, dtype)
+    glob = _arg32(inp.glob_scale, dtype)
     su = inp.scales[:, 0].to(dtype) * glob
     sv = inp.scales[:, 1].to(dtype) * glob
     mu = inp.means.to(dtype)
@@ -485,6 +493,8 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
                 if tt.requires_grad:
                     tt.register_hook(lambda gr, nm=nm, rec=rec: rec.__setitem__(nm, gr.detach().clone()))
             CAPTURE.append(rec)
+        else:
+            rec = None
         if decisions is None:
             nz = pzc != 0
         else:
@@ -618,6 +628,13 @@ def _render(inp: RasterInputs, dtype, tile_ranges, sorted_ids, decisions, edit=N
                 edit["out"].index_add_(0, idx, vals[sel].to(torch.float64))
         kk = torch.arange(K)[:, None].expand(K, P)
         last = torch.where(incl, kk, torch.full_like(kk, -1)).max(0).values
+        if rec is not None:  # (precision analysis: the pair values of this fp32 pass)
+            rec.update({k: v.detach().clone() for k, v in dict(
+                u=u, v=v, ipz=ipz, use3=use3, zz=zz, G=G, a_raw=a_raw, alpha=alpha, incl=incl, w=w,
+                xy=g["xy"], rgb=g["rgb"], nrm=g["nrm"], Tw=g["Tw"], opac=g["opac"], Tfin=Tfin, M1=M1, M2=M2,
+                last=last).items()})
+            rec["aclamp"] = aclamp.clone()
+            rec["t"] = t
         rows["img"].append(img); rows["depth"].append(depth); rows["reg"].append(reg)
         rows["T"].append(Tfin); rows["tex"].append(texo); rows["normal"].append(normal)
         rows["M1"].append(M1); rows["M2"].append(M2)

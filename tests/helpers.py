@@ -66,7 +66,9 @@ def _differentiable(settings, outputs):
     return outputs
 
 
-def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64, outputs=None):
+def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64, outputs=None, flip_mask=None):
+    """flip_mask: use this mask (e.g. one computed on another machine, whose CPU exp may round differently) instead of
+    the one this run's margins give."""
     inp = case.inp
     leaves = {}
     if grads:
@@ -77,7 +79,7 @@ def oracle_run(case: Case, grads=True, seed=5, grad_dtype=torch.float64, outputs
     o32, o64, aux = O.rasterize(inp, grad_dtype=grad_dtype)
     # pixels with a threshold decision within FLIP_MARGIN (an exp ulp may flip it on the GPU; the forward check
     # accounts for them) take no upstream gradient in either run, so a flipped pair cannot enter the comparison
-    case.flip_mask = aux["margin"] < FLIP_MARGIN
+    case.flip_mask = aux["margin"] < FLIP_MARGIN if flip_mask is None else flip_mask
     out = {}
     outputs = _differentiable(inp.settings, outputs)
     if grads:
