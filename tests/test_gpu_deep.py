@@ -16,7 +16,7 @@ import torch
 
 from helpers import DIFF, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, make_window_case, \
     oracle_run
-from test_gpu_parity import COND_FACTOR, GRAD_RTOL, _report
+from test_gpu_parity import GRAD_RTOL, _report
 
 pytestmark = pytest.mark.gpu
 
@@ -45,10 +45,8 @@ def _check(name, case, outputs=None, min_depth=0):
     _report(f"{name} bwd fp32-oracle norm-rel", inh_n)
     _report(f"{name} bwd fp32-oracle max-rel", inh)
     for k in DIFF:
-        nb = max(GRAD_RTOL, COND_FACTOR * inh_n[k])
-        assert norm_errs[k] <= nb, f"{name}: grad {k} norm-wise rel err {norm_errs[k]:.3e} > {nb:.3e}"
-        bound = max(GRAD_RTOL, COND_FACTOR * inh[k])
-        assert errs[k] <= bound, f"{name}: grad {k} max rel err {errs[k]:.3e} > {bound:.3e}"
+        assert norm_errs[k] <= GRAD_RTOL, f"{name}: grad {k} norm-wise rel err {norm_errs[k]:.3e} > {GRAD_RTOL:.0e}"
+        assert errs[k] <= GRAD_RTOL, f"{name}: grad {k} max rel err {errs[k]:.3e} > {GRAD_RTOL:.0e}"
     return tr, last
 
 

@@ -3,22 +3,20 @@
 Tolerances (written here, per north_star): integer/index work bit-exact; forward images within
 1e-5 abs + 1e-5 rel of the oracle's fp64 evaluation (same fp32 decisions).  Gradients, against
 the oracle's fp64 autograd of the same function:
-  * norm-wise relative error ||g - ref|| / ||ref|| and element-wise max|g - ref| / max|ref| are
-    each <= max(1e-5, 4 x the same error of the oracle's OWN fp32 autograd evaluation of the same
-    function).  The 4x-of-fp32 clause is the conditioning floor of the fp32 per-splat record: the raster
-    record is evaluated in fp64 and rounded once (raster.hip setup_kernel; setup_bwd_chain in fp64), and
-    tools/grad_precision.py shows that exact arithmetic on that rounded record alone leaves means / quats
-    errors of ~5e-5 on the cfg3 96x96 window (near-edge-on splats: (u, v) = p.xy / p.z ill-conditioned).
-    Measured (profiles/r03_deep_parity_fp64record.log, norm-wise): means / quats 6.6e-5 / 4.2e-5 on cfg3
-    96x96 (floor 5.0e-5 / 4.3e-5), 5.4e-6 / 7.2e-6 on cfg3 48x48, 9.8e-6 / 1.1e-5 on cfg2 128x128,
-    7.2e-6 / 3.5e-5 on cfg1; every other gradient is within 1e-5 outright on these cases (max-element:
-    texture 5.0e-6, centers 7.2e-6, uv0 8.4e-6).
+  * norm-wise relative error ||g - ref|| / ||ref|| and element-wise max|g - ref| / max|ref| are each
+    <= 1e-5, outright.  The raster record is evaluated in fp64 and rounded once (raster.hip setup_kernel;
+    setup_bwd_chain in fp64), and near-edge-on splats (|normal . view dir| < 0.1, whose p = dx A + dy B + (0, 0, Pz)
+    is a small difference of larger terms) take p from their fp64 setup row in the forward and the backward alike
+    (DESIGN.md §4); the oracle restates both (RasterInputs.hp) and evaluates with the fp32-rounded camera
+    intrinsics the kernels receive.  The oracle's own fp32 autograd error is printed beside each result (it is
+    the yardstick, no longer part of the bound).  Measured (profiles/r06_parity_hp.log): every gradient of every
+    case <= 8.8e-6 norm-wise and <= 4.6e-6 max-element (cfg3 96x96: means / quats 3.0e-6 / 3.3e-6 norm-wise).
 """
 import numpy as np
 import pytest
 import torch
 
-from helpers import COND_FACTOR, DIFF, GRAD_RTOL, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, \
+from helpers import DIFF, GRAD_RTOL, assert_close_fwd, gpu_run, grad_norm_err, grad_rel_err, make_case, \
     oracle_run, upstream
 from oracle import raster as O
 
@@ -190,10 +188,8 @@ def _check_raster(name, outputs):
     _report(f"{name} bwd fp32-oracle max-rel", inherent)
     _report(f"{name} bwd norm-rel", norm_errs)
     for k in DIFF:
-        nb = max(GRAD_RTOL, COND_FACTOR * inherent_n[k])
-        assert norm_errs[k] <= nb, f"{name}: grad {k} norm-wise rel err {norm_errs[k]:.3e} > {nb:.3e}"
-        bound = max(GRAD_RTOL, COND_FACTOR * inherent[k])
-        assert errs[k] <= bound, f"{name}: grad {k} max rel err {errs[k]:.3e} > {bound:.3e}"
+        assert norm_errs[k] <= GRAD_RTOL, f"{name}: grad {k} norm-wise rel err {norm_errs[k]:.3e} > {GRAD_RTOL:.0e}"
+        assert errs[k] <= GRAD_RTOL, f"{name}: grad {k} max rel err {errs[k]:.3e} > {GRAD_RTOL:.0e}"
 
 
 def test_empty_and_offscreen():
