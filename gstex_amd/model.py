@@ -296,9 +296,10 @@ class GStexTrainer:
     # ------------------------------------------------------------------ forward
     def render(self, view: View, sh_degree_now: int | None = None, composite: bool = True, geometry: bool | None = None):
         """get_outputs (gstex.py:992-1236), training branch.  geometry: render depth / distortion / normal (default:
-        the trainer's geometry_outputs)."""
+        the trainer's geometry_outputs).  sh_degree_now: default min(step // sh_degree_interval, sh_degree), as
+        get_outputs evaluates it in training and eval alike (gstex.py:1103)."""
         means = self.means
-        deg = self.sh_degree if sh_degree_now is None else sh_degree_now
+        deg = self.sh_degree_now() if sh_degree_now is None else sh_degree_now
         if self._pending_tex is not None and not self._pending_collective and self.pairs is not None:
             # the deferred texel update first (read-back-free step: there is no pair-count wait to fill): ~90 us of
             # streaming work the device starts on while the host enqueues the step's short preprocessing and binning
