@@ -48,9 +48,6 @@ constexpr int kThreads = kTilePixels;  // 256
 #define GSTEX_UNIT_COARSE 3  // backward unit-order cost buckets of 2^k visits (inside a bucket: about slot order,
                              // better L2 reuse of texel blocks). Measured: 3 same time, bwd fetch -18 %; 5, 6 slower
 #endif
-#ifndef GSTEX_FWD_HALF
-#define GSTEX_FWD_HALF 0  // 1 (C = 3): each wave's two 8x4 half-blocks walk their own cull lists (VERDICT r05 #4 experiment)
-#endif
 #ifndef GSTEX_FWD_OCC
 #define GSTEX_FWD_OCC 6  // forward waves per SIMD the register allocation targets (measured: 8 at 64 VGPRs is slower; 5 with
                          // a record prefetch or a second pending texel set, both measured slower in round 5)
@@ -396,11 +393,6 @@ __device__ __forceinline__ void hit_p_hp_uniform(const double* __restrict__ row,
              (float)__builtin_fma(dy, row[H_B + 2], __builtin_fma(dx, row[H_A + 2], row[H_PZ]))};
 }
 
-// The same with a per-lane row (the forward's half-block walk: the two halves of a wave visit different splats)
-__device__ __forceinline__ void hit_p_hp_lane(const double* __restrict__ row, float px, float py, Hit& h) {
-    hit_p_hp_uniform(row, px, py, h);
-}
-
 // Returns false when the pair is skipped (degenerate, behind the near plane or alpha < 1/255).  h.dx, h.dy, h.p from
 // hit_p / hit_p_hp.
 __device__ __forceinline__ bool eval_rest(const Rec& r, float px, float py, bool aa, Hit& h) {
@@ -484,25 +476,6 @@ __device__ __forceinline__ void load_texel_quad_unclamped(__amdgpu_buffer_rsrc_t
                                                           float (&t11)[3]) {
     const int rowb = w * 12;  // row stride in bytes (wave-uniform: scalar when w is)
     const int o00 = (int)(__umul24(b.i0, (unsigned)rowb) + __umul24(b.j0, 12u));
-    const int o10 = o00 + rowb;
-    const auto a = __builtin_amdgcn_raw_buffer_load_b96(rs, o00, 0, 0);
-    const auto c = __builtin_amdgcn_raw_buffer_load_b96(rs, o00 + 12, 0, 0);
-    const auto d = __builtin_amdgcn_raw_buffer_load_b96(rs, o10, 0, 0);
-    const auto e = __builtin_amdgcn_raw_buffer_load_b96(rs, o10 + 12, 0, 0);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        t00[k] = __int_as_float(a[k]);
-        t01[k] = __int_as_float(c[k]);
-        t10[k] = __int_as_float(d[k]);
-        t11[k] = __int_as_float(e[k]);
-    }
-}
-// The same over a whole-texture resource with the block's byte offset per lane (the forward's half-block walk)
-__device__ __forceinline__ void load_texel_quad_lane(__amdgpu_buffer_rsrc_t rs, int ob, const Bilerp& b, int w,
-                                                     float (&t00)[3], float (&t01)[3], float (&t10)[3],
-                                                     float (&t11)[3]) {
-    const int rowb = w * 12;
-    const int o00 = ob + (int)(__umul24(b.i0, (unsigned)rowb) + __umul24(b.j0, 12u));
     const int o10 = o00 + rowb;
     const auto a = __builtin_amdgcn_raw_buffer_load_b96(rs, o00, 0, 0);
     const auto c = __builtin_amdgcn_raw_buffer_load_b96(rs, o00 + 12, 0, 0);
@@ -660,21 +633,6 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         return kDefer ? __builtin_fmaf(tex[c], tex_scale, tex_bias * texw) : tex[c];
     };
     const int lane = tid & 63, wave = tid >> 6;
-    // half-block walk (GSTEX_FWD_HALF, C = 3 with the deferred texel path): the halves' cull boxes (rows 0-3 and 4-7
-    // of the quadrant, +-0.05 px like wave_block's) and a resource over the whole texture (the halves' blocks differ)
-    constexpr bool kHalf = GSTEX_FWD_HALF && C == 3 && kDefer;
-    const bool upper = lane >= 32;
-    float hy0A = 0.f, hy1A = 0.f, hy0B = 0.f, hy1B = 0.f;
-    const __amdgpu_buffer_rsrc_t rs_all = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(texture), 0, (int)((unsigned)n_texels * 12u), 0x00020000);
-    if constexpr (kHalf) {
-        auto uni = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
-        const float yq = (float)(ty * kTile + (wave >> 1) * 8) + 0.5f;
-        hy0A = uni(yq - 0.05f);
-        hy1A = uni((yq + 3.0f) + 0.05f);
-        hy0B = uni((yq + 4.0f) - 0.05f);
-        hy1B = uni((yq + 7.0f) + 0.05f);
-    }
     const size_t vm_base = visit_mask_base(rng.x, tile);
     const int sbase = seg_base(rng.x, tile);
     int seg_visits = 0, cur_seg = 0;  // this wave's splat evaluations in the current segment (backward cost)
@@ -729,84 +687,6 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             }
         }
         __syncthreads();
-        if constexpr (kHalf) {
-        // half-block walk: lanes 0-31 (rows 0-3 of the quadrant) and 32-63 (rows 4-7) each test the batch against
-        // their own 8x4 box and walk their own list, the two halves visiting different splats side by side; the
-        // backward gets the union (tighter than the quadrant box's cull, and every pair it drops cannot reach
-        // alpha >= 1/255 anywhere in the quadrant)
-        unsigned long long todoA[kWords], todoB[kWords];
-#pragma unroll
-        for (int hb = 0; hb < kWords; ++hb) {
-            const int jj = hb * 64 + lane;
-            const int jc = jj < nb ? jj : 0;
-            const bool hitA = jj < nb && wave_may_hit<kFwdBatch>(s_rec, jc, wx0, wx1, hy0A, hy1A, aa);
-            const bool hitB = jj < nb && wave_may_hit<kFwdBatch>(s_rec, jc, wx0, wx1, hy0B, hy1B, aa);
-            todoA[hb] = __ballot(hitA);
-            todoB[hb] = __ballot(hitB);
-            if (visit_masks && lane == 0 && hb * 64 < nb)
-                visit_masks[(vm_base + ((b0 - rng.x) >> 6) + hb) * 4 + wave] = todoA[hb] | todoB[hb];
-        }
-        bool all_done = __all(GSTEX_FWD_DONE);
-        for (int hb = 0; hb < kWords && !all_done; ++hb) {
-          unsigned long long mA = todoA[hb], mB = todoB[hb];
-          while (mA | mB) {
-            const int jA = mA ? __builtin_ctzll(mA) : 64, jB = mB ? __builtin_ctzll(mB) : 64;
-            mA &= mA - 1;
-            mB &= mB - 1;
-            seg_visits += (jA < 64) + (jB < 64) - (jA == jB && jA < 64);
-            const int my = upper ? jB : jA;
-            const bool has = my < 64;
-            const int j = hb * 64 + (has ? my : 0);
-            const Rec r = read_rec<kFwdBatch>(s_rec, j);
-            Hit h;
-            hit_p(r, px, py, h);
-            if (hp_records && __ballot(has && __float_as_int(r.mark) < 0)) {
-                if (has && __float_as_int(r.mark) < 0) hit_p_hp_lane(hp_records + (size_t)s_gid[j] * H_FIELDS, px, py, h);
-            }
-            const bool ok = has && eval_rest(r, px, py, aa, h) && alive != 0.0f;
-            const float test_T = T * (1.0f - h.alpha);
-            const bool stop = ok && test_T < kTMin;
-            alive = stop ? 0.0f : alive;
-            if (ok && !stop) {
-                const float w = h.alpha * T;
-                const bool has_tex = r.h * r.w > 0 && r.off + r.h * r.w <= n_texels;
-                float tu, tv;
-                tex_coords(r, h.u, h.v, tu, tv);
-                const Bilerp b = bilerp_xy(tu, tv, r.h, r.w, r.hm1, r.wm1);
-                fold_pending();
-                if (has_tex) {
-                    load_texel_quad_lane(rs_all, r.off * 12, b, r.w, p00, p01, p10, p11);
-                    pax = b.ax;
-                    pay = b.ay;
-                    pw = w;
-                    pend = 1.0f;
-                }
-                img[0] = __builtin_fmaf(r.rgb[0], w, img[0]);
-                img[1] = __builtin_fmaf(r.rgb[1], w, img[1]);
-                img[2] = __builtin_fmaf(r.rgb[2], w, img[2]);
-                if (GEOF) {
-                    D = D + h.z * w;
-                    nrm[0] = nrm[0] + r.nrm[0] * w;
-                    nrm[1] = nrm[1] + r.nrm[1] * w;
-                    nrm[2] = nrm[2] + r.nrm[2] * w;
-                }
-                if (GEOF && dreg) {
-                    const float A = 1.0f - T;
-                    const float mm = kFarRatio * (1.0f - kNear * grad_rcp(h.z));
-                    reg = reg + ((mm * mm * A + M2) - 2.0f * mm * M1) * w;
-                    M1 = M1 + mm * w;
-                    M2 = M2 + mm * mm * w;
-                }
-                T = test_T;
-                last = b0 - rng.x + j;
-            }
-            if (__builtin_amdgcn_ballot_w64(alive != 0.0f) == 0) {
-                all_done = true;
-                break;
-            }
-          }
-        }
-        } else {
         // the batch splats whose contribution region meets this wave's 8x8 block, tested all at once
         unsigned long long todo[kWords];
 #pragma unroll
@@ -834,10 +714,8 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
             Hit h;
             hit_p(r, px, py, h);
             // a near-edge-on splat (the record opacity's sign bit, wave-uniform): p from its fp64 row
-#ifndef GSTEX_HP_FWD_OFF  // (timing experiment only: the forward without its near-edge-on branch)
             if (hp_records && __builtin_amdgcn_readfirstlane(__float_as_int(r.mark)) < 0)
                 hit_p_hp_uniform(hp_records + (size_t)__builtin_amdgcn_readfirstlane(s_gid[j]) * H_FIELDS, px, py, h);
-#endif
             const bool ok = eval_rest(r, px, py, aa, h) && alive != 0.0f;
             const float test_T = T * (1.0f - h.alpha);
             const bool stop = ok && test_T < kTMin;
@@ -900,7 +778,6 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
                 break;
             }
           }
-        }
         }
     }
     fold_pending();
@@ -1065,8 +942,7 @@ __device__ __forceinline__ float mask_one(unsigned long long m) {
 template <int NV>
 __device__ __forceinline__ bool seg_reduce_rows(int key, float (&v)[NV]) {
     constexpr int SW = GSTEX_SEG_W;
-    static_assert(SW == 1 || SW == 2 || SW == 4 || SW == 8 || SW == 16, "segment width");
-    if constexpr (SW == 1) return key >= 0;  // (experiment: no scan, every live lane stages its own values)
+    static_assert(SW == 2 || SW == 4 || SW == 8 || SW == 16, "segment width");
     constexpr unsigned long long kFirst = SW == 2 ? 0x5555555555555555ull : SW == 4 ? 0x1111111111111111ull
                                         : SW == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
     constexpr unsigned long long kLast = kFirst << (SW - 1);
@@ -1119,17 +995,9 @@ __device__ __forceinline__ int fixed_round(float y) {  // y already scaled by 2^
     return q;
 }
 constexpr int kTexFixBits = 30;
-#ifndef GSTEX_TEX_F32
-#define GSTEX_TEX_F32 0  // 1: stage the run tails as fp32 LDS atomics (ds_add_f32), no fixed point and no bound
-#endif
+
 // (fp32 staging with ds_add_f32 instead measured 2x slower: 3.2 vs 1.57 ms, round 2; 3.0 vs 1.4 ms, round 4)
-__device__ __forceinline__ void stage_add(int* a, float y) {
-#if GSTEX_TEX_F32
-    atomicAdd(reinterpret_cast<float*>(a), y);
-#else
-    atomicAdd(a, fixed_round(y));
-#endif
-}
+__device__ __forceinline__ void stage_add(int* a, float y) { atomicAdd(a, fixed_round(y)); }
 #ifndef GSTEX_FLUSH_U
 #define GSTEX_FLUSH_U 4
 #endif
@@ -1335,7 +1203,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 if (has_tex) {
                     tkey = (int)(__umul24(b.i0, r.w) + b.j0) | ((b.i1 - b.i0) << 29) | ((b.j1 - b.j0) << 30);
                     tw = w * tex_scale;  // d value / d stored texel
-                    if (!GSTEX_TEX_F32) P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
+                    P[kMBound] = fabsf(tw) * gabs;  // summed by the reduce: the visit's fixed-point bound
                     tax = b.ax;
                     tay = b.ay;
                 }
@@ -1460,17 +1328,12 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                 // S = 30 - e with vis_M = m 2^e, m in [0.5, 1) (frexp), from the float's exponent field on the scalar
                 // unit (vis_M is wave-uniform); 2^S and 2^-S are built as float bit patterns, so the scalings below
                 // are exact multiplies (what ldexp computed); S is clamped to [-126, 126] (denormal / zero bounds)
-#if GSTEX_TEX_F32
-                const float pow_S = 1.0f, pow_mS = 1.0f;
-                (void)vis_M;
-#else
                 const uint32_t mbits = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(vis_M));
                 const int biased = (int)((mbits >> 23) & 0xFFu);
                 const int e_m = biased > 0 ? biased - 126 : 0;
                 const int tex_S = min(max(kTexFixBits - e_m, -126), 126);
                 const float pow_S = __uint_as_float((uint32_t)(tex_S + 127) << 23);     // 2^S
                 const float pow_mS = __uint_as_float((uint32_t)(127 - tex_S) << 23);    // 2^-S
-#endif
                 const float twq = tw * pow_S;
                 float tg[4 * CM];
                 {
@@ -1537,11 +1400,7 @@ __global__ __launch_bounds__(64, (BwdShape<C, GEO>::kWaves)) void raster_bwd_ker
                             GSTEX_STAT(6, __popcll(__ballot(v[k] != 0)));
                             if (v[k] == 0) continue;
                             s_texq[e0 + 64 * k] = 0;
-#if GSTEX_TEX_F32
-                            atomicAdd(dst + e0 + 64 * k, __int_as_float(v[k]));
-#else
                             atomicAdd(dst + e0 + 64 * k, (float)v[k] * pow_mS);
-#endif
                         }
                     }
                 }
