@@ -289,9 +289,6 @@ __device__ __forceinline__ bool conic_edge(float ax, float ay, float az, float q
 // (the cull fields are record dwords [0, 12): planes 0-2, RecField)
 __device__ __forceinline__ bool may_hit_planes(float4 p0, float4 p1, float4 p2, float wx0, float wx1, float wy0,
                                                float wy1, bool aa) {
-#ifdef GSTEX_NO_CULL
-    return true;  // diagnostic builds only: every listed splat is evaluated
-#endif
     const float v[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
     const float opac = fabsf(v[R_OPAC]);
     if (!(opac * 255.0f > 1.0f)) return false;
