@@ -192,6 +192,24 @@ def _check_raster(name, outputs):
         assert errs[k] <= GRAD_RTOL, f"{name}: grad {k} max rel err {errs[k]:.3e} > {GRAD_RTOL:.0e}"
 
 
+def test_raster_without_near_edge_on_rows(monkeypatch):
+    """GSTEX_HP=0 (no hp_records buffer: the marks are ignored, every pair evaluated from the fp32 record) against the
+    oracle restating that path (RasterInputs.hp = False): the forward within the usual tolerance; the gradients
+    within 1e-4 (the fp32 record's conditioning, DESIGN.md §4, is what the rows remove)."""
+    from gstex_amd import ops
+
+    monkeypatch.setattr(ops, "HP_RECORDS", False)
+    case = make_case(**CASES["no_reg"])
+    case.inp.hp = False
+    o32, o64, aux, og = oracle_run(case, grads=True)
+    gout, gg = gpu_run(case, grads=True)
+    assert_close_fwd(gout, o64, margin=aux["margin"])
+    errs = {k: grad_norm_err(gg[k], og[k]) for k in DIFF}
+    _report("no hp rows bwd norm-rel", errs)
+    for k, e in errs.items():
+        assert e <= 1e-4, f"grad {k} norm-wise rel err {e:.3e}"
+
+
 def test_empty_and_offscreen():
     case = make_case(n=50, n_texels=1000, H=32, W=32, seed=10)
     case.nth = torch.zeros_like(case.nth)  # nothing visible
