@@ -94,8 +94,10 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int H, int W, int C, cons
         s_y[ry][rx] = yv;
     }
     __syncthreads();
-    // rows: 26 x 16 horizontal filters of the five quantities
+    // rows: 26 x 16 horizontal filters of the five quantities (fused multiply-adds: the window sums need no fixed
+    // operation order -- the loss and its gradient are compared with tolerances, only the composite bit for bit)
     for (int i = tid; i < kReg * kLT; i += 256) {
+#pragma clang fp contract(fast)
         const int ry = i / kLT, cx = i % kLT;
         float a = 0.f, b = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
 #pragma unroll
@@ -119,6 +121,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(int H, int W, int C, cons
     const int py = y0 + cy, px = x0 + cx;
     float ssum = 0.f;
     if (py < Hv && px < Wv) {
+#pragma clang fp contract(fast)
         float q[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < kWin; ++k)
@@ -231,6 +234,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int H, int W, int C, cons
         __syncthreads();
         // transposed rows: for output column hx, sum_k w[k] G(position hx + 10 - k)
         for (int i = tid; i < kReg * kLT; i += 256) {
+#pragma clang fp contract(fast)
             const int ry = i / kLT, hx = i % kLT;
             float a = 0.f, b = 0.f, d = 0.f;
 #pragma unroll
@@ -246,6 +250,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(int H, int W, int C, cons
         __syncthreads();
         gch[c] = 0.f;
         if (out) {
+#pragma clang fp contract(fast)
             float t0 = 0.f, t1 = 0.f, t2 = 0.f;
 #pragma unroll
             for (int k = 0; k < kWin; ++k) {
