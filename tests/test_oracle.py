@@ -252,3 +252,26 @@ def test_texture_edit_uniform_stroke_known_answer():
     # total weight: sum_texels out[:, 4] = sum_pixels w (bilinear weights sum to 1 per pair)
     fwd = O._render(inp, torch.float32, *O.bin_and_sort(inp.centers, inp.extents, inp.depths, H, W)[1:3], None)
     assert abs(float(out[:, 4].sum()) - float(fwd["out"]["alpha"].double().sum())) < 1e-4
+
+
+def test_near_edge_on_rows_change_only_the_ill_conditioned_pairs():
+    """RasterInputs.hp (raster.hip hit_p_hp: near-edge-on splats' p from their fp64 row, rounded once): the fp32 pass
+    moves by fp32 noise only (the fp64 evaluation is the same function), and only pixels of marked splats move."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from helpers import make_case
+
+    case = make_case(n=300, n_texels=20000, H=48, W=48, seed=12)
+    tab = O._splat_table(case.inp, F64)
+    assert 0 < int(tab["hp"].sum()) < case.inp.means.shape[0], "the scene must hold marked and unmarked splats"
+    with_hp, _, aux = O.rasterize(case.inp)
+    case.inp.hp = False
+    without, _, _ = O.rasterize(case.inp)
+    ok = aux["margin"] >= 1e-5
+    moved = False
+    for k in ("img", "alpha", "depth", "tex", "normal"):
+        d = (with_hp[k].double() - without[k].double()).abs()
+        d = d[ok] if d.dim() == 2 else d[ok]
+        assert float(d.max()) <= 1e-5, k
+        moved |= bool((d > 0).any())
+    assert moved, "some near-edge-on pair must change in its last bits"
