@@ -18,8 +18,9 @@ from . import _lib
 from ._lib import PARTIAL_FLOATS, PARTIAL_FLOATS_PHOTO, REC_FLOATS, call, ptr
 
 BLOCK_WIDTH = 16
-# near-edge-on splats re-evaluated in fp64 by the raster backward (gstex_raster_setup / gstex_raster_bwd hp_records,
-# ABI 18); GSTEX_HP=0 evaluates every pair in fp32 (the round-5 numerics)
+# near-edge-on splats' homogeneous points evaluated from their fp64 setup rows by the raster forward and backward alike
+# (gstex_raster_setup / _fwd_zero / _bwd hp_records, ABI 18); GSTEX_HP=0 evaluates every pair from the
+# fp32 record (the round-5 numerics)
 HP_RECORDS = os.environ.get("GSTEX_HP", "1") != "0"
 # diagnostics: called with (partials, row_flags, records, hp rows) after each raster backward (tools/hp_partials.py)
 PARTIALS_HOOK = None
