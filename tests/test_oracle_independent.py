@@ -124,3 +124,145 @@ def test_world_space_ray_restatement_matches_oracle(name, kw):
         err = float(np.abs(a - b).max())
         # fp64 both: agreement to rounding (the fp32 oracle output differs by ~2e-7 here, so this is a sharp check)
         assert err <= 1e-12 * max(1.0, float(np.abs(b).max())), f"{name}: {k} differs by {err:.3e}"
+
+
+def ray_render_torch(inp, leaves):
+    """The same world-space restatement in torch float64, differentiable w.r.t. the leaves (means, scales, quats,
+    opacities, rgbs, texture, centers): per tile, every (splat, pixel) pair's ray-plane system solved by Cramer's
+    rule, the pair decisions (skips, low-pass branch, termination) taken in float64 without gradient, the composite
+    as a product scan.  Outputs img, alpha, depth, tex, normal of the whole image."""
+    cam = inp.cam
+    H, W = cam.H, cam.W
+    f32 = lambda v: float(np.float32(v))  # noqa: E731
+    fx, fy, cx, cy = f32(cam.fx), f32(cam.fy), f32(cam.cx), f32(cam.cy)
+    F = torch.float64
+    V = cam.viewmat.to(F)
+    campos = cam.campos.to(F)
+    mu = leaves["means"].to(F)
+    glob = f32(inp.glob_scale)
+    su = leaves["scales"][:, 0].to(F) * glob
+    sv = leaves["scales"][:, 1].to(F) * glob
+    q = leaves["quats"].to(F)
+    q = q / q.norm(dim=-1, keepdim=True)
+    w_, x_, y_, z_ = q.unbind(-1)
+    t_u = torch.stack([1 - 2 * (y_ * y_ + z_ * z_), 2 * (x_ * y_ + w_ * z_), 2 * (x_ * z_ - w_ * y_)], -1)
+    t_v = torch.stack([2 * (x_ * y_ - w_ * z_), 1 - 2 * (x_ * x_ + z_ * z_), 2 * (y_ * z_ + w_ * x_)], -1)
+    t_w = torch.stack([2 * (x_ * z_ + w_ * y_), 2 * (y_ * z_ - w_ * x_), 1 - 2 * (x_ * x_ + y_ * y_)], -1)
+    R, tt = V[:, :3], V[:, 3]
+    c = mu @ R.T + tt
+    a = (t_u * su[:, None]) @ R.T
+    b = (t_v * sv[:, None]) @ R.T
+    flip = ((t_w * (campos[None] - mu)).sum(-1) < 0).detach()
+    nrm = torch.where(flip[:, None], -t_w, t_w)
+    opac = leaves["opacities"][:, 0].to(F)
+    rgb = leaves["rgbs"].to(F)
+    ctr = leaves["centers"].to(F)
+    tex = leaves["texture"].to(F)
+    dims = inp.texture_dims.long()
+    uv0 = inp.uv0[:, 0, :].to(F)
+    um, vm = inp.umap[:, 0, :].to(F), inp.vmap[:, 0, :].to(F)
+    aa = bool(inp.settings & O.SETTING_AA_BLUR)
+    C = tex.shape[1]
+    _, tile_ranges, sorted_ids, _ = O.bin_and_sort(inp.centers, inp.extents, inp.depths, H, W)
+    tiles_x = (W + 15) // 16
+    out = {k: torch.zeros((H, W) + s, dtype=F) for k, s in (("img", (3,)), ("alpha", ()), ("depth", ()),
+                                                              ("tex", (C,)), ("normal", (3,)))}
+    rows = {k: [] for k in out}
+    pix_all = []
+    for t, (s, e) in enumerate(tile_ranges):
+        if e <= s:
+            continue
+        ids = torch.from_numpy(np.asarray(sorted_ids[s:e], dtype=np.int64))
+        ty, tx = divmod(t, tiles_x)
+        ys, xs = torch.meshgrid(torch.arange(ty * 16, min(ty * 16 + 16, H)), torch.arange(tx * 16, min(tx * 16 + 16, W)),
+                                indexing="ij")
+        ys, xs = ys.reshape(-1), xs.reshape(-1)
+        d = torch.stack([(xs.to(F) + 0.5 - cx) / fx, (ys.to(F) + 0.5 - cy) / fy, torch.ones(len(xs), dtype=F)], -1)
+        A_, B_, C_ = a[ids][:, None, :], b[ids][:, None, :], c[ids][:, None, :]
+        D_ = -d[None, :, :]
+        det = lambda p, q_, r: (p * torch.cross(q_, r, dim=-1)).sum(-1)  # noqa: E731
+        M0 = det(A_.expand(-1, len(xs), -1), B_.expand(-1, len(xs), -1), D_.expand(len(ids), -1, -1))
+        rhs = -C_.expand(-1, len(xs), -1)
+        Ae, Be, De = A_.expand_as(rhs), B_.expand_as(rhs), D_.expand_as(rhs)
+        u = det(rhs, Be, De) / M0
+        v = det(Ae, rhs, De) / M0
+        lam = det(Ae, Be, rhs) / M0
+        rho3 = u * u + v * v
+        rho2 = 2.0 * ((ctr[ids][:, None, 0] - (xs.to(F) + 0.5)[None]) ** 2 + (ctr[ids][:, None, 1] - (ys.to(F) + 0.5)[None]) ** 2)
+        use3 = (rho3 <= rho2).detach() if aa else torch.ones_like(rho3, dtype=torch.bool)
+        rho = torch.where(use3, rho3, rho2)
+        z = torch.where(use3, lam, c[ids][:, None, 2].expand_as(lam))
+        a_raw = opac[ids][:, None] * torch.exp(-0.5 * rho)
+        alpha = torch.clamp(a_raw, max=AMAX)
+        with torch.no_grad():
+            valid = (z >= NEAR) & (alpha >= AMIN)
+            ae = torch.where(valid, alpha, torch.zeros_like(alpha))
+            Tafter = torch.cumprod(1.0 - ae, 0)
+            stop = valid & (Tafter < TMIN)
+            first = torch.where(stop.any(0), stop.to(F).argmax(0), torch.full((len(xs),), len(ids)))
+            incl = valid & (torch.arange(len(ids))[:, None] < first[None, :])
+        ai = torch.where(incl, alpha, torch.zeros_like(alpha))
+        Tb = torch.cat([torch.ones(1, len(xs), dtype=F), torch.cumprod(1.0 - ai, 0)[:-1]], 0)
+        w = ai * Tb
+        hit = mu[ids][:, None, :] + u[..., None] * (su[ids][:, None, None] * t_u[ids][:, None, :]) + \
+            v[..., None] * (sv[ids][:, None, None] * t_v[ids][:, None, :])
+        hh, ww, off = dims[ids, 0][:, None], dims[ids, 1][:, None], dims[ids, 2][:, None]
+        has = (hh * ww > 0)
+        xr = hh.to(F) * (uv0[ids][:, None, 0] + ((hit - mu[ids][:, None, :]) * um[ids][:, None, :]).sum(-1))
+        yr = ww.to(F) * (uv0[ids][:, None, 1] + ((hit - mu[ids][:, None, :]) * vm[ids][:, None, :]).sum(-1))
+        xc = torch.minimum(torch.clamp(xr, min=0.0), (hh - 1).clamp(min=0).to(F))
+        yc = torch.minimum(torch.clamp(yr, min=0.0), (ww - 1).clamp(min=0).to(F))
+        i0, j0 = xc.detach().floor().long(), yc.detach().floor().long()
+        i1, j1 = torch.minimum(i0 + 1, (hh - 1).clamp(min=0)), torch.minimum(j0 + 1, (ww - 1).clamp(min=0))
+        ax, ay = (xc - i0.to(F))[..., None], (yc - j0.to(F))[..., None]
+        if tex.shape[0]:
+            fetch = lambda i, j: tex[torch.where(has, off + i * ww + j, torch.zeros_like(i)).clamp(0, tex.shape[0] - 1)]  # noqa: E731
+            val = (1 - ax) * ((1 - ay) * fetch(i0, j0) + ay * fetch(i0, j1)) + ax * ((1 - ay) * fetch(i1, j0) + ay * fetch(i1, j1))
+            val = torch.where(has[..., None], val, torch.zeros_like(val))
+        else:
+            val = torch.zeros(len(ids), len(xs), C, dtype=F)
+        rows["img"].append((w[..., None] * rgb[ids][:, None, :]).sum(0))
+        rows["alpha"].append(1.0 - torch.prod(1.0 - ai, 0))
+        rows["depth"].append((w * torch.where(incl, z, torch.ones_like(z))).sum(0))
+        rows["tex"].append((w[..., None] * val).sum(0))
+        rows["normal"].append((w[..., None] * nrm[ids][:, None, :]).sum(0))
+        pix_all.append(ys * W + xs)
+    pix = torch.cat(pix_all)
+    for k in out:
+        flat = out[k].reshape(H * W, *out[k].shape[2:]).index_put((pix,), torch.cat(rows[k], 0))
+        out[k] = flat.reshape(out[k].shape)
+    return out
+
+
+@pytest.mark.parametrize("n_texels,keys", [
+    # 2DGS mode: every gradient
+    (0, ("rgbs", "opacities", "means", "scales", "quats", "centers")),
+    # textured: the oracle takes the texel cell of each pair from the fp32 pass (what the kernels see), this
+    # restatement from float64, so where a sample point lies within an fp32 ulp of a texel edge the two bilinear
+    # slopes differ -- the coordinate gradients (means, scales, quats) are compared on the 2DGS scene only
+    (3000, ("rgbs", "opacities", "texture", "centers")),
+])
+def test_world_space_ray_restatement_gradients_match_oracle(n_texels, keys):
+    """The oracle's fp64 autograd (of the kernels' formulation) against autograd of the world-space restatement, for
+    the same upstream gradients, both in float64: equal to 1e-10 of each gradient's largest element."""
+    from helpers import DIFF, upstream
+
+    case = make_case(n=60, n_texels=n_texels, H=32, W=32, seed=21)
+    inp = case.inp
+    mine = {k: getattr(inp, k).detach().clone().double().requires_grad_(True) for k in DIFF}
+    theirs = {k: getattr(inp, k).detach().clone().double().requires_grad_(True) for k in DIFF}
+    for k, t in theirs.items():
+        setattr(inp, k, t)
+    _, o64, aux = O.rasterize(inp)
+    up = upstream(32, 32, case.C, 5, aux["margin"] < FLIP_MARGIN)
+    names = ("img", "alpha", "depth", "tex", "normal")
+    sum((o64[k] * up[k].double()).sum() for k in names).backward()
+    ref = ray_render_torch(inp, mine)
+    sum((ref[k] * up[k].double()).sum() for k in names).backward()
+    for k in names:
+        assert float((ref[k] - o64[k]).detach().abs().max()) < 1e-10, k
+    for k in keys:
+        g, r = theirs[k].grad, mine[k].grad
+        scale = float(r.abs().max())
+        assert scale > 0, k
+        assert float((g - r).abs().max()) <= 1e-10 * scale, f"{k}: {float((g - r).abs().max()):.3e} vs {scale:.3e}"
