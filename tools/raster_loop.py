@@ -76,7 +76,7 @@ def main():
         names = ["units", "visits", "visits_any", "contrib_lanes", "flush_passes", "tail_lanes", "flushed_entries", "tex_visits",
                  "fwd_candidates", "fwd_cull_pass", "fwd_visits", "fwd_visits_any", "fwd_contrib_lanes",
                  "bwd_alive_lanes", "bwd_visits_le16", "bwd_visits_ge48", "disjoint_runs", "disjoint_runs_le2",
-                 "disjoint_runs_le4", "dense_passes", "half_visits_contrib"]
+                 "disjoint_runs_le4", "dense_passes", "half_visits_contrib", "merged_passes", "merge_disjoint"]
         if os.environ.get("GSTEX_STATS_PHASES"):  # GSTEX_STATS=2: wave-clock sums per backward phase
             names = ["load+barrier", "place+cull", "visits", "barrier_pre_combine", "combine+flush", "barrier_end",
                      "prologue", "-"]
