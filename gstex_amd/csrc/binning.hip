@@ -474,11 +474,13 @@ constexpr unsigned kOrderTileBits = 14;
 constexpr unsigned kOrderMaxCount = (1u << (32 - kOrderTileBits)) - 1;
 
 // Tile order by ranking: tile t goes to position #{tiles u : key_u < key_t} (keys are unique: the tile index is
-// in the low bits).  Each 256-thread workgroup ranks 256 tiles against all keys, staged through LDS in chunks
-// and read as broadcast 16-B vectors: O(n^2) compares spread over the whole chip instead of a bitonic sort
-// in one workgroup (78 barrier-separated stages for 2 500 tiles).
-constexpr int kRankThreads = 256;
-constexpr int kRankTiles = 64;  // tiles per workgroup; the 4 waves each compare against a quarter of the keys
+// in the low bits).  Each workgroup ranks 64 tiles against all keys, staged through LDS in chunks and read as
+// broadcast 16-B vectors, its 16 waves each comparing against a sixteenth of the keys: O(n^2) compares spread over
+// the whole chip instead of a bitonic sort in one workgroup (78 barrier-separated stages for 2 500 tiles), and a
+// short serial chain of LDS reads per wave (4 waves with a quarter each: 9.4 us at cfg3).
+constexpr int kRankThreads = 1024;
+constexpr int kRankParts = kRankThreads / 64;
+constexpr int kRankTiles = 64;  // tiles per workgroup (one per lane)
 constexpr int kRankChunk = 4096;
 
 // Sort keys, all unique (the item index sits in the low bits), ascending = launch order:
@@ -495,7 +497,7 @@ template <int SRC>
 __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, const int32_t* __restrict__ tile_ranges,
                                                                  int32_t* __restrict__ tile_order) {
     __shared__ uint4 s_key[kRankChunk / 4];
-    __shared__ int s_rank[4][kRankTiles];
+    __shared__ int s_rank[kRankParts][kRankTiles];
     unsigned* s_k = reinterpret_cast<unsigned*>(s_key);
     const int part = threadIdx.x >> 6;
     const int t = blockIdx.x * kRankTiles + (threadIdx.x & 63);
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, co
             s_k[i] = i < cn ? order_key<SRC>(tile_ranges, c0 + i) : ~0u;  // padding never ranks below a key
         __syncthreads();
         const int nv = (cn + 3) >> 2;
-        const int q0 = (nv * part) >> 2, q1 = (nv * (part + 1)) >> 2;
+        const int q0 = nv * part / kRankParts, q1 = nv * (part + 1) / kRankParts;
         for (int i = q0; i < q1; ++i) {
             const uint4 k = s_key[i];
             rank += (int)(k.x < mine) + (int)(k.y < mine) + (int)(k.z < mine) + (int)(k.w < mine);
@@ -516,8 +518,12 @@ __global__ __launch_bounds__(kRankThreads) void tile_rank_kernel(int n_tiles, co
     }
     s_rank[part][threadIdx.x & 63] = rank;
     __syncthreads();
-    if (part == 0 && t < n_tiles)
-        tile_order[s_rank[0][threadIdx.x] + s_rank[1][threadIdx.x] + s_rank[2][threadIdx.x] + s_rank[3][threadIdx.x]] = t;
+    if (part == 0 && t < n_tiles) {
+        int r = 0;
+#pragma unroll
+        for (int p = 0; p < kRankParts; ++p) r += s_rank[p][threadIdx.x];
+        tile_order[r] = t;
+    }
 }
 
 __global__ void iota_kernel(int n, int32_t* __restrict__ out) {
@@ -722,8 +728,8 @@ extern "C" int gstex_tile_order(int32_t n_tiles, const int32_t* tile_ranges, int
 #define GSTEX_UNITS_PER_BLOCK 1024  // measured: 4096 17.5 us, 2048 12.6, 1024 10.3 (unit scatter at cfg3)
 #endif
 constexpr int kUnitsPerBlock = GSTEX_UNITS_PER_BLOCK;
-// scratch (int32): [0, 8192) histogram, [8192, 16384) group-interleaved starts, [16384, 24576) plain starts,
-// [24576] mode (1 = group-interleaved)
+// scratch (int32): [0, 8192) histogram, [8192, 16384) per-bin placement counters (both zeroed by the caller), the rest
+// spare
 constexpr int kUnitScratch = 3 * kUnitBins + 16;
 
 __global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __restrict__ key,
@@ -741,13 +747,22 @@ __global__ __launch_bounds__(256) void unit_hist_kernel(int n, const int32_t* __
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
-__global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int n, int32_t* __restrict__ ws) {
-    // thread t = bucket t: per group, the exclusive scan of its buckets (costliest first) -> the group-interleaved
-    // starts; over all groups (bucket-major, group-minor) -> the plain starts.  The 9 scans run together: wave
-    // scans, then one exchange of the 16 wave totals.
+// The counting sort's scan and scatter in one launch (round 6; the two launches took 8.4 + 9.9 us at cfg3): every
+// workgroup scans the whole histogram itself (8192 bins from L2; cheaper than a launch and its latency), thread t =
+// bucket t: per group, the exclusive scan of its buckets (costliest first) -> the group-interleaved starts; over all
+// groups (bucket-major, group-minor) -> the plain starts; then it reserves one range per bin it touches by an atomic
+// on a zeroed counter (scratch[kUnitBins, 2 kUnitBins)) and places its units (one per thread).
+static_assert(kUnitsPerBlock == kUnitBuckets, "one unit per thread of the placing workgroup");
+__global__ __launch_bounds__(kUnitBuckets) void unit_place_kernel(int n, const int32_t* __restrict__ key,
+                                                                  int32_t* __restrict__ ws, int32_t* __restrict__ order,
+                                                                  int bias) {
     constexpr int NV = kUnitGroups + 1, NW = kUnitBuckets / 64;
     __shared__ int s_tot[NW][NV];
+    __shared__ int s_start[kUnitBins];
+    __shared__ int s_h[kUnitBins];
+    __shared__ int s_grouped;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    for (int i = t; i < kUnitBins; i += kUnitBuckets) s_h[i] = 0;
     int h[NV], x[NV];
     h[kUnitGroups] = 0;
 #pragma unroll
@@ -767,47 +782,33 @@ __global__ __launch_bounds__(kUnitBuckets) void unit_scan_kernel(int n, int32_t*
         for (int w = 0; w < wave; ++w) off += s_tot[w][i];
         x[i] += off - h[i];  // exclusive
     }
-#pragma unroll
-    for (int g = 0; g < kUnitGroups; ++g) ws[kUnitBins + g * kUnitBuckets + t] = x[g];
-    int run = x[kUnitGroups];
-#pragma unroll
-    for (int g = 0; g < kUnitGroups; ++g) {
-        ws[2 * kUnitBins + g * kUnitBuckets + t] = run;
-        run += h[g];
-    }
-    if (t == 0) {
+    if (t == 0) {  // group-interleaved only if no group is longer than n / kUnitGroups
         int mx = 0;
         for (int g = 0; g < kUnitGroups; ++g) {
             int len = 0;
             for (int w = 0; w < NW; ++w) len += s_tot[w][g];
             mx = max(mx, len);
         }
-        ws[3 * kUnitBins] = (long long)kUnitGroups * mx <= (long long)n ? 1 : 0;
-    }
-}
-
-__global__ __launch_bounds__(256) void unit_scatter_kernel(int n, const int32_t* __restrict__ key,
-                                                           int32_t* __restrict__ ws, int32_t* __restrict__ order,
-                                                           int bias) {
-    __shared__ int s_h[kUnitBins];
-    const bool grouped = ws[3 * kUnitBins] != 0;
-    int32_t* next = ws + (grouped ? kUnitBins : 2 * kUnitBins);
-    for (int i = threadIdx.x; i < kUnitBins; i += 256) s_h[i] = 0;
-    __syncthreads();
-    const int u0 = blockIdx.x * kUnitsPerBlock;
-    const int u1 = min(n, u0 + kUnitsPerBlock);
-    for (int u = u0 + threadIdx.x; u < u1; u += 256) {
-        const int k = key[u];
-        if (k & 0xFFFFFF) atomicAdd(&s_h[unit_bin(k)], 1);
+        s_grouped = (long long)kUnitGroups * mx <= (long long)n ? 1 : 0;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kUnitBins; i += 256)
-        if (s_h[i]) s_h[i] = atomicAdd(&next[i], s_h[i]);  // this workgroup's range start in bin i
+    const bool grouped = s_grouped != 0;
+    int run = x[kUnitGroups];
+#pragma unroll
+    for (int g = 0; g < kUnitGroups; ++g) {
+        s_start[g * kUnitBuckets + t] = grouped ? x[g] : run;
+        run += h[g];
+    }
+    const int u = blockIdx.x * kUnitBuckets + t;
+    const int k = u < n ? key[u] : 0;
+    const int b = (k & 0xFFFFFF) ? unit_bin(k) : -1;
+    if (b >= 0) atomicAdd(&s_h[b], 1);
     __syncthreads();
-    for (int u = u0 + threadIdx.x; u < u1; u += 256) {
-        const int k = key[u];
-        if (!(k & 0xFFFFFF)) continue;
-        const int b = unit_bin(k);
+    int32_t* cnt = ws + kUnitBins;
+    for (int i = t; i < kUnitBins; i += kUnitBuckets)
+        if (s_h[i]) s_h[i] = s_start[i] + atomicAdd(&cnt[i], s_h[i]);  // this workgroup's range start in bin i
+    __syncthreads();
+    if (b >= 0) {
         const int r = atomicAdd(&s_h[b], 1);
         order[grouped ? kUnitGroups * r + b / kUnitBuckets : r] = u + bias;
     }
@@ -821,13 +822,12 @@ extern "C" int gstex_unit_order(int32_t n_units, const int32_t* unit_key, int32_
     if (n_units == 0) return GSTEX_OK;
     GSTEX_REQUIRE(unit_key && unit_order && scratch, "gstex_unit_order: null pointer");
     hipStream_t st = as_stream(stream);
-    if (hipMemsetAsync(scratch, 0, kUnitBins * sizeof(int32_t), st) != hipSuccess ||
+    if (hipMemsetAsync(scratch, 0, 2 * kUnitBins * sizeof(int32_t), st) != hipSuccess ||
         hipMemsetAsync(unit_order, 0xFF, (size_t)n_units * sizeof(int32_t), st) != hipSuccess)
         return launch_status("gstex_unit_order");
     const int nb = div_up(n_units, kUnitsPerBlock);
     unit_hist_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch);
-    unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(n_units, scratch);
-    unit_scatter_kernel<<<nb, 256, 0, st>>>(n_units, unit_key, scratch, unit_order, 0);
+    unit_place_kernel<<<nb, kUnitBuckets, 0, st>>>(n_units, unit_key, scratch, unit_order, 0);
     return launch_status("gstex_unit_order");
 }
 
@@ -835,8 +835,7 @@ namespace gstex {
 int unit_order_from_hist(int32_t n_units, const int32_t* unit_key, int32_t* unit_order, int32_t* scratch,
                          hipStream_t st) {
     if (n_units <= 0) return GSTEX_OK;
-    unit_scan_kernel<<<1, kUnitBuckets, 0, st>>>(n_units, scratch);
-    unit_scatter_kernel<<<div_up(n_units, kUnitsPerBlock), 256, 0, st>>>(n_units, unit_key, scratch, unit_order, 1);
+    unit_place_kernel<<<div_up(n_units, kUnitsPerBlock), kUnitBuckets, 0, st>>>(n_units, unit_key, scratch, unit_order, 1);
     return launch_status("unit_order_from_hist");
 }
 }  // namespace gstex

@@ -417,7 +417,8 @@ __device__ __forceinline__ int unit_bin(int key) {
     return g * kUnitBuckets + (kUnitBuckets - 1 - min(c, kUnitBuckets - 1));
 }
 // Internal entry (binning.hip) for the raster backward: the order from a histogram the forward already built in
-// scratch[0, kUnitBins); order[] entries are unit + 1 (0 = no unit at that launch position; the caller zeroed it).
+// scratch[0, kUnitBins) (scratch[kUnitBins, 2 kUnitBins) zeroed with it: the placement counters); order[] entries are
+// unit + 1 (0 = no unit at that launch position; the caller zeroed it).
 int unit_order_from_hist(int32_t n_units, const int32_t* unit_key, int32_t* unit_order, int32_t* scratch,
                          hipStream_t st);
 

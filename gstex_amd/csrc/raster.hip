@@ -1752,7 +1752,7 @@ __global__ __launch_bounds__(kEpiBlock) void train_epilogue_kernel(
 namespace gstex {
 ZeroSpan raster_aux_zero_span(void* aux, int64_t n_isect, int32_t n_tiles, int32_t channels) {
     const AuxLayout al = aux_layout(n_isect, n_tiles, channels);
-    return ZeroSpan{aux ? (char*)aux + al.cost : nullptr, al.order_ws - al.cost + (size_t)kUnitBins * 4};
+    return ZeroSpan{aux ? (char*)aux + al.cost : nullptr, al.order_ws - al.cost + (size_t)2 * kUnitBins * 4};
 }
 }  // namespace gstex
 
@@ -1817,7 +1817,7 @@ extern "C" int gstex_raster_fwd_zero(const gstex_camera* cam, int32_t channels, 
     // one fill: unit costs (units the forward never reaches keep 0; the backward skips them), the launch order
     // (0 = no unit at that position) and the unit-order histogram the forward builds (contiguous in the layout)
     if (aux && !(settings & GSTEX_SETTING_AUX_ZEROED) &&
-        hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)kUnitBins * 4, st) != hipSuccess)
+        hipMemsetAsync(ap.cost, 0, al.order_ws - al.cost + (size_t)2 * kUnitBins * 4, st) != hipSuccess)
         return launch_status("gstex_raster_fwd (aux)");
     settings &= ~GSTEX_SETTING_AUX_ZEROED;
     ZeroBufs zbuf;
