@@ -230,9 +230,27 @@ __global__ __launch_bounds__(256) void count_lds_kernel(int n, const float* __re
     }
     __syncthreads();
     // one global range per touched tile; s_hist[t] becomes the range's start inside the tile's bucket
-    for (int t = threadIdx.x; t < n_tiles; t += 256) {
-        const int c = s_hist[t];
-        if (c > 0) s_hist[t] = atomicAdd(&tile_count[t], c);
+    // the workgroups start their reservations at different tiles (a rotation of the tile range per workgroup), so at
+    // any moment they hit different counters instead of all queueing on the same 256, and each thread issues its
+    // returning atomics in groups of 8 before it waits for them (28.0 -> 25.9 us at cfg3)
+    {
+        const int rot = (int)(((long long)blockIdx.x * 977) % (n_tiles > 0 ? n_tiles : 1));
+        for (int i0 = threadIdx.x; i0 < n_tiles; i0 += 256 * 8) {
+            int tt[8], cc[8], rr[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + 256 * k;
+                int t = i + rot;
+                t = t >= n_tiles ? t - n_tiles : t;
+                tt[k] = i < n_tiles ? t : -1;
+                cc[k] = tt[k] >= 0 ? s_hist[t] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rr[k] = cc[k] > 0 ? atomicAdd(&tile_count[tt[k]], cc[k]) : 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (cc[k] > 0) s_hist[tt[k]] = rr[k];
+        }
     }
     __syncthreads();
 #pragma unroll
