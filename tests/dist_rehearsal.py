@@ -257,6 +257,12 @@ def main():
         line = f"{name:14s} every rank == rank 0: {same}"
         if rank == 0:
             rp = dict(zip(free.param_groups(), free.parameters()))[name].detach()
+            if rp.shape != r0.shape:
+                # the free-running reference recharted from its own parameters, which differ from rank 0's by float
+                # rounding (order of the float atomics): a splat whose chart size is an integer step function of its
+                # scale can land on the other side of a step, so the texel stores differ in length -- reported only
+                say(line + f";  free-running reference recharted to {tuple(rp.shape)} vs {tuple(r0.shape)} (not compared)")
+                continue
             scale = max(float(rp.abs().max()), 1e-30)
             d = (r0 - rp).abs()
             lr = free.optimizer.param_groups[names.index(name)]["lr"]
