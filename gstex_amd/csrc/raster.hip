@@ -573,6 +573,9 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
     constexpr int kStep = kFwdBatch, kWords = kStep / 64;
     __shared__ float4 s_rec[kRecF4 * kFwdBatch];
     __shared__ int s_gid[kFwdBatch];  // the batch's splat ids (the near-edge-on splats' fp64 rows are read by id)
+    // the next batch's ids, copied global -> LDS (no VGPR) during the current batch's visits, so the batch staging's
+    // record loads do not wait on a dependent id load first (raster loop at cfg3: forward 0.510 vs 0.5155 ms)
+    __shared__ int s_gid_next[kFwdBatch];
     const int ti = (int)blockIdx.x;
     const int tile = tile_order ? tile_order[ti] : ti;  // largest-first when given
     const int tx = tile % tiles_x, ty = tile / tiles_x;
@@ -659,6 +662,7 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         }
     };
 
+    if (tid < kFwdBatch && rng.x + tid < rng.y) s_gid_next[tid] = sorted_ids[rng.x + tid];  // the first batch's
     for (int b0 = rng.x; b0 < rng.y; b0 += kStep) {
         if (aux.cost && b0 > rng.x && (b0 - rng.x) % kSegLen == 0) {
             // segment cur_seg complete: its cost, and the state after it while a lane of the wave still runs
@@ -678,12 +682,16 @@ __global__ __launch_bounds__(kThreads, GSTEX_FWD_OCC) void raster_fwd_kernel(
         for (int q = tid; q < kFwdBatch * kRecF4; q += kThreads) {
             const int j = q / kRecF4, k = q % kRecF4;
             if (b0 + j < rng.y) {
-                const int gid = sorted_ids[b0 + j];
+                const int gid = s_gid_next[j];
                 s_rec[k * kFwdBatch + j] = records[(size_t)gid * kRecF4 + k];
                 if (k == 0) s_gid[j] = gid;
             }
         }
         __syncthreads();
+        if (tid < kFwdBatch && b0 + kStep < rng.y) {  // waves 0-1: lane l of wave w fetches id kStep + 64 w + l ahead
+            const int nx = min(b0 + kStep + tid, rng.y - 1);  // (past the list: a valid address, value unused)
+            __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(sorted_ids + nx), s_gid_next + (tid & ~63), 4, 0, 0);
+        }
         // the batch splats whose contribution region meets this wave's 8x8 block, tested all at once
         unsigned long long todo[kWords];
 #pragma unroll
