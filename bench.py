@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_TAG = "r06c"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
+PROFILE_TAG = "r06d"  # profiles/<tag>_traffic.json: PMC HBM bytes per launch (tools/profile_bench.sh)
 N_POSES = 8
 
 
